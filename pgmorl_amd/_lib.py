@@ -1,0 +1,112 @@
+"""ctypes binding of libpgm.so (include/pgm_abi.h).
+
+torch is imported first so that the HIP runtime torch ships (same soname libamdhip64.so.7)
+is the one libpgm.so binds to: device pointers and streams are then shared.
+There is no fallback: if the library is missing or fails to load, every op raises.
+"""
+import ctypes as C
+import os
+
+import torch  # noqa: F401  (must precede loading libpgm.so)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, 'libpgm.so')
+
+PGM_ABI_VERSION = 1
+PGM_OK, PGM_E_INVALID_ARG, PGM_E_SHAPE, PGM_E_HIP, PGM_E_UNSUPPORTED = 0, -1, -2, -3, -4
+PARAM_TENSORS = ['actor_w1', 'actor_b1', 'actor_w2', 'actor_b2', 'critic_w1', 'critic_b1', 'critic_w2',
+                 'critic_b2', 'value_w', 'value_b', 'mean_w', 'mean_b', 'logstd']
+
+P_ = C.c_void_p
+I32 = C.c_int32
+F32 = C.c_float
+F64 = C.c_double
+
+
+class Dims(C.Structure):
+    _fields_ = [(n, I32) for n in ('P', 'N', 'T', 'O', 'A', 'K', 'H')]
+
+
+class EnvSpec(C.Structure):
+    _fields_ = [('d', P_), ('U', P_), ('c', P_), ('V', P_), ('ebase', P_), ('ecoef', P_), ('act_lo', P_),
+                ('act_hi', P_), ('max_episode_steps', I32), ('_pad', I32)]
+
+
+class EnvState(C.Structure):
+    _fields_ = [('s', P_), ('elapsed', P_), ('obj_acc', P_), ('obj_acc_valid', P_), ('ret', P_), ('s0', P_)]
+
+
+class NormState(C.Structure):
+    _fields_ = [('ob_mean', P_), ('ob_var', P_), ('ob_count', P_), ('ret_mean', P_), ('ret_var', P_),
+                ('ret_count', P_), ('obj_mean', P_), ('obj_var', P_), ('obj_count', P_), ('gamma', F64),
+                ('clipob', F64), ('cliprew', F64), ('epsilon', F64), ('use_ob_rms', I32), ('use_obj_rms', I32)]
+
+
+class RolloutBuf(C.Structure):
+    _fields_ = [(n, P_) for n in ('obs', 'actions', 'logp', 'values', 'rewards', 'masks', 'bad_masks',
+                                  'returns', 'adv')]
+
+
+class PPOHParams(C.Structure):
+    _fields_ = [('clip_param', F32), ('value_loss_coef', F32), ('entropy_coef', F32), ('max_grad_norm', F32),
+                ('adam_eps', F32), ('beta1', F32), ('beta2', F32), ('_pad', F32), ('ppo_epoch', I32),
+                ('num_mini_batch', I32), ('use_clipped_value_loss', I32), ('_pad2', I32)]
+
+
+_SIGS = {
+    'pgm_abi_version': (C.c_int, []),
+    'pgm_last_error': (C.c_char_p, []),
+    'pgm_param_layout': (C.c_int, [I32, I32, I32, I32, C.POINTER(I32), C.POINTER(I32)]),
+    'pgm_act_forward': (C.c_int, [C.POINTER(Dims), P_, P_, P_, I32, P_, P_, P_, P_]),
+    'pgm_env_reset': (C.c_int, [C.POINTER(Dims), C.POINTER(EnvSpec), C.POINTER(EnvState), C.POINTER(NormState),
+                                P_, P_]),
+    'pgm_env_step': (C.c_int, [C.POINTER(Dims), C.POINTER(EnvSpec), C.POINTER(EnvState), C.POINTER(NormState),
+                               P_, P_, P_, P_, P_, P_]),
+    'pgm_rollout': (C.c_int, [C.POINTER(Dims), P_, C.POINTER(EnvSpec), C.POINTER(EnvState), C.POINTER(NormState),
+                              C.POINTER(RolloutBuf), P_, C.c_uint64, I32, P_]),
+    'pgm_gae': (C.c_int, [C.POINTER(Dims), C.POINTER(RolloutBuf), F32, F32, I32, I32, P_]),
+    'pgm_adv_normalize': (C.c_int, [C.POINTER(Dims), C.POINTER(RolloutBuf), P_, P_, P_]),
+    'pgm_ppo_update': (C.c_int, [C.POINTER(Dims), C.POINTER(PPOHParams), P_, P_, P_, P_, P_, P_,
+                                 C.POINTER(RolloutBuf), P_, P_]),
+    'pgm_eval': (C.c_int, [C.POINTER(Dims), P_, C.POINTER(EnvSpec), P_, P_, P_, I32, I32, I32, F64, P_, P_]),
+    'pgm_randperm': (C.c_int, [I32, I32, C.c_uint64, P_, P_]),
+    'pgm_normal_noise': (C.c_int, [C.c_int64, C.c_uint64, P_, P_]),
+}
+
+EXPORTS = tuple(_SIGS)
+
+_lib = None
+
+
+class PGMError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libpgm.so once (raises if it is missing: there is no CPU fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise PGMError(f'{LIB_PATH} not built; run `python -m pgmorl_amd.build` (hipcc, gfx950)')
+        h = C.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            f = getattr(h, name)
+            f.restype, f.argtypes = res, args
+        if h.pgm_abi_version() != PGM_ABI_VERSION:
+            raise PGMError(f'libpgm ABI {h.pgm_abi_version()} != {PGM_ABI_VERSION}')
+        _lib = h
+    return _lib
+
+
+def check(rc, what):
+    if rc != PGM_OK:
+        msg = lib().pgm_last_error().decode(errors='replace')
+        raise PGMError(f'{what} failed ({rc}): {msg}')
+
+
+def param_layout(O, A, K, H=64):
+    """(offsets dict, total) of the flat per-task parameter vector (pgm_param_layout)."""
+    offs = (I32 * 13)()
+    tot = I32()
+    check(lib().pgm_param_layout(O, A, K, H, offs, C.byref(tot)), 'pgm_param_layout')
+    return dict(zip(PARAM_TENSORS, list(offs))), tot.value

@@ -1,0 +1,61 @@
+"""Build libpgm.so (gfx950) in-tree with hipcc.  ``python -m pgmorl_amd.build``."""
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, 'csrc')
+ROOT = os.path.dirname(HERE)
+LIB = os.path.join(HERE, 'libpgm.so')
+OBJDIR = os.path.join(HERE, 'build')
+SOURCES = ['pgm_abi.cpp', 'pgm_policy_env.hip', 'pgm_misc.hip', 'pgm_ppo_update.hip']
+HEADERS = ['pgm_common.hpp', 'pgm_dispatch.hpp']
+ARCH = os.environ.get('PGM_OFFLOAD_ARCH', 'gfx950')
+FLAGS = ['-O3', '-std=c++17', '-fPIC', f'--offload-arch={ARCH}', '-I', os.path.join(ROOT, 'include')]
+
+
+def _hipcc():
+    for cand in (os.environ.get('HIPCC'), '/opt/rocm/bin/hipcc', 'hipcc'):
+        if cand and (os.path.isabs(cand) and os.path.exists(cand) or not os.path.isabs(cand)):
+            return cand
+    return 'hipcc'
+
+
+def _newest(paths):
+    return max(os.path.getmtime(p) for p in paths)
+
+
+def build(force=False, verbose=False):
+    os.makedirs(OBJDIR, exist_ok=True)
+    deps = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(ROOT, 'include', 'pgm_abi.h')]
+    dep_t = _newest(deps)
+    hipcc = _hipcc()
+
+    def compile_one(src):
+        s = os.path.join(CSRC, src)
+        o = os.path.join(OBJDIR, src + '.o')
+        if not force and os.path.exists(o) and os.path.getmtime(o) >= max(os.path.getmtime(s), dep_t):
+            return o
+        cmd = [hipcc, *FLAGS, '-c', s, '-o', o]
+        if verbose:
+            print(' '.join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f'hipcc failed on {src}:\n{r.stdout}\n{r.stderr}')
+        return o
+
+    with ThreadPoolExecutor(max_workers=min(4, len(SOURCES))) as ex:
+        objs = list(ex.map(compile_one, SOURCES))
+    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < _newest(objs):
+        cmd = [hipcc, f'--offload-arch={ARCH}', '-shared', '-fPIC', *objs, '-o', LIB]
+        if verbose:
+            print(' '.join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f'hipcc link failed:\n{r.stdout}\n{r.stderr}')
+    return LIB
+
+
+if __name__ == '__main__':
+    print(build(force='--force' in sys.argv, verbose=True))

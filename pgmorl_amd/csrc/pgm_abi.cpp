@@ -1,0 +1,67 @@
+// Host plumbing of the C ABI: version, thread-local error string, parameter layout.
+#include <stdarg.h>
+#include <stdio.h>
+
+#include "pgm_common.hpp"
+
+namespace pgm {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    set_error("%s: %s", what, hipGetErrorString(e));
+    return PGM_E_HIP;
+}
+
+int launch_status(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, what);
+    return PGM_OK;
+}
+
+static inline int32_t round_up(int32_t x, int32_t m) { return (x + m - 1) / m * m; }
+
+Layout make_layout(int O, int A, int K, int Hd) {
+    const int32_t sizes[PGM_NUM_PARAM_TENSORS] = {
+        O * Hd, Hd, Hd * Hd, Hd,   // actor tower
+        O * Hd, Hd, Hd * Hd, Hd,   // critic tower
+        Hd * K, K,                 // critic_linear
+        Hd * A, A,                 // fc_mean
+        A};                        // logstd
+    Layout L;
+    int32_t p = 0;
+    for (int i = 0; i < PGM_NUM_PARAM_TENSORS; ++i) {
+        L.off[i] = p;
+        p = round_up(p + sizes[i], 4);  // 16-byte aligned tensors
+    }
+    L.total = round_up(p, 64);
+    return L;
+}
+
+}  // namespace pgm
+
+extern "C" {
+
+int pgm_abi_version(void) { return PGM_ABI_VERSION; }
+
+const char* pgm_last_error(void) { return pgm::g_err; }
+
+int pgm_param_layout(int32_t O, int32_t A, int32_t K, int32_t H, int32_t* offsets, int32_t* total) {
+    if (O <= 0 || A <= 0 || K <= 0 || H <= 0 || !offsets || !total) {
+        pgm::set_error("pgm_param_layout: bad arguments");
+        return PGM_E_INVALID_ARG;
+    }
+    pgm::Layout L = pgm::make_layout(O, A, K, H);
+    for (int i = 0; i < PGM_NUM_PARAM_TENSORS; ++i) offsets[i] = L.off[i];
+    *total = L.total;
+    return PGM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,721 @@
+// Policy forward, synthetic env + VecNormalize, the fused rollout and the deterministic
+// evaluation.  One workgroup (256 threads) per task; everything a task touches per step lives
+// in LDS, so a T-step rollout is one launch with only workgroup barriers (tasks never interact).
+//
+// Reference semantics (paths relative to the reference tree):
+//   Policy.act / get_value                 a2c_ppo_acktr/model.py:57-73, 237-246
+//   DiagGaussian sample + log_prob         a2c_ppo_acktr/distributions.py:29-40,71-90
+//   DummyVecEnv auto-reset                 baselines/common/vec_env/dummy_vec_env.py:45-56
+//   TimeLimitMask bad_transition           a2c_ppo_acktr/envs.py:122-131
+//   VecNormalize.step_wait / reset         baselines/common/vec_env/vec_normalize.py:29-66
+//   RunningMeanStd Chan merge              baselines/common/running_mean_std.py:3-31
+//   masks / bad_masks / obj_tensor         morl/mopg.py:110-130
+//   RolloutStorage.insert / after_update   a2c_ppo_acktr/storage.py:50-75
+//   evaluation()                           morl/mopg.py:25-46
+#include "pgm_dispatch.hpp"
+
+namespace pgm {
+
+constexpr int NMAX = 8;    // envs per task handled by one workgroup
+constexpr int RT = 256;    // threads per workgroup
+
+template <int O>
+constexpr int opad() { return (O + 3) & ~3; }
+template <int O>
+constexpr bool w1_in_lds() { return O <= 128; }
+
+// ------------------------------------------------------------------------------------------
+// LDS images
+template <int O, int A, int K>
+struct PolSmem {
+    float W1t[w1_in_lds<O>() ? O : 1][H2];  // [in][col]: col < H critic tower, col >= H actor tower
+    float b1[H2];
+    float W2t[2][H][H];                     // [tower 0=critic,1=actor][in][out]
+    float b2[H2];
+    float Wv[H][K];
+    float bv[K];
+    float Wm[H][A];
+    float bm[A];
+    float logstd[A];
+    float x[NMAX][opad<O>()];               // fp32 policy input rows
+    float h1[NMAX][H2];
+    float h2[NMAX][H2];
+    float val[NMAX][K];
+    float mu[NMAX][A];
+    float lp[NMAX][A];
+};
+
+template <int O, int A, int K>
+struct EnvSmem {
+    double s[NMAX][O];        // env state
+    double snew[NMAX][O];     // observation returned by step (post auto-reset)
+    double ac[NMAX][A];       // clipped action
+    double objraw[NMAX][K];   // info['obj'] before obj_rms scaling
+    double obj_acc[NMAX][K];  // VecNormalize.obj
+    double ret[NMAX];         // VecNormalize.ret
+    double ob_mean[O], ob_var[O];
+    double obj_mean[K], obj_var[K];
+    double ob_count, obj_count, ret_mean, ret_var, ret_count;
+    double objsum[K];         // evaluation accumulator
+    int elapsed[NMAX], done[NMAX], bad[NMAX];
+    int obj_valid;
+};
+
+struct NormCfg {
+    double gamma, clipob, cliprew, eps;
+    int use_ob, use_obj;
+};
+__host__ __device__ inline NormCfg norm_cfg(const pgm_norm_state& ns) {
+    return NormCfg{ns.gamma, ns.clipob, ns.cliprew, ns.epsilon, ns.use_ob_rms, ns.use_obj_rms};
+}
+
+// ------------------------------------------------------------------------------------------
+// policy
+template <int O, int A, int K>
+__device__ void load_policy(PolSmem<O, A, K>& S, const float* __restrict__ prm, const Layout& L) {
+    const int t = threadIdx.x;
+    if constexpr (w1_in_lds<O>()) {
+        for (int i = t; i < O * H2; i += RT) {
+            const int k = i / H2, c = i % H2;
+            S.W1t[k][c] = prm[(c < H ? L.off[PGM_P_CRITIC_W1] : L.off[PGM_P_ACTOR_W1]) + k * H + (c & (H - 1))];
+        }
+    }
+    for (int c = t; c < H2; c += RT) {
+        S.b1[c] = prm[(c < H ? L.off[PGM_P_CRITIC_B1] : L.off[PGM_P_ACTOR_B1]) + (c & (H - 1))];
+        S.b2[c] = prm[(c < H ? L.off[PGM_P_CRITIC_B2] : L.off[PGM_P_ACTOR_B2]) + (c & (H - 1))];
+    }
+    for (int i = t; i < 2 * H * H; i += RT) {
+        const int m = i / (H * H), r = i % (H * H);
+        (&S.W2t[m][0][0])[r] = prm[(m == 0 ? L.off[PGM_P_CRITIC_W2] : L.off[PGM_P_ACTOR_W2]) + r];
+    }
+    for (int i = t; i < H * K; i += RT) (&S.Wv[0][0])[i] = prm[L.off[PGM_P_VALUE_W] + i];
+    for (int i = t; i < H * A; i += RT) (&S.Wm[0][0])[i] = prm[L.off[PGM_P_MEAN_W] + i];
+    if (t < K) S.bv[t] = prm[L.off[PGM_P_VALUE_B] + t];
+    if (t < A) {
+        S.bm[t] = prm[L.off[PGM_P_MEAN_B] + t];
+        S.logstd[t] = prm[L.off[PGM_P_LOGSTD] + t];
+    }
+}
+
+// value [N][K] -> S.val, action mean [N][A] -> S.mu, from S.x.  Ends with a barrier.
+template <int O, int A, int K>
+__device__ void policy_forward(PolSmem<O, A, K>& S, int N, const float* __restrict__ prm, const Layout& L) {
+    const int t = threadIdx.x, c = t & (H2 - 1), rg = t >> 7;
+    constexpr int RPT = NMAX / 2;  // rows per thread
+    {   // tower layer 1
+        float acc[RPT];
+        const float b = S.b1[c];
+#pragma unroll
+        for (int i = 0; i < RPT; ++i) acc[i] = b;
+        const float* gw = prm + (c < H ? L.off[PGM_P_CRITIC_W1] : L.off[PGM_P_ACTOR_W1]) + (c & (H - 1));
+        for (int k = 0; k < O; ++k) {
+            float w;
+            if constexpr (w1_in_lds<O>()) w = S.W1t[k][c];
+            else w = gw[k * H];
+#pragma unroll
+            for (int i = 0; i < RPT; ++i)
+                if (rg + 2 * i < N) acc[i] = fmaf(S.x[rg + 2 * i][k], w, acc[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < RPT; ++i)
+            if (rg + 2 * i < N) S.h1[rg + 2 * i][c] = tanh_f(acc[i]);
+    }
+    __syncthreads();
+    {   // tower layer 2
+        const int m = c >> 6, j = c & (H - 1);
+        float acc[RPT];
+        const float b = S.b2[c];
+#pragma unroll
+        for (int i = 0; i < RPT; ++i) acc[i] = b;
+        for (int k = 0; k < H; ++k) {
+            const float w = S.W2t[m][k][j];
+#pragma unroll
+            for (int i = 0; i < RPT; ++i)
+                if (rg + 2 * i < N) acc[i] = fmaf(S.h1[rg + 2 * i][m * H + k], w, acc[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < RPT; ++i)
+            if (rg + 2 * i < N) S.h2[rg + 2 * i][c] = tanh_f(acc[i]);
+    }
+    __syncthreads();
+    {   // heads: 8 lanes per output dot
+        const int sub = t & 7;
+        const int nout = N * (K + A);
+        for (int o = t >> 3; o < nout; o += RT / 8) {
+            const int r = o / (K + A), q = o % (K + A);
+            float s = 0.f;
+            if (q < K) {
+#pragma unroll
+                for (int hh = 0; hh < 8; ++hh) s = fmaf(S.h2[r][sub * 8 + hh], S.Wv[sub * 8 + hh][q], s);
+            } else {
+#pragma unroll
+                for (int hh = 0; hh < 8; ++hh) s = fmaf(S.h2[r][H + sub * 8 + hh], S.Wm[sub * 8 + hh][q - K], s);
+            }
+            s = group_sum<8>(s);
+            if (sub == 0) {
+                if (q < K) S.val[r][q] = s + S.bv[q];
+                else S.mu[r][q - K] = s + S.bm[q - K];
+            }
+        }
+    }
+    __syncthreads();
+}
+
+// ------------------------------------------------------------------------------------------
+// env
+template <int O, int A, int K>
+__device__ void load_env(EnvSmem<O, A, K>& E, const pgm_env_state& st, const pgm_norm_state& ns, int p, int N) {
+    const int t = threadIdx.x;
+    for (int i = t; i < N * O; i += RT) (&E.s[0][0])[i] = st.s[(size_t)p * N * O + i];
+    for (int i = t; i < N * K; i += RT) E.obj_acc[i / K][i % K] = st.obj_acc[(size_t)p * N * K + i];
+    if (t < N) {
+        E.elapsed[t] = st.elapsed[p * N + t];
+        E.ret[t] = st.ret[p * N + t];
+    }
+    for (int o = t; o < O; o += RT) {
+        E.ob_mean[o] = ns.ob_mean[(size_t)p * O + o];
+        E.ob_var[o] = ns.ob_var[(size_t)p * O + o];
+    }
+    if (t < K) {
+        E.obj_mean[t] = ns.obj_mean[p * K + t];
+        E.obj_var[t] = ns.obj_var[p * K + t];
+    }
+    if (t == 0) {
+        E.ob_count = ns.ob_count[p];
+        E.obj_count = ns.obj_count[p];
+        E.ret_mean = ns.ret_mean[p];
+        E.ret_var = ns.ret_var[p];
+        E.ret_count = ns.ret_count[p];
+        E.obj_valid = st.obj_acc_valid[p];
+    }
+}
+
+template <int O, int A, int K>
+__device__ void store_env(const EnvSmem<O, A, K>& E, const pgm_env_state& st, const pgm_norm_state& ns, int p, int N) {
+    const int t = threadIdx.x;
+    for (int i = t; i < N * O; i += RT) st.s[(size_t)p * N * O + i] = (&E.s[0][0])[i];
+    for (int i = t; i < N * K; i += RT) st.obj_acc[(size_t)p * N * K + i] = E.obj_acc[i / K][i % K];
+    if (t < N) {
+        st.elapsed[p * N + t] = E.elapsed[t];
+        st.ret[p * N + t] = E.ret[t];
+    }
+    for (int o = t; o < O; o += RT) {
+        ns.ob_mean[(size_t)p * O + o] = E.ob_mean[o];
+        ns.ob_var[(size_t)p * O + o] = E.ob_var[o];
+    }
+    if (t < K) {
+        ns.obj_mean[p * K + t] = E.obj_mean[t];
+        ns.obj_var[p * K + t] = E.obj_var[t];
+    }
+    if (t == 0) {
+        ns.ob_count[p] = E.ob_count;
+        ns.obj_count[p] = E.obj_count;
+        ns.ret_mean[p] = E.ret_mean;
+        ns.ret_var[p] = E.ret_var;
+        ns.ret_count[p] = E.ret_count;
+        st.obj_acc_valid[p] = E.obj_valid;
+    }
+}
+
+// Chan merge of a batch (bm, bv, n) into (mean, var, count) -- running_mean_std.py:20-31
+__device__ __forceinline__ void chan_merge(double& mean, double& var, double count, double bm, double bv, double n) {
+    const double delta = bm - mean;
+    const double tot = count + n;
+    const double new_mean = mean + delta * n / tot;
+    const double m2 = var * count + bv * n + delta * delta * count * n / tot;
+    mean = new_mean;
+    var = m2 / tot;
+}
+
+// s' = tanh(d*s + U a_c + c); objectives; time limit; DummyVecEnv auto-reset to s0.
+// Needs E.ac filled and E.s current.  Ends with a barrier.
+template <int O, int A, int K>
+__device__ void env_dynamics(EnvSmem<O, A, K>& E, int N, const pgm_env_spec& sp, const double* __restrict__ s0) {
+    const int t = threadIdx.x;
+    for (int i = t; i < N * O; i += RT) {
+        const int n = i / O, o = i % O;
+        double ua = 0.0;
+#pragma unroll
+        for (int a = 0; a < A; ++a) ua += sp.U[o * A + a] * E.ac[n][a];
+        E.snew[n][o] = tanh(sp.d[o] * E.s[n][o] + ua + sp.c[o]);
+    }
+    __syncthreads();
+    for (int i = t; i < N * K; i += RT) {
+        const int n = i / K, k = i % K;
+        double v = 0.0, e2 = 0.0;
+        for (int o = 0; o < O; ++o) v += sp.V[k * O + o] * E.snew[n][o];
+#pragma unroll
+        for (int a = 0; a < A; ++a) e2 += E.ac[n][a] * E.ac[n][a];
+        E.objraw[n][k] = v + sp.ebase[k] - sp.ecoef[k] * e2;
+    }
+    if (t < N) {
+        const int el = E.elapsed[t] + 1;
+        const int d = el >= sp.max_episode_steps;
+        E.done[t] = d;
+        E.bad[t] = d && (el == sp.max_episode_steps);
+        E.elapsed[t] = d ? 0 : el;
+    }
+    __syncthreads();
+    for (int i = t; i < N * O; i += RT) {
+        const int n = i / O, o = i % O;
+        if (E.done[n]) E.snew[n][o] = s0[n * O + o];
+        E.s[n][o] = E.snew[n][o];
+    }
+    __syncthreads();
+}
+
+// VecNormalize.step_wait statistics (ob_rms, obj accumulators + obj_rms, ret_rms).  Ends with a barrier.
+template <int O, int A, int K>
+__device__ void vecnorm_stats(EnvSmem<O, A, K>& E, int N, const NormCfg& nc) {
+    const int t = threadIdx.x;
+    const double dn = (double)N;
+    if (nc.use_ob) {
+        for (int o = t; o < O; o += RT) {
+            double sum = 0.0;
+            for (int n = 0; n < N; ++n) sum += E.snew[n][o];
+            const double bm = sum / dn;
+            double sq = 0.0;
+            for (int n = 0; n < N; ++n) {
+                const double dd = E.snew[n][o] - bm;
+                sq += dd * dd;
+            }
+            chan_merge(E.ob_mean[o], E.ob_var[o], E.ob_count, bm, sq / dn, dn);
+        }
+    }
+    for (int k = t; k < K; k += RT) {
+        for (int n = 0; n < N; ++n)
+            E.obj_acc[n][k] = E.obj_valid ? E.obj_acc[n][k] * nc.gamma + E.objraw[n][k] : E.objraw[n][k];
+        if (nc.use_obj) {
+            double sum = 0.0;
+            for (int n = 0; n < N; ++n) sum += E.obj_acc[n][k];
+            const double bm = sum / dn;
+            double sq = 0.0;
+            for (int n = 0; n < N; ++n) {
+                const double dd = E.obj_acc[n][k] - bm;
+                sq += dd * dd;
+            }
+            chan_merge(E.obj_mean[k], E.obj_var[k], E.obj_count, bm, sq / dn, dn);
+        }
+    }
+    if (t == RT - 1) {  // ret_rms on the (always zero-reward) discounted return, vec_normalize.py:32,41-43
+        double sum = 0.0;
+        for (int n = 0; n < N; ++n) {
+            E.ret[n] = E.ret[n] * nc.gamma + 0.0;
+            sum += E.ret[n];
+        }
+        const double bm = sum / dn;
+        double sq = 0.0;
+        for (int n = 0; n < N; ++n) sq += (E.ret[n] - bm) * (E.ret[n] - bm);
+        chan_merge(E.ret_mean, E.ret_var, E.ret_count, bm, sq / dn, dn);
+        E.ret_count += dn;
+    }
+    __syncthreads();
+    if (t == 0) {
+        if (nc.use_ob) E.ob_count += dn;
+        if (nc.use_obj) E.obj_count += dn;
+        E.obj_valid = 1;
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ double clipd(double x, double lo, double hi) { return fmin(fmax(x, lo), hi); }
+
+// Writes the normalised fp32 obs (into xs rows and obs_out), scaled objectives, masks; zeroes the
+// accumulators of done envs.  Ends with a barrier.
+template <int O, int A, int K, int XS>
+__device__ void vecnorm_emit(EnvSmem<O, A, K>& E, int N, const NormCfg& nc, float (*xs)[XS], float* obs_out,
+                             float* rew_out, float* mask_out, float* bad_out) {
+    const int t = threadIdx.x;
+    for (int i = t; i < N * O; i += RT) {
+        const int n = i / O, o = i % O;
+        double v = E.snew[n][o];
+        if (nc.use_ob) v = clipd((v - E.ob_mean[o]) / sqrt(E.ob_var[o] + nc.eps), -nc.clipob, nc.clipob);
+        const float f = (float)v;  // VecPyTorch .float() (envs.py:192)
+        xs[n][o] = f;
+        if (obs_out) obs_out[i] = f;
+    }
+    for (int i = t; i < N * K; i += RT) {
+        const int n = i / K, k = i % K;
+        double r = E.objraw[n][k];
+        if (nc.use_obj) r = clipd(r / sqrt(E.obj_var[k] + nc.eps), -nc.cliprew, nc.cliprew);
+        if (rew_out) rew_out[i] = (float)r;
+    }
+    __syncthreads();
+    if (t < N) {
+        if (mask_out) mask_out[t] = E.done[t] ? 0.f : 1.f;
+        if (bad_out) bad_out[t] = E.bad[t] ? 0.f : 1.f;
+        if (E.done[t]) E.ret[t] = 0.0;
+    }
+    for (int i = t; i < N * K; i += RT)
+        if (E.done[i / K]) E.obj_acc[i / K][i % K] = 0.0;
+    __syncthreads();
+}
+
+// ------------------------------------------------------------------------------------------
+// kernels
+template <int O, int A, int K>
+struct StepSmem {
+    PolSmem<O, A, K> pol;
+    EnvSmem<O, A, K> env;
+};
+
+struct ActArgs {
+    int P, N;
+    Layout L;
+    const float* params;
+    const float* obs;
+    const float* noise;
+    int deterministic;
+    float *value, *action, *logp;
+};
+
+template <int O, int A, int K>
+__global__ __launch_bounds__(RT) void act_forward_kernel(ActArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    auto& S = *reinterpret_cast<PolSmem<O, A, K>*>(smem_raw);
+    const int p = blockIdx.x, t = threadIdx.x, N = a.N;
+    const float* prm = a.params + (size_t)p * a.L.total;
+    load_policy(S, prm, a.L);
+    for (int i = t; i < N * O; i += RT) S.x[i / O][i % O] = a.obs[(size_t)p * N * O + i];
+    __syncthreads();
+    policy_forward(S, N, prm, a.L);
+    for (int i = t; i < N * K; i += RT) a.value[(size_t)p * N * K + i] = S.val[i / K][i % K];
+    for (int i = t; i < N * A; i += RT) {
+        const int n = i / A, j = i % A;
+        const float mu = S.mu[n][j], ls = S.logstd[j], sd = expf(ls);
+        const float act = a.deterministic ? mu : fmaf(a.noise[i], sd, mu);
+        const float dz = (act - mu) / sd;
+        S.lp[n][j] = -0.5f * dz * dz - ls - LOG_SQRT_2PI;
+        a.action[(size_t)p * N * A + i] = act;
+    }
+    __syncthreads();
+    if (t < N) {
+        float s = 0.f;
+        for (int j = 0; j < A; ++j) s += S.lp[t][j];
+        a.logp[(size_t)p * N + t] = s;
+    }
+}
+
+struct EnvArgs {
+    int P, N;
+    pgm_env_spec spec;
+    pgm_env_state st;
+    pgm_norm_state ns;
+    const float* action;
+    float *obs_out, *rew_out, *mask_out, *bad_out;
+    int reset;
+};
+
+template <int O, int A, int K>
+__global__ __launch_bounds__(RT) void env_kernel(EnvArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    auto& S = *reinterpret_cast<StepSmem<O, A, K>*>(smem_raw);
+    auto& E = S.env;
+    const int p = blockIdx.x, t = threadIdx.x, N = a.N;
+    const NormCfg nc = norm_cfg(a.ns);
+    load_env(E, a.st, a.ns, p, N);
+    __syncthreads();
+    if (a.reset) {  // fresh make_vec_envs + reset(): vec_normalize.py:10-27,63-66
+        for (int i = t; i < N * O; i += RT) {
+            const double v = a.st.s0[i];
+            (&E.s[0][0])[i] = v;
+            (&E.snew[0][0])[i] = v;
+        }
+        if (t < N) {
+            E.elapsed[t] = 0;
+            E.ret[t] = 0.0;
+        }
+        if (t == 0) E.obj_valid = 0;
+        __syncthreads();
+        if (nc.use_ob) {
+            const double dn = (double)N;
+            for (int o = t; o < O; o += RT) {
+                double sum = 0.0;
+                for (int n = 0; n < N; ++n) sum += E.snew[n][o];
+                const double bm = sum / dn;
+                double sq = 0.0;
+                for (int n = 0; n < N; ++n) sq += (E.snew[n][o] - bm) * (E.snew[n][o] - bm);
+                chan_merge(E.ob_mean[o], E.ob_var[o], E.ob_count, bm, sq / dn, dn);
+            }
+            __syncthreads();
+            if (t == 0) E.ob_count += dn;
+            __syncthreads();
+        }
+        for (int i = t; i < N * O; i += RT) {
+            const int o = i % O;
+            double v = (&E.snew[0][0])[i];
+            if (nc.use_ob) v = clipd((v - E.ob_mean[o]) / sqrt(E.ob_var[o] + nc.eps), -nc.clipob, nc.clipob);
+            a.obs_out[(size_t)p * N * O + i] = (float)v;
+        }
+    } else {
+        for (int i = t; i < N * A; i += RT) {
+            const int j = i % A;
+            E.ac[i / A][j] = clipd((double)a.action[(size_t)p * N * A + i], a.spec.act_lo[j], a.spec.act_hi[j]);
+        }
+        __syncthreads();
+        env_dynamics(E, N, a.spec, a.st.s0);
+        vecnorm_stats(E, N, nc);
+        vecnorm_emit<O, A, K, opad<O>()>(E, N, nc, S.pol.x, a.obs_out + (size_t)p * N * O,
+                                         a.rew_out + (size_t)p * N * K, a.mask_out + (size_t)p * N,
+                                         a.bad_out + (size_t)p * N);
+    }
+    __syncthreads();
+    store_env(E, a.st, a.ns, p, N);
+}
+
+struct RolloutArgs {
+    int P, N, T;
+    Layout L;
+    const float* params;
+    pgm_env_spec spec;
+    pgm_env_state st;
+    pgm_norm_state ns;
+    pgm_rollout_buf rb;
+    const float* noise;
+    uint64_t seed;
+    int carry;
+};
+
+template <int O, int A, int K>
+__global__ __launch_bounds__(RT) void rollout_kernel(RolloutArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    auto& S = *reinterpret_cast<StepSmem<O, A, K>*>(smem_raw);
+    auto& P = S.pol;
+    auto& E = S.env;
+    const int p = blockIdx.x, t = threadIdx.x, N = a.N, T = a.T;
+    const NormCfg nc = norm_cfg(a.ns);
+    const float* prm = a.params + (size_t)p * a.L.total;
+    float* obs = a.rb.obs + (size_t)p * (T + 1) * N * O;
+    float* act = a.rb.actions + (size_t)p * T * N * A;
+    float* logp = a.rb.logp + (size_t)p * T * N;
+    float* val = a.rb.values + (size_t)p * (T + 1) * N * K;
+    float* rew = a.rb.rewards + (size_t)p * T * N * K;
+    float* masks = a.rb.masks + (size_t)p * (T + 1) * N;
+    float* bad = a.rb.bad_masks + (size_t)p * (T + 1) * N;
+
+    load_policy(P, prm, a.L);
+    load_env(E, a.st, a.ns, p, N);
+    if (a.carry) {  // after_update(): slot T -> slot 0 (storage.py:71-75)
+        for (int i = t; i < N * O; i += RT) obs[i] = obs[(size_t)T * N * O + i];
+        if (t < N) {
+            masks[t] = masks[(size_t)T * N + t];
+            bad[t] = bad[(size_t)T * N + t];
+        }
+        // each thread re-reads only the obs[0] elements it wrote itself
+    }
+    for (int i = t; i < N * O; i += RT) P.x[i / O][i % O] = obs[i];
+    __syncthreads();
+
+    for (int step = 0; step < T; ++step) {
+        policy_forward(P, N, prm, a.L);
+        for (int i = t; i < N * K; i += RT) val[(size_t)step * N * K + i] = P.val[i / K][i % K];
+        for (int i = t; i < N * A; i += RT) {
+            const int n = i / A, j = i % A;
+            const size_t idx = (size_t)step * N * A + i;
+            const float eps = a.noise ? a.noise[idx] : counter_normal(a.seed, idx);
+            const float mu = P.mu[n][j], ls = P.logstd[j], sd = expf(ls);
+            const float av = fmaf(eps, sd, mu);  // torch.normal(mean, std) = z*std + mean
+            const float dz = (av - mu) / sd;
+            P.lp[n][j] = -0.5f * dz * dz - ls - LOG_SQRT_2PI;
+            act[idx] = av;
+            E.ac[n][j] = clipd((double)av, a.spec.act_lo[j], a.spec.act_hi[j]);
+        }
+        __syncthreads();
+        if (t < N) {
+            float s = 0.f;
+            for (int j = 0; j < A; ++j) s += P.lp[t][j];
+            logp[(size_t)step * N + t] = s;
+        }
+        env_dynamics(E, N, a.spec, a.st.s0);
+        vecnorm_stats(E, N, nc);
+        vecnorm_emit<O, A, K, opad<O>()>(E, N, nc, P.x, obs + (size_t)(step + 1) * N * O,
+                                         rew + (size_t)step * N * K, masks + (size_t)(step + 1) * N,
+                                         bad + (size_t)(step + 1) * N);
+    }
+    // bootstrap value (mopg.py:132-135) -> value_preds[T] (storage.py:85)
+    policy_forward(P, N, prm, a.L);
+    for (int i = t; i < N * K; i += RT) val[(size_t)T * N * K + i] = P.val[i / K][i % K];
+    store_env(E, a.st, a.ns, p, N);
+}
+
+struct EvalArgs {
+    int P;
+    Layout L;
+    const float* params;
+    pgm_env_spec spec;
+    const double *ob_mean, *ob_var, *s0_eval;
+    int eval_num, use_ob, raw;
+    double gamma;
+    double* objs;
+};
+
+template <int O, int A, int K>
+__global__ __launch_bounds__(RT) void eval_kernel(EvalArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    auto& S = *reinterpret_cast<StepSmem<O, A, K>*>(smem_raw);
+    auto& P = S.pol;
+    auto& E = S.env;
+    double* objsum = E.objsum;
+    const int p = blockIdx.x, t = threadIdx.x;
+    const float* prm = a.params + (size_t)p * a.L.total;
+    load_policy(P, prm, a.L);
+    for (int o = t; o < O; o += RT) {
+        E.ob_mean[o] = a.ob_mean[(size_t)p * O + o];
+        E.ob_var[o] = a.ob_var[(size_t)p * O + o];
+    }
+    if (t < K) objsum[t] = 0.0;
+    __syncthreads();
+    for (int e = 0; e < a.eval_num; ++e) {
+        const double* s0 = a.s0_eval + (size_t)e * O;
+        for (int o = t; o < O; o += RT) E.s[0][o] = s0[o];
+        if (t == 0) E.elapsed[0] = 0;
+        double g = 1.0;
+        __syncthreads();
+        while (true) {
+            for (int o = t; o < O; o += RT) {  // mopg.py:37-38 (fp64 normalisation, no fp32 round of the env obs)
+                double v = E.s[0][o];
+                if (a.use_ob) v = clipd((v - E.ob_mean[o]) / sqrt(E.ob_var[o] + 1e-8), -10.0, 10.0);
+                P.x[0][o] = (float)v;
+            }
+            __syncthreads();
+            policy_forward(P, 1, prm, a.L);
+            if (t < A) E.ac[0][t] = clipd((double)P.mu[0][t], a.spec.act_lo[t], a.spec.act_hi[t]);
+            __syncthreads();
+            env_dynamics(E, 1, a.spec, s0);
+            if (t < K) objsum[t] += g * E.objraw[0][t];
+            if (!a.raw) g *= a.gamma;
+            const int done = E.done[0];
+            __syncthreads();
+            if (done) break;
+        }
+    }
+    if (t < K) a.objs[(size_t)p * K + t] = objsum[t] / (double)a.eval_num;
+}
+
+// ------------------------------------------------------------------------------------------
+template <class Kern, class Args>
+static int launch_smem(Kern k, int grid, size_t smem, hipStream_t s, const Args& args, const char* what) {
+    if (smem > 160 * 1024) {
+        set_error("%s: LDS image %zu bytes exceeds 160 KiB", what, smem);
+        return PGM_E_UNSUPPORTED;
+    }
+    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    if (e != hipSuccess) return hip_fail(e, what);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(RT), smem, s, args);
+    return launch_status(what);
+}
+
+static bool spec_ok(const pgm_env_spec* sp) {
+    return sp && sp->d && sp->U && sp->c && sp->V && sp->ebase && sp->ecoef && sp->act_lo && sp->act_hi &&
+           sp->max_episode_steps > 0;
+}
+static bool state_ok(const pgm_env_state* st) {
+    return st && st->s && st->elapsed && st->obj_acc && st->obj_acc_valid && st->ret && st->s0;
+}
+static bool norm_ok(const pgm_norm_state* ns) {
+    return ns && ns->ob_mean && ns->ob_var && ns->ob_count && ns->ret_mean && ns->ret_var && ns->ret_count &&
+           ns->obj_mean && ns->obj_var && ns->obj_count;
+}
+
+}  // namespace pgm
+
+using namespace pgm;
+
+extern "C" {
+
+int pgm_act_forward(const pgm_dims* d, const float* params, const float* obs, const float* noise,
+                    int32_t deterministic, float* value, float* action, float* logp, pgm_stream_t stream) {
+    if (int rc = check_dims(d, "pgm_act_forward")) return rc;
+    if (!params || !obs || !value || !action || !logp || (!deterministic && !noise)) {
+        set_error("pgm_act_forward: null pointer (noise is required unless deterministic)");
+        return PGM_E_INVALID_ARG;
+    }
+    ActArgs a{d->P, d->N, make_layout(d->O, d->A, d->K, d->H), params, obs, noise, deterministic, value, action, logp};
+    return dispatch_dims(d->O, d->A, d->K, "pgm_act_forward", [&](auto o, auto aa, auto k) {
+        constexpr int O = decltype(o)::value, A = decltype(aa)::value, K = decltype(k)::value;
+        return launch_smem(act_forward_kernel<O, A, K>, d->P, sizeof(PolSmem<O, A, K>), (hipStream_t)stream, a,
+                           "pgm_act_forward");
+    });
+}
+
+static int env_common(const pgm_dims* d, const pgm_env_spec* spec, const pgm_env_state* st,
+                      const pgm_norm_state* ns, const char* what) {
+    if (int rc = check_dims(d, what)) return rc;
+    if (!spec_ok(spec) || !state_ok(st) || !norm_ok(ns)) {
+        set_error("%s: null pointer in spec/state/norm structs", what);
+        return PGM_E_INVALID_ARG;
+    }
+    return PGM_OK;
+}
+
+int pgm_env_reset(const pgm_dims* d, const pgm_env_spec* spec, const pgm_env_state* st,
+                  const pgm_norm_state* ns, float* obs_out, pgm_stream_t stream) {
+    if (int rc = env_common(d, spec, st, ns, "pgm_env_reset")) return rc;
+    if (!obs_out) {
+        set_error("pgm_env_reset: null obs_out");
+        return PGM_E_INVALID_ARG;
+    }
+    EnvArgs a{d->P, d->N, *spec, *st, *ns, nullptr, obs_out, nullptr, nullptr, nullptr, 1};
+    return dispatch_dims(d->O, d->A, d->K, "pgm_env_reset", [&](auto o, auto aa, auto k) {
+        constexpr int O = decltype(o)::value, A = decltype(aa)::value, K = decltype(k)::value;
+        return launch_smem(env_kernel<O, A, K>, d->P, sizeof(StepSmem<O, A, K>), (hipStream_t)stream, a,
+                           "pgm_env_reset");
+    });
+}
+
+int pgm_env_step(const pgm_dims* d, const pgm_env_spec* spec, const pgm_env_state* st,
+                 const pgm_norm_state* ns, const float* action, float* obs_out, float* reward_out,
+                 float* masks_out, float* bad_masks_out, pgm_stream_t stream) {
+    if (int rc = env_common(d, spec, st, ns, "pgm_env_step")) return rc;
+    if (!action || !obs_out || !reward_out || !masks_out || !bad_masks_out) {
+        set_error("pgm_env_step: null pointer");
+        return PGM_E_INVALID_ARG;
+    }
+    EnvArgs a{d->P, d->N, *spec, *st, *ns, action, obs_out, reward_out, masks_out, bad_masks_out, 0};
+    return dispatch_dims(d->O, d->A, d->K, "pgm_env_step", [&](auto o, auto aa, auto k) {
+        constexpr int O = decltype(o)::value, A = decltype(aa)::value, K = decltype(k)::value;
+        return launch_smem(env_kernel<O, A, K>, d->P, sizeof(StepSmem<O, A, K>), (hipStream_t)stream, a,
+                           "pgm_env_step");
+    });
+}
+
+int pgm_rollout(const pgm_dims* d, const float* params, const pgm_env_spec* spec, const pgm_env_state* st,
+                const pgm_norm_state* ns, const pgm_rollout_buf* rb, const float* noise, uint64_t seed,
+                int32_t carry, pgm_stream_t stream) {
+    if (int rc = env_common(d, spec, st, ns, "pgm_rollout")) return rc;
+    if (!params || !rb || !rb->obs || !rb->actions || !rb->logp || !rb->values || !rb->rewards || !rb->masks ||
+        !rb->bad_masks) {
+        set_error("pgm_rollout: null pointer");
+        return PGM_E_INVALID_ARG;
+    }
+    if (d->T <= 0) {
+        set_error("pgm_rollout: T must be positive");
+        return PGM_E_SHAPE;
+    }
+    RolloutArgs a{d->P, d->N, d->T, make_layout(d->O, d->A, d->K, d->H), params, *spec, *st, *ns, *rb,
+                  noise, seed, carry};
+    return dispatch_dims(d->O, d->A, d->K, "pgm_rollout", [&](auto o, auto aa, auto k) {
+        constexpr int O = decltype(o)::value, A = decltype(aa)::value, K = decltype(k)::value;
+        return launch_smem(rollout_kernel<O, A, K>, d->P, sizeof(StepSmem<O, A, K>), (hipStream_t)stream, a,
+                           "pgm_rollout");
+    });
+}
+
+int pgm_eval(const pgm_dims* d, const float* params, const pgm_env_spec* spec, const double* ob_mean,
+             const double* ob_var, const double* s0_eval, int32_t eval_num, int32_t use_ob_rms, int32_t raw,
+             double gamma, double* objs_out, pgm_stream_t stream) {
+    if (int rc = check_dims(d, "pgm_eval")) return rc;
+    if (!params || !spec_ok(spec) || !s0_eval || !objs_out || eval_num <= 0 || (use_ob_rms && (!ob_mean || !ob_var))) {
+        set_error("pgm_eval: bad arguments");
+        return PGM_E_INVALID_ARG;
+    }
+    EvalArgs a{d->P, make_layout(d->O, d->A, d->K, d->H), params, *spec, ob_mean, ob_var, s0_eval,
+               eval_num, use_ob_rms, raw, gamma, objs_out};
+    return dispatch_dims(d->O, d->A, d->K, "pgm_eval", [&](auto o, auto aa, auto k) {
+        constexpr int O = decltype(o)::value, A = decltype(aa)::value, K = decltype(k)::value;
+        return launch_smem(eval_kernel<O, A, K>, d->P, sizeof(StepSmem<O, A, K>), (hipStream_t)stream, a,
+                           "pgm_eval");
+    });
+}
+
+}  // extern "C"

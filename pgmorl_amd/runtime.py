@@ -1,0 +1,225 @@
+"""Device-resident state of P MOPG tasks on one GPU and the per-iteration kernel sequence.
+
+One ``TaskBatch`` owns every HBM buffer of P tasks (parameters + Adam state, env state, running
+statistics, rollout storage) and drives the libpgm kernels on torch's current stream:
+
+    rollout (T steps, fused act + env + VecNormalize + insert + bootstrap value)
+      -> gae -> adv_normalize -> ppo_update -> eval
+
+i.e. one iteration of MOPG_worker's loop body (morl/mopg.py:95-155) for all tasks at once.
+torch is used only for device memory and the stream; every op is a libpgm kernel and raises if
+the library is unavailable (no CPU fallback).
+"""
+import ctypes as C
+import math
+
+import numpy as np
+import torch
+
+from . import envspec
+from ._lib import (Dims, EnvSpec, EnvState, NormState, PPOHParams, RolloutBuf, check, lib)
+from .layout import ParamLayout
+
+F32, F64, I32 = torch.float32, torch.float64, torch.int32
+
+
+def _ptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else C.c_void_p(0)
+
+
+def _stream():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+class TaskBatch:
+    """HBM state of P tasks sharing env, rollout shape and PPO hyper-parameters."""
+
+    def __init__(self, env_name, P, num_processes=4, num_steps=2048, seed=0, eval_num=1, gamma=0.995,
+                 gae_lambda=0.95, use_gae=True, use_proper_time_limits=True, ob_rms=True, obj_rms=True, raw=True,
+                 clip_param=0.2, ppo_epoch=10, num_mini_batch=32, value_loss_coef=0.5, entropy_coef=0.0,
+                 max_grad_norm=0.5, adam_eps=1e-5, use_clipped_value_loss=True, device='cuda'):
+        self.spec = envspec.make_spec(env_name)
+        sp = self.spec
+        self.env_name = env_name
+        self.P, self.N, self.T = P, num_processes, num_steps
+        self.O, self.A, self.K, self.H = sp['obs_dim'], sp['act_dim'], sp['obj_num'], 64
+        self.eval_num, self.gamma, self.gae_lambda = eval_num, gamma, gae_lambda
+        self.use_gae, self.proper = use_gae, use_proper_time_limits
+        self.use_ob_rms, self.use_obj_rms, self.raw = ob_rms, obj_rms, raw
+        self.dev = torch.device(device)
+        self.layout = ParamLayout(self.O, self.A, self.K, self.H)
+        L, O, A, K, N, T = self.layout.total, self.O, self.A, self.K, self.N, self.T
+        z = lambda *s, dt=F32: torch.zeros(*s, dtype=dt, device=self.dev)
+        # spec constants + reset tables (fp64)
+        self._spec_t = {k: torch.tensor(np.ascontiguousarray(sp[k]), dtype=F64, device=self.dev)
+                        for k in ('d', 'U', 'c', 'V', 'ebase', 'ecoef', 'act_lo', 'act_hi')}
+        self.s0_train = torch.tensor(envspec.reset_table(O, seed, N), dtype=F64, device=self.dev)
+        self.s0_eval = torch.tensor(envspec.reset_table(O, seed, eval_num), dtype=F64, device=self.dev)
+        # policy + optimiser
+        self.params, self.adam_m, self.adam_v = z(P, L), z(P, L), z(P, L)
+        self.adam_step = z(P, dt=I32)
+        self.lr = z(P)
+        self.weights = z(P, K, dt=F64)
+        # env + running statistics
+        self.s, self.elapsed = z(P, N, O, dt=F64), z(P, N, dt=I32)
+        self.obj_acc, self.obj_valid, self.ret = z(P, N, K, dt=F64), z(P, dt=I32), z(P, N, dt=F64)
+        self.ob_mean, self.ob_var, self.ob_count = z(P, O, dt=F64), z(P, O, dt=F64), z(P, dt=F64)
+        self.ret_mean, self.ret_var, self.ret_count = z(P, dt=F64), z(P, dt=F64), z(P, dt=F64)
+        self.obj_mean, self.obj_var, self.obj_count = z(P, K, dt=F64), z(P, K, dt=F64), z(P, dt=F64)
+        # rollout storage (storage.py:12-30)
+        self.obs = z(P, T + 1, N, O)
+        self.actions, self.logp = z(P, T, N, A), z(P, T, N)
+        self.values, self.returns = z(P, T + 1, N, K), z(P, T + 1, N, K)
+        self.rewards, self.adv = z(P, T, N, K), z(P, T, N)
+        self.masks, self.bad_masks = torch.ones(P, T + 1, N, device=self.dev), torch.ones(P, T + 1, N, device=self.dev)
+        self.stats, self.objs = z(P, 3), z(P, K, dt=F64)
+        self.perms = z(ppo_epoch, T * N, dt=I32)
+        self.noise = z(T, N, A)
+        self.hp = PPOHParams(clip_param=clip_param, value_loss_coef=value_loss_coef, entropy_coef=entropy_coef,
+                             max_grad_norm=max_grad_norm, adam_eps=adam_eps, beta1=0.9, beta2=0.999,
+                             ppo_epoch=ppo_epoch, num_mini_batch=num_mini_batch,
+                             use_clipped_value_loss=int(use_clipped_value_loss))
+        self.reset_stats()
+        self._build_structs()
+
+    # ------------------------------------------------------------------ structs
+    def _build_structs(self):
+        self.dims = Dims(self.P, self.N, self.T, self.O, self.A, self.K, self.H)
+        st = self._spec_t
+        self.c_spec = EnvSpec(_ptr(st['d']), _ptr(st['U']), _ptr(st['c']), _ptr(st['V']), _ptr(st['ebase']),
+                              _ptr(st['ecoef']), _ptr(st['act_lo']), _ptr(st['act_hi']),
+                              self.spec['max_episode_steps'], 0)
+        self.c_state = EnvState(_ptr(self.s), _ptr(self.elapsed), _ptr(self.obj_acc), _ptr(self.obj_valid),
+                                _ptr(self.ret), _ptr(self.s0_train))
+        self.c_norm = NormState(_ptr(self.ob_mean), _ptr(self.ob_var), _ptr(self.ob_count), _ptr(self.ret_mean),
+                                _ptr(self.ret_var), _ptr(self.ret_count), _ptr(self.obj_mean), _ptr(self.obj_var),
+                                _ptr(self.obj_count), self.gamma, 10.0, 10.0, 1e-8, int(self.use_ob_rms),
+                                int(self.use_obj_rms))
+        self.c_rb = RolloutBuf(*(_ptr(t) for t in (self.obs, self.actions, self.logp, self.values, self.rewards,
+                                                   self.masks, self.bad_masks, self.returns, self.adv)))
+
+    def reset_stats(self):
+        """Fresh RunningMeanStd objects: count 1e-4, mean 0, var 1 (running_mean_std.py:5-8)."""
+        for mean, var, cnt in ((self.ob_mean, self.ob_var, self.ob_count), (self.ret_mean, self.ret_var, self.ret_count),
+                               (self.obj_mean, self.obj_var, self.obj_count)):
+            mean.zero_()
+            var.fill_(1.0)
+            cnt.fill_(1e-4)
+
+    # ------------------------------------------------------------------ kernels
+    def env_reset(self):
+        """Fresh make_vec_envs + envs.reset() (mopg.py:67-82): obs[:, 0], masks[:, 0] = 1."""
+        out = torch.empty(self.P, self.N, self.O, dtype=F32, device=self.dev)
+        check(lib().pgm_env_reset(C.byref(self.dims), C.byref(self.c_spec), C.byref(self.c_state),
+                                  C.byref(self.c_norm), _ptr(out), _stream()), 'pgm_env_reset')
+        self.obs[:, 0].copy_(out)
+        self.masks[:, 0] = 1.0
+        self.bad_masks[:, 0] = 1.0
+        return out
+
+    def env_step(self, action):
+        P, N, O, K = self.P, self.N, self.O, self.K
+        action = action.to(device=self.dev, dtype=F32).contiguous()
+        obs = torch.empty(P, N, O, dtype=F32, device=self.dev)
+        rew = torch.empty(P, N, K, dtype=F32, device=self.dev)
+        m, b = torch.empty(P, N, dtype=F32, device=self.dev), torch.empty(P, N, dtype=F32, device=self.dev)
+        check(lib().pgm_env_step(C.byref(self.dims), C.byref(self.c_spec), C.byref(self.c_state),
+                                 C.byref(self.c_norm), _ptr(action), _ptr(obs), _ptr(rew), _ptr(m), _ptr(b),
+                                 _stream()), 'pgm_env_step')
+        return obs, rew, m, b
+
+    def act(self, obs, noise=None, deterministic=False):
+        P, N = self.P, obs.shape[1]
+        obs = obs.to(device=self.dev, dtype=F32).contiguous()
+        d = Dims(P, N, self.T, self.O, self.A, self.K, self.H)
+        value = torch.empty(P, N, self.K, dtype=F32, device=self.dev)
+        action = torch.empty(P, N, self.A, dtype=F32, device=self.dev)
+        logp = torch.empty(P, N, dtype=F32, device=self.dev)
+        nz = None if noise is None else noise.to(device=self.dev, dtype=F32).contiguous()
+        check(lib().pgm_act_forward(C.byref(d), _ptr(self.params), _ptr(obs), _ptr(nz), int(deterministic),
+                                    _ptr(value), _ptr(action), _ptr(logp), _stream()), 'pgm_act_forward')
+        return value, action, logp
+
+    def rollout(self, seed, noise=None, carry=True):
+        nz = None
+        if noise is not None:
+            self.noise.copy_(noise.to(dtype=F32))
+            nz = self.noise
+        check(lib().pgm_rollout(C.byref(self.dims), _ptr(self.params), C.byref(self.c_spec), C.byref(self.c_state),
+                                C.byref(self.c_norm), C.byref(self.c_rb), _ptr(nz), C.c_uint64(seed),
+                                int(carry), _stream()), 'pgm_rollout')
+
+    def gae(self):
+        check(lib().pgm_gae(C.byref(self.dims), C.byref(self.c_rb), self.gamma, self.gae_lambda, int(self.use_gae),
+                            int(self.proper), _stream()), 'pgm_gae')
+
+    def adv_normalize(self):
+        var = self.obj_var if self.use_obj_rms else None
+        check(lib().pgm_adv_normalize(C.byref(self.dims), C.byref(self.c_rb), _ptr(self.weights), _ptr(var),
+                                      _stream()), 'pgm_adv_normalize')
+
+    def make_perms(self, seed):
+        E, n = self.perms.shape
+        check(lib().pgm_randperm(n, E, C.c_uint64(seed), _ptr(self.perms), _stream()), 'pgm_randperm')
+
+    def ppo_update(self, perms=None):
+        if perms is not None:
+            self.perms.copy_(torch.as_tensor(np.asarray(perms), dtype=I32))
+        check(lib().pgm_ppo_update(C.byref(self.dims), C.byref(self.hp), _ptr(self.params), _ptr(self.adam_m),
+                                   _ptr(self.adam_v), _ptr(self.adam_step), _ptr(self.lr), _ptr(self.perms),
+                                   C.byref(self.c_rb), _ptr(self.stats), _stream()), 'pgm_ppo_update')
+
+    def evaluate(self, ob_mean=None, ob_var=None):
+        mean = self.ob_mean if ob_mean is None else ob_mean
+        var = self.ob_var if ob_var is None else ob_var
+        check(lib().pgm_eval(C.byref(self.dims), _ptr(self.params), C.byref(self.c_spec), _ptr(mean), _ptr(var),
+                             _ptr(self.s0_eval), self.eval_num, int(self.use_ob_rms), int(self.raw), self.gamma,
+                             _ptr(self.objs), _stream()), 'pgm_eval')
+        return self.objs
+
+    def iteration(self, j, lr, noise=None, perms=None, carry=True):
+        """One MOPG iteration for every task: rollout, returns, advantages, PPO update, evaluation.
+
+        noise/perms: the reference's RNG draws of iteration j (parity mode); None draws the
+        device counter streams keyed by j (perf mode)."""
+        self.lr.fill_(float(lr))
+        self.rollout(j, noise=noise, carry=carry)
+        self.gae()
+        self.adv_normalize()
+        if perms is None:
+            self.make_perms(j)
+        self.ppo_update(perms)
+        self.evaluate()
+
+    # ------------------------------------------------------------------ host transfer
+    def set_task(self, p, state_dict, opt_state=None, env_params=None, weights=None):
+        lay = self.layout
+        self.params[p].copy_(torch.from_numpy(lay.flatten(state_dict)))
+        m, v, step = lay.adam_from_optimizer_state(opt_state or {})
+        self.adam_m[p].copy_(torch.from_numpy(m))
+        self.adam_v[p].copy_(torch.from_numpy(v))
+        self.adam_step[p] = step
+        if weights is not None:
+            self.weights[p].copy_(torch.as_tensor(np.asarray(weights, dtype=np.float64)))
+        if env_params is not None:
+            self.set_env_params(p, env_params)
+
+    def set_env_params(self, p, env_params):
+        """Restore ob_rms / ret_rms / obj_rms (mopg.py:70-75); obj_rms may still be scalar-shaped."""
+        K = self.K
+        ob, rt, oj = env_params.get('ob_rms'), env_params.get('ret_rms'), env_params.get('obj_rms')
+        if ob is not None:
+            self.ob_mean[p].copy_(torch.as_tensor(np.asarray(ob.mean, np.float64)))
+            self.ob_var[p].copy_(torch.as_tensor(np.asarray(ob.var, np.float64)))
+            self.ob_count[p] = float(ob.count)
+        if rt is not None:
+            self.ret_mean[p] = float(np.asarray(rt.mean).reshape(-1)[0])
+            self.ret_var[p] = float(np.asarray(rt.var).reshape(-1)[0])
+            self.ret_count[p] = float(rt.count)
+        if oj is not None:
+            self.obj_mean[p].copy_(torch.as_tensor(np.broadcast_to(np.asarray(oj.mean, np.float64), (K,)).copy()))
+            self.obj_var[p].copy_(torch.as_tensor(np.broadcast_to(np.asarray(oj.var, np.float64), (K,)).copy()))
+            self.obj_count[p] = float(oj.count)
+
+    def get_params(self, p):
+        return self.layout.unflatten(self.params[p])

@@ -1,0 +1,111 @@
+"""CPU-side checks of the C ABI library: it loads, exports exactly what include/pgm_abi.h declares,
+its structs match ctypes, and the parameter layout round-trips reference state_dicts.
+No kernel is launched here (no GPU in this container)."""
+import os
+import re
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+
+from pgmorl_amd import _lib
+from pgmorl_amd.layout import STATE_KEYS, ParamLayout
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, 'include', 'pgm_abi.h')
+
+
+def _declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r'/\*.*?\*/', '', src, flags=re.S)
+    return sorted(set(re.findall(r'\b(pgm_[a-z0-9_]+)\s*\(', src)))
+
+
+def test_library_loads_and_reports_abi():
+    assert _lib.lib().pgm_abi_version() == _lib.PGM_ABI_VERSION
+
+
+def test_exports_every_declared_symbol():
+    declared = _declared_functions()
+    assert set(declared) == set(_lib.EXPORTS), (declared, _lib.EXPORTS)
+    out = subprocess.run(['nm', '-D', '--defined-only', _lib.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r' T (pgm_[a-z0-9_]+)', out))
+    missing = set(declared) - exported
+    assert not missing, missing
+
+
+def test_struct_sizes_match_header():
+    import ctypes as C
+    prog = r'''
+#include <stdio.h>
+#include "pgm_abi.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu %zu\n", sizeof(pgm_dims), sizeof(pgm_env_spec), sizeof(pgm_env_state),
+         sizeof(pgm_norm_state), sizeof(pgm_rollout_buf), sizeof(pgm_ppo_hparams));
+  return 0; }
+'''
+    with tempfile.TemporaryDirectory() as d:
+        c, exe = os.path.join(d, 's.c'), os.path.join(d, 's')
+        open(c, 'w').write(prog)
+        subprocess.run(['gcc', '-I', os.path.join(ROOT, 'include'), c, '-o', exe], check=True)
+        sizes = [int(x) for x in subprocess.run([exe], capture_output=True, text=True).stdout.split()]
+    want = [C.sizeof(s) for s in (_lib.Dims, _lib.EnvSpec, _lib.EnvState, _lib.NormState, _lib.RolloutBuf,
+                                   _lib.PPOHParams)]
+    assert sizes == want
+
+
+def test_error_reporting_without_gpu():
+    import ctypes as C
+    L = _lib.lib()
+    d = _lib.Dims(0, 4, 8, 17, 6, 2, 64)  # P=0 is rejected before any HIP call
+    rc = L.pgm_gae(C.byref(d), None, 0.99, 0.95, 1, 1, None)
+    assert rc == _lib.PGM_E_INVALID_ARG
+    d = _lib.Dims(2, 4, 8, 17, 6, 2, 32)
+    rc = L.pgm_act_forward(C.byref(d), C.c_void_p(1), C.c_void_p(1), C.c_void_p(1), 0, C.c_void_p(1),
+                           C.c_void_p(1), C.c_void_p(1), None)
+    assert rc == _lib.PGM_E_UNSUPPORTED and b'hidden size' in L.pgm_last_error()
+    d = _lib.Dims(2, 4, 8, 19, 6, 2, 64)
+    rc = L.pgm_act_forward(C.byref(d), C.c_void_p(1), C.c_void_p(1), C.c_void_p(1), 0, C.c_void_p(1),
+                           C.c_void_p(1), C.c_void_p(1), None)
+    assert rc == _lib.PGM_E_UNSUPPORTED and b'unsupported dims' in L.pgm_last_error()
+
+
+@pytest.mark.parametrize('O,A,K', [(17, 6, 2), (11, 3, 3), (376, 17, 2)])
+def test_param_layout_roundtrip(O, A, K):
+    from oracle.policy import make_policy
+    torch.manual_seed(3)
+    pol = make_policy(O, A, K)
+    sd = pol.state_dict()
+    assert [k for k, _, _ in STATE_KEYS] == list(sd.keys())
+    lay = ParamLayout(O, A, K)
+    assert lay.total % 64 == 0
+    for name, off in lay.offsets.items():
+        assert off % 4 == 0
+    flat = lay.flatten(sd, dtype=np.float64)
+    back = lay.unflatten(flat)
+    for k in sd:
+        assert torch.equal(back[k], sd[k]), k
+    # actor_w1 is stored transposed: element (in=k, out=j) at off + k*H + j
+    w = sd['base.actor.0.weight']
+    assert flat[lay.offsets['actor_w1'] + 2 * 64 + 5] == float(w[5, 2])
+    n_params = sum(v.numel() for v in sd.values())
+    assert n_params == 2 * (O * 64 + 64 + 64 * 64 + 64) + 64 * K + K + 64 * A + A + A
+
+
+def test_adam_state_roundtrip():
+    from oracle.policy import make_policy
+    torch.manual_seed(0)
+    pol = make_policy(17, 6, 2)
+    opt = torch.optim.Adam(pol.parameters(), lr=3e-4, eps=1e-5)
+    sum((q * q).sum() for q in pol.parameters()).backward()
+    opt.step()
+    lay = ParamLayout(17, 6, 2)
+    m, v, step = lay.adam_from_optimizer_state(opt.state_dict()['state'])
+    assert step == 1
+    st = lay.adam_to_optimizer_state(m, v, step)
+    opt2 = torch.optim.Adam(pol.parameters(), lr=3e-4, eps=1e-5)
+    opt2.load_state_dict({'state': st, 'param_groups': opt.state_dict()['param_groups']})
+    for i in st:
+        assert torch.allclose(opt2.state_dict()['state'][i]['exp_avg'], opt.state_dict()['state'][i]['exp_avg'].float().double())

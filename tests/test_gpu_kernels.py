@@ -1,0 +1,340 @@
+"""Parity of every libpgm kernel (MI355X, fp32) against the CPU oracle (fp64) on identical inputs.
+
+Tolerances are stated per test; the north-star bar is scalarised returns within 1e-5 relative.
+All calls go through the C ABI (include/pgm_abi.h) via pgmorl_amd.runtime.TaskBatch.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ppo as oppo
+from oracle.mopg import evaluation as oracle_evaluation
+from oracle.mopg import initial_sample, mopg_worker
+from oracle.vecenv import RunningMeanStd, VecNormalizedSynth
+from pgmorl_amd import envspec
+from pgmorl_amd.runtime import TaskBatch
+
+from .helpers import fp32_policies, perturb, small_args, weights_grid
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(a, b, atol, rtol, what):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    err = np.abs(a - b)
+    bad = err > atol + rtol * np.abs(b)
+    assert not bad.any(), f'{what}: {bad.sum()}/{bad.size} off, max abs err {err.max():.3e}'
+
+
+def _batch_with_policies(env, P, N=4, T=16, seed=0, scale=0.05, **kw):
+    spec = envspec.make_spec(env)
+    tb = TaskBatch(env, P, num_processes=N, num_steps=T, **kw)
+    gen = torch.Generator().manual_seed(seed + 100)
+    pols = [perturb(p, scale, gen) for p in fp32_policies(spec, P, seed)]
+    for p, pol in enumerate(pols):
+        tb.set_task(p, pol.state_dict())
+    return spec, tb, pols
+
+
+@pytest.mark.parametrize('env', ['MO-Walker2d-v2', 'MO-Hopper-v3', 'MO-Humanoid-v2', 'MO-Swimmer-v2'])
+def test_act_forward(gpu, env):
+    P, N = 3, 4
+    spec, tb, pols = _batch_with_policies(env, P, N)
+    g = torch.Generator().manual_seed(1)
+    obs = torch.randn(P, N, spec['obs_dim'], generator=g).float()
+    noise = torch.randn(N, spec['act_dim'], generator=g).float()
+    v, a, lp = (x.cpu() for x in tb.act(obs.to(gpu), noise.to(gpu)))
+    _, am, _ = (x.cpu() for x in tb.act(obs.to(gpu), deterministic=True))
+    for p in range(P):
+        with torch.no_grad():
+            rv, ra, rlp = pols[p].act(obs[p].double(), noise=noise.double())
+            _, rm, _ = pols[p].act(obs[p].double(), deterministic=True)
+        _close(v[p], rv, 2e-5, 1e-5, 'value')
+        _close(a[p], ra, 2e-5, 1e-5, 'action')
+        _close(lp[p], rlp[:, 0], 5e-5, 1e-5, 'log_prob')
+        _close(am[p], rm, 2e-5, 1e-5, 'deterministic action')
+
+
+@pytest.mark.parametrize('env,N', [('MO-Hopper-v2', 4), ('MO-Walker2d-v2', 1), ('MO-Hopper-v3', 8)])
+def test_env_reset_step_vecnormalize(gpu, env, N):
+    """envs.reset + 520 envs.step (crosses the 500-step time limit: auto-reset, bad_transition)."""
+    P, steps = 2, 520
+    spec = envspec.make_spec(env)
+    tb = TaskBatch(env, P, num_processes=N, num_steps=4)
+    s0 = envspec.reset_table(spec['obs_dim'], 0, N)
+    ref = [VecNormalizedSynth(spec, s0, 0.995) for _ in range(P)]
+    o_gpu = tb.env_reset().cpu().numpy()
+    for p in range(P):
+        _close(o_gpu[p], ref[p].reset(), 1e-6, 1e-6, 'reset obs')
+    rng = np.random.RandomState(3)
+    for t in range(steps):
+        act = (rng.randn(P, N, spec['act_dim']) * 0.7).astype(np.float32)
+        obs, rew, m, b = (x.cpu().numpy() for x in tb.env_step(torch.from_numpy(act).to(gpu)))
+        for p in range(P):
+            ro, rd, infos = ref[p].step(act[p].astype(np.float64))
+            _close(obs[p], ro, 2e-6, 2e-6, f'obs step {t}')
+            _close(rew[p], np.stack([i['obj'] for i in infos]), 1e-5, 1e-6, f'reward step {t}')
+            np.testing.assert_array_equal(m[p], np.where(rd, 0.0, 1.0))
+            np.testing.assert_array_equal(b[p], [0.0 if 'bad_transition' in i else 1.0 for i in infos])
+    for p in range(P):
+        _close(tb.ob_mean[p].cpu(), ref[p].ob_rms.mean, 0, 1e-9, 'ob_rms.mean')
+        _close(tb.ob_var[p].cpu(), ref[p].ob_rms.var, 0, 1e-9, 'ob_rms.var')
+        assert float(tb.ob_count[p]) == pytest.approx(ref[p].ob_rms.count, rel=1e-12)
+        _close(tb.obj_mean[p].cpu(), ref[p].obj_rms.mean, 0, 1e-9, 'obj_rms.mean')
+        _close(tb.obj_var[p].cpu(), ref[p].obj_rms.var, 0, 1e-9, 'obj_rms.var')
+        assert float(tb.ret_count[p]) == pytest.approx(ref[p].ret_rms.count, rel=1e-12)
+
+
+def _random_storage(P, T, N, K, seed):
+    rng = np.random.RandomState(seed)
+    rew = rng.randn(P, T, N, K)
+    val = rng.randn(P, T + 1, N, K)
+    masks = np.ones((P, T + 1, N))
+    bad = np.ones((P, T + 1, N))
+    done = rng.rand(P, T + 1, N) < 0.05
+    masks[done] = 0.0
+    tl = done & (rng.rand(P, T + 1, N) < 0.5)
+    bad[tl] = 0.0
+    return [x.astype(np.float32) for x in (rew, val, masks, bad)]
+
+
+@pytest.mark.parametrize('use_gae,proper', [(True, True), (True, False), (False, True), (False, False)])
+@pytest.mark.parametrize('N,K,T', [(4, 2, 2048), (8, 2, 300), (1, 3, 77)])
+def test_gae(gpu, use_gae, proper, N, K, T):
+    P = 3
+    env = {2: 'MO-Walker2d-v2', 3: 'MO-Hopper-v3'}[K]
+    tb = TaskBatch(env, P, num_processes=N, num_steps=T, use_gae=use_gae, use_proper_time_limits=proper,
+                   gamma=0.99, gae_lambda=0.95)
+    rew, val, masks, bad = _random_storage(P, T, N, K, seed=T + N)
+    for dst, src in ((tb.rewards, rew), (tb.values, val), (tb.masks, masks), (tb.bad_masks, bad)):
+        dst.copy_(torch.from_numpy(src))
+    tb.gae()
+    got = tb.returns.cpu().numpy()
+    for p in range(P):
+        r, v = torch.from_numpy(rew[p]).double(), torch.from_numpy(val[p]).double()
+        m = torch.from_numpy(masks[p]).double().unsqueeze(-1)
+        b = torch.from_numpy(bad[p]).double().unsqueeze(-1)
+        ret = torch.zeros(T + 1, N, K, dtype=torch.float64)
+        oppo.compute_returns_inplace(r, v.clone(), m, b, ret, v[-1], use_gae, 0.99, 0.95, proper)
+        _close(got[p, :T], ret[:T].numpy(), 1e-5, 1e-5, 'returns')
+
+
+@pytest.mark.parametrize('use_obj_rms', [True, False])
+def test_adv_normalize(gpu, use_obj_rms):
+    P, T, N, K = 3, 512, 4, 2
+    tb = TaskBatch('MO-Walker2d-v2', P, num_processes=N, num_steps=T, obj_rms=use_obj_rms)
+    rng = np.random.RandomState(5)
+    R = (rng.randn(P, T + 1, N, K) * 3 + 1).astype(np.float32)
+    V = (rng.randn(P, T + 1, N, K) * 2).astype(np.float32)
+    w = weights_grid(K, P)
+    var = rng.rand(P, K) * 4 + 0.1
+    tb.returns.copy_(torch.from_numpy(R))
+    tb.values.copy_(torch.from_numpy(V))
+    tb.weights.copy_(torch.from_numpy(w))
+    tb.obj_var.copy_(torch.from_numpy(var))
+    tb.adv_normalize()
+    got = tb.adv.cpu().numpy()
+    for p in range(P):
+        ref = oppo.scalarized_normalized_advantages(torch.from_numpy(R[p]).double(), torch.from_numpy(V[p]).double(),
+                                                    w[p], var[p] if use_obj_rms else None)
+        _close(got[p], ref.numpy(), 1e-5, 1e-5, 'advantages')
+
+
+def _update_setup(env, P, T, N, E, M, seed):
+    args = small_args(env, num_steps=T, num_processes=N, ppo_epoch=E, num_mini_batch=M)
+    spec, tb, pols = _batch_with_policies(env, P, N, T, seed=seed, scale=0.05, ppo_epoch=E, num_mini_batch=M)
+    O, A, K, B = spec['obs_dim'], spec['act_dim'], spec['obj_num'], T * N
+    rng = np.random.RandomState(seed)
+    obs = np.clip(rng.randn(P, T + 1, N, O), -3, 3).astype(np.float32)
+    eps = rng.randn(P, T, N, A)
+    acts, lps, vals = [], [], []
+    for p in range(P):
+        with torch.no_grad():
+            v, a, lp = pols[p].act(torch.from_numpy(obs[p, :T]).double().reshape(B, O),
+                                   noise=torch.from_numpy(eps[p]).reshape(B, A))
+        acts.append(a.float().reshape(T, N, A))
+        lps.append((lp[:, 0] + torch.from_numpy(rng.randn(B) * 0.05)).float().reshape(T, N))
+        vals.append((v + torch.from_numpy(rng.randn(B, K) * 0.1)).float().reshape(T, N, K))
+    actions, logp, values = torch.stack(acts), torch.stack(lps), torch.stack(vals)
+    values = torch.cat([values, torch.zeros(P, 1, N, K)], 1)
+    returns = (values + torch.from_numpy(rng.randn(P, T + 1, N, K) * 0.5).float())
+    adv = torch.from_numpy(rng.randn(P, T, N)).float()
+    for dst, src in ((tb.obs, torch.from_numpy(obs)), (tb.actions, actions), (tb.logp, logp), (tb.values, values),
+                     (tb.returns, returns), (tb.adv, adv)):
+        dst.copy_(src)
+    perms = [torch.randperm(B, generator=torch.Generator().manual_seed(seed * 10 + e)) for e in range(E)]
+    return args, spec, tb, pols, (obs, actions, logp, values, returns, adv), perms
+
+
+@pytest.mark.parametrize('env,T,N,E,M', [('MO-Hopper-v2', 64, 4, 2, 4), ('MO-Walker2d-v2', 128, 4, 2, 2),
+                                         ('MO-Hopper-v3', 50, 3, 1, 3), ('MO-Swimmer-v2', 64, 1, 1, 1)])
+def test_ppo_update(gpu, env, T, N, E, M):
+    P, lr = 2, 3e-4
+    args, spec, tb, pols, data, perms = _update_setup(env, P, T, N, E, M, seed=11)
+    obs, actions, logp, values, returns, adv = data
+    tb.lr.fill_(lr)
+    tb.ppo_update(torch.stack(perms).numpy())
+    B = T * N
+    for p in range(P):
+        agent = oppo.PPO(pols[p], args.clip_param, E, M, args.value_loss_coef, args.entropy_coef, lr=lr, eps=1e-5,
+                         max_grad_norm=args.max_grad_norm)
+        ro = oppo.RolloutStorage(T, N, spec['obs_dim'], spec['act_dim'], spec['obj_num'])
+        ro.obs.copy_(torch.from_numpy(obs[p]).double())
+        ro.actions.copy_(actions[p].double())
+        ro.action_log_probs.copy_(logp[p].double().unsqueeze(-1))
+        ro.value_preds.copy_(values[p].double())
+        ro.returns.copy_(returns[p].double())
+        stats = np.zeros(3)
+        for e in range(E):
+            for mbt in ro.minibatches(adv[p].double(), M, perms[e]):
+                stats += agent.minibatch_step(*mbt)
+        stats /= E * M
+        ref = tb.layout.flatten(pols[p].state_dict(), dtype=np.float64)
+        _close(tb.params[p].cpu(), ref, 2e-6, 1e-5, f'params after update ({env})')
+        st = agent.optimizer.state_dict()['state']
+        m_ref, v_ref, step = tb.layout.adam_from_optimizer_state(st)
+        assert int(tb.adam_step[p]) == step == E * (B // (B // M))
+        _close(tb.adam_m[p].cpu(), m_ref, 1e-7, 1e-3, 'adam exp_avg')
+        _close(tb.adam_v[p].cpu(), v_ref, 1e-10, 1e-3, 'adam exp_avg_sq')
+        _close(tb.stats[p].cpu(), stats, 1e-5, 1e-4, 'loss stats')
+
+
+def test_randperm_and_noise_streams(gpu):
+    tb = TaskBatch('MO-Walker2d-v2', 1, num_processes=4, num_steps=2048)
+    tb.make_perms(5)
+    perms = tb.perms.cpu().numpy()
+    for row in perms:
+        np.testing.assert_array_equal(np.sort(row), np.arange(row.size))
+    assert len({row.tobytes() for row in perms}) == perms.shape[0]
+    tb.make_perms(5)
+    np.testing.assert_array_equal(tb.perms.cpu().numpy(), perms)  # deterministic per seed
+    from pgmorl_amd import _lib
+    import ctypes as C
+    x = torch.empty(1 << 20, device=gpu)
+    _lib.check(_lib.lib().pgm_normal_noise(x.numel(), 9, C.c_void_p(x.data_ptr()),
+                                           C.c_void_p(torch.cuda.current_stream().cuda_stream)), 'noise')
+    x = x.double().cpu()
+    assert abs(float(x.mean())) < 5e-3 and abs(float(x.std()) - 1) < 5e-3
+
+
+def _oracle_rollout(pol, envs, ro, noise):
+    for t in range(ro.num_steps):
+        with torch.no_grad():
+            value, action, logp = pol.act(ro.obs[t], noise=noise[t])
+        obs, dones, infos = envs.step(action.numpy())
+        obj = torch.tensor(np.stack([i['obj'] for i in infos]), dtype=torch.float64)
+        masks = torch.tensor([[0.0] if d else [1.0] for d in dones], dtype=torch.float64)
+        bad = torch.tensor([[0.0] if 'bad_transition' in i else [1.0] for i in infos], dtype=torch.float64)
+        ro.insert(torch.from_numpy(obs).double(), action, logp, value, obj, masks, bad)
+    with torch.no_grad():
+        ro.value_preds[-1] = pol.get_value(ro.obs[-1])
+
+
+@pytest.mark.parametrize('env,N,T', [('MO-Hopper-v2', 4, 48), ('MO-Walker2d-v2', 2, 520)])
+def test_rollout(gpu, env, N, T):
+    P = 2
+    spec, tb, pols = _batch_with_policies(env, P, N, T, seed=3, scale=0.05)
+    s0 = envspec.reset_table(spec['obs_dim'], 0, N)
+    noise = torch.randn(T, N, spec['act_dim'], generator=torch.Generator().manual_seed(4), dtype=torch.float64)
+    tb.env_reset()
+    tb.rollout(0, noise=noise.float(), carry=False)
+    for p in range(P):
+        envs = VecNormalizedSynth(spec, s0, 0.995)
+        ro = oppo.RolloutStorage(T, N, spec['obs_dim'], spec['act_dim'], spec['obj_num'])
+        ro.obs[0].copy_(torch.from_numpy(envs.reset()).double())
+        _oracle_rollout(pols[p], envs, ro, noise.float().double())
+        _close(tb.obs[p].cpu(), ro.obs, 5e-5, 1e-4, 'obs')
+        _close(tb.actions[p].cpu(), ro.actions, 5e-5, 1e-4, 'actions')
+        _close(tb.logp[p].cpu(), ro.action_log_probs[..., 0], 2e-4, 1e-4, 'logp')
+        _close(tb.values[p].cpu(), ro.value_preds, 5e-5, 1e-4, 'values (incl. bootstrap)')
+        _close(tb.rewards[p].cpu(), ro.rewards, 5e-5, 1e-4, 'rewards')
+        np.testing.assert_array_equal(tb.masks[p].cpu().numpy(), ro.masks[..., 0].numpy())
+        np.testing.assert_array_equal(tb.bad_masks[p].cpu().numpy(), ro.bad_masks[..., 0].numpy())
+        _close(tb.obj_var[p].cpu(), envs.obj_rms.var, 0, 1e-6, 'obj_rms.var')
+
+
+def test_rollout_perf_rng_equals_explicit_noise(gpu):
+    """The perf-mode counter RNG inside the rollout is exactly pgm_normal_noise's stream."""
+    from pgmorl_amd import _lib
+    import ctypes as C
+    P, N, T = 2, 4, 32
+    spec, tb, _ = _batch_with_policies('MO-Walker2d-v2', P, N, T)
+    tb.env_reset()
+    snap = {k: getattr(tb, k).clone() for k in ('s', 'elapsed', 'obj_acc', 'obj_valid', 'ret', 'ob_mean', 'ob_var',
+                                                 'ob_count', 'obj_mean', 'obj_var', 'obj_count', 'ret_mean',
+                                                 'ret_var', 'ret_count', 'obs')}
+    tb.rollout(77, noise=None, carry=False)
+    a_rng = tb.actions.clone()
+    for k, v in snap.items():
+        getattr(tb, k).copy_(v)
+    nz = torch.empty(T, N, spec['act_dim'], device=gpu)
+    _lib.check(_lib.lib().pgm_normal_noise(nz.numel(), 77, C.c_void_p(nz.data_ptr()),
+                                           C.c_void_p(torch.cuda.current_stream().cuda_stream)), 'noise')
+    tb.rollout(77, noise=nz, carry=False)
+    assert torch.equal(a_rng, tb.actions)
+
+
+@pytest.mark.parametrize('env,eval_num,raw', [('MO-Walker2d-v2', 1, True), ('MO-Hopper-v3', 2, False)])
+def test_eval(gpu, env, eval_num, raw):
+    P = 3
+    spec, tb, pols = _batch_with_policies(env, P, 4, 8, seed=5, scale=0.1, eval_num=eval_num, raw=raw)
+    args = small_args(env, eval_num=eval_num, raw=raw)
+    rng = np.random.RandomState(2)
+    rms = []
+    for p in range(P):
+        r = RunningMeanStd(shape=(spec['obs_dim'],))
+        r.update(rng.randn(50, spec['obs_dim']) * 0.3 + 0.1)
+        rms.append(r)
+        tb.set_env_params(p, {'ob_rms': r})
+    objs = tb.evaluate().cpu().numpy()
+    s0_eval = envspec.reset_table(spec['obs_dim'], 0, eval_num)
+    for p in range(P):
+        ref = oracle_evaluation(args, spec, s0_eval, pols[p], rms[p])
+        _close(objs[p], ref, 1e-4, 1e-5, 'evaluation objs')
+
+
+def _noise_fn(T, N, A, E, B):
+    def fn(j):
+        torch.manual_seed(j)
+        noise = torch.stack([torch.normal(torch.zeros(N, A, dtype=torch.float64), torch.ones(N, A, dtype=torch.float64))
+                             for _ in range(T)])
+        perms = [torch.randperm(B) for _ in range(E)]
+        return noise, perms
+    return fn
+
+
+def test_mopg_iterations_end_to_end(gpu):
+    """Two full MOPG iterations (rollout, GAE, scalarised PPO, eval) vs the oracle MOPG_worker."""
+    env, P, N, T, E, M, iters = 'MO-Hopper-v2', 2, 4, 64, 2, 4, 2
+    args = small_args(env, num_steps=T, num_processes=N, ppo_epoch=E, num_mini_batch=M, num_env_steps=T * N * 10)
+    spec = envspec.make_spec(env)
+    A, B = spec['act_dim'], T * N
+    tb = TaskBatch(env, P, num_processes=N, num_steps=T, ppo_epoch=E, num_mini_batch=M)
+    fn = _noise_fn(T, N, A, E, B)
+    w = weights_grid(spec['obj_num'], P)
+    torch.manual_seed(0)
+    samples = [initial_sample(args, spec) for _ in range(P)]
+    for s in samples:
+        with torch.no_grad():
+            for prm in s.actor_critic.parameters():
+                prm.copy_(prm.float().double())
+    for p, s in enumerate(samples):
+        tb.set_task(p, s.actor_critic.state_dict(), {}, s.env_params, w[p])
+    tb.env_reset()
+    total = int(args.num_env_steps) // T // N
+    gpu_objs, gpu_params = [], []
+    for j in range(iters):
+        noise, perms = fn(j)
+        tb.iteration(j, oppo.linear_lr(j, total, args.lr), noise=noise.float(), perms=torch.stack(perms).numpy(),
+                     carry=j > 0)
+        gpu_objs.append(tb.objs.cpu().numpy().copy())
+        gpu_params.append(tb.params.cpu().numpy().copy())
+    s0_train = envspec.reset_table(spec['obs_dim'], 0, N)
+    s0_eval = envspec.reset_table(spec['obs_dim'], 0, 1)
+    for p in range(P):
+        offs = mopg_worker(args, spec, s0_train, s0_eval, samples[p], w[p], 0, iters, noise_fn=fn)
+        for j, off in enumerate(offs):
+            ref = tb.layout.flatten(off.actor_critic.state_dict(), dtype=np.float64)
+            _close(gpu_params[j][p], ref, 2e-5, 1e-4, f'params iter {j}')
+            _close(gpu_objs[j][p], off.objs, 1e-3, 1e-4, f'eval objs iter {j}')

@@ -1,0 +1,184 @@
+#!/usr/bin/env python3
+"""Benchmark of the MOPG hot path on MI355X (BASELINE.json metric, SynthMO-Walker2d pop=40 per GPU).
+
+One *step* = one MOPG iteration for every task on the GPU (morl/mopg.py:95-155): a T x N rollout
+with the fused act + env + VecNormalize kernel, GAE, advantage scalarisation, ppo_epoch x
+num_mini_batch Adam steps, the deterministic evaluation episode, and the generation-boundary
+objective merge (RCCL all-gather of the per-task objective vectors when N > 1).
+Counted env-steps = tasks x num_processes x num_steps per step (eval steps are not counted,
+like the reference's FPS print, morl/mopg.py:159).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+"""
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = 'env steps/sec (whole node) + hypervolume@budget, MO-Walker2d-v2 pop=40'
+PEAK_FP32_TFLOPS = 157.3   # MI355X dense fp32 (vector == f32-input MFMA), MI355X_MICROARCH.md
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=5)
+    ap.add_argument('--warmup', type=int, default=2)
+    ap.add_argument('--env-name', default='MO-Walker2d-v2')
+    ap.add_argument('--tasks', type=int, default=40, help='tasks (policies) per GPU')
+    ap.add_argument('--num-processes', type=int, default=4)
+    ap.add_argument('--num-steps', type=int, default=2048)
+    ap.add_argument('--ppo-epoch', type=int, default=10)
+    ap.add_argument('--num-mini-batch', type=int, default=32)
+    ap.add_argument('--cpu-iters', type=int, default=3, help='oracle iterations timed for cpu_baseline')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--traffic-file', default=os.path.join(ROOT, 'profiles', 'r01_ppo_update_pmc.json'))
+    return ap.parse_args()
+
+
+def mflops_per_row(O, A, K, H=64):
+    """M_f = 2(O*H + H^2) + H*A + H*K multiply-adds per row forward."""
+    return 2 * (O * H + H * H) + H * A + H * K
+
+
+def cpu_baseline(args, spec):
+    """The oracle (fp64 torch restatement, 1 thread like morl/morl.py:34) on one task."""
+    from oracle.mopg import initial_sample, mopg_worker
+    from pgmorl_amd import envspec
+    torch.set_num_threads(1)
+    ns = argparse.Namespace(env_name=args.env_name, obj_num=spec['obj_num'], num_env_steps=10 ** 9, seed=0,
+                            num_steps=args.num_steps, num_processes=args.num_processes, ppo_epoch=args.ppo_epoch,
+                            num_mini_batch=args.num_mini_batch, clip_param=0.2, value_loss_coef=0.5,
+                            entropy_coef=0.0, lr=3e-4, max_grad_norm=0.5, gamma=0.995, gae_lambda=0.95,
+                            use_gae=True, use_proper_time_limits=True, ob_rms=True, obj_rms=True, raw=True,
+                            eval_num=1, use_linear_lr_decay=True, lr_decay_ratio=1.0, layernorm=False)
+    torch.manual_seed(0)
+    sample = initial_sample(ns, spec)
+    s0 = envspec.reset_table(spec['obs_dim'], 0, args.num_processes)
+    s0e = envspec.reset_table(spec['obs_dim'], 0, 1)
+    w = np.array([0.5] * spec['obj_num'])
+    t0 = time.perf_counter()
+    mopg_worker(ns, spec, s0, s0e, sample, w, 0, args.cpu_iters)
+    dt = time.perf_counter() - t0
+    steps = args.cpu_iters * args.num_processes * args.num_steps
+    return {'value': steps / dt, 'unit': 'env steps/sec', 'cores': 1, 'kind': 'port',
+            'sample': f'1 task x {args.cpu_iters} MOPG iterations ({steps} train env-steps, T={args.num_steps}, '
+                      f'N={args.num_processes}, E={args.ppo_epoch}, M={args.num_mini_batch}, + eval) of the fp64 '
+                      f'torch/numpy oracle, torch.set_num_threads(1), {dt:.1f} s on {platform.processor() or "host"}'
+                      f' ({os.cpu_count()} logical CPUs visible)'}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    dev = torch.device('cuda', local)
+    torch.cuda.set_device(dev)
+
+    from pgmorl_amd import envspec
+    from pgmorl_amd.policy import new_policy
+    from pgmorl_amd.runtime import TaskBatch
+    spec = envspec.make_spec(args.env_name)
+    P, N, T, E, M = args.tasks, args.num_processes, args.num_steps, args.ppo_epoch, args.num_mini_batch
+    tb = TaskBatch(args.env_name, P, num_processes=N, num_steps=T, ppo_epoch=E, num_mini_batch=M, device=dev)
+    torch.manual_seed(rank * 1000)
+    w = np.linspace(0, 1, P * world)[rank * P:(rank + 1) * P]
+    for p in range(P):
+        pol = new_policy(spec['obs_dim'], spec['act_dim'], spec['obj_num'])
+        tb.set_task(p, pol.state_dict(), {}, None, [w[p], 1 - w[p]] if spec['obj_num'] == 2 else
+                    np.ones(spec['obj_num']) / spec['obj_num'])
+    tb.env_reset()
+    gathered = torch.zeros(world * P, spec['obj_num'], dtype=torch.float64, device=dev)
+    total_updates = 5_000_000 // T // N
+
+    def step(j):
+        tb.iteration(j, 3e-4 * (1 - j / total_updates), carry=True)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, tb.objs)
+        else:
+            gathered.copy_(tb.objs)
+
+    j = 0
+    for _ in range(args.warmup):
+        step(j)
+        j += 1
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    # per-launch duration of the dominant kernel (ppo_update) with events on the launch stream
+    ev = []
+    orig_update = tb.ppo_update
+
+    def timed_update(perms=None):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        orig_update(perms)
+        e.record()
+        ev.append((s, e))
+
+    tb.ppo_update = timed_update
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(j)
+        j += 1
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    tb.ppo_update = orig_update
+    upd_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    if world > 1:
+        t = torch.tensor([dt, upd_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt, upd_ms = float(t[0]), float(t[1])
+    env_steps = world * P * N * T * args.steps
+    value = env_steps / dt
+    mf = mflops_per_row(spec['obs_dim'], spec['act_dim'], spec['obj_num'])
+    upd_flop = P * T * N * E * 6 * mf          # fwd (2 M_f) + bwd (4 M_f) per row per epoch, one launch
+    achieved = upd_flop / (upd_ms * 1e-3) / 1e12
+    traffic = None
+    if os.path.exists(args.traffic_file):
+        try:
+            tr = json.load(open(args.traffic_file))
+            if tr.get('workload') == f'{args.env_name}/P{P}/N{N}/T{T}/E{E}/M{M}':
+                traffic = tr.get('hbm_bytes_per_launch')
+        except Exception:
+            traffic = None
+    out = {
+        'metric': METRIC, 'value': value, 'unit': 'env steps/sec', 'n_gpus': world, 'steps': args.steps,
+        'warmup': args.warmup, 'ms_per_step': dt / args.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak',
+        'vs_baseline': None, 'dtype': 'fp32', 'data': 'synthetic (SynthMO-Walker2d env, reference-order random init)',
+        'config': {'workload': f'{args.env_name} (SynthMO) pop={P}/GPU, N={N}, T={T}, ppo_epoch={E}, '
+                               f'num_mini_batch={M}, eval_num=1, perf-mode device RNG',
+                   'env': args.env_name, 'tasks_per_gpu': P, 'global_tasks': P * world, 'num_processes': N,
+                   'num_steps': T, 'ppo_epoch': E, 'num_mini_batch': M, 'parallelism': f'task-sharded x{world}'},
+        'roofline': {'bound': 'mfma', 'kernel': 'ppo_update_kernel', 'achieved': achieved, 'peak': PEAK_FP32_TFLOPS,
+                     'unit': 'TFLOP/s', 'frac': achieved / PEAK_FP32_TFLOPS, 'traffic': traffic,
+                     'avg_launch_ms': upd_ms, 'flop_per_launch': upd_flop},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out['cpu_baseline'] = cpu_baseline(args, spec)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

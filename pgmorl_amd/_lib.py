@@ -10,7 +10,7 @@ import os
 import torch  # noqa: F401  (must precede loading libpgm.so)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, 'libpgm.so')
+LIB_PATH = os.environ.get('PGM_LIB') or os.path.join(HERE, 'libpgm.so')
 
 PGM_ABI_VERSION = 1
 PGM_OK, PGM_E_INVALID_ARG, PGM_E_SHAPE, PGM_E_HIP, PGM_E_UNSUPPORTED = 0, -1, -2, -3, -4

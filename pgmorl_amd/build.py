@@ -26,18 +26,22 @@ def _newest(paths):
     return max(os.path.getmtime(p) for p in paths)
 
 
-def build(force=False, verbose=False):
-    os.makedirs(OBJDIR, exist_ok=True)
+def build(force=False, verbose=False, stamps=False):
+    """stamps=True builds the diagnostic libpgm_stamps.so (-DPGM_STAMPS phase timers); never shipped."""
+    objdir = OBJDIR + ('_stamps' if stamps else '')
+    lib = LIB.replace('libpgm.so', 'libpgm_stamps.so') if stamps else LIB
+    flags = FLAGS + (['-DPGM_STAMPS'] if stamps else [])
+    os.makedirs(objdir, exist_ok=True)
     deps = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(ROOT, 'include', 'pgm_abi.h')]
     dep_t = _newest(deps)
     hipcc = _hipcc()
 
     def compile_one(src):
         s = os.path.join(CSRC, src)
-        o = os.path.join(OBJDIR, src + '.o')
+        o = os.path.join(objdir, src + '.o')
         if not force and os.path.exists(o) and os.path.getmtime(o) >= max(os.path.getmtime(s), dep_t):
             return o
-        cmd = [hipcc, *FLAGS, '-c', s, '-o', o]
+        cmd = [hipcc, *flags, '-c', s, '-o', o]
         if verbose:
             print(' '.join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)
@@ -47,15 +51,15 @@ def build(force=False, verbose=False):
 
     with ThreadPoolExecutor(max_workers=min(4, len(SOURCES))) as ex:
         objs = list(ex.map(compile_one, SOURCES))
-    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < _newest(objs):
-        cmd = [hipcc, f'--offload-arch={ARCH}', '-shared', '-fPIC', *objs, '-o', LIB]
+    if force or not os.path.exists(lib) or os.path.getmtime(lib) < _newest(objs):
+        cmd = [hipcc, f'--offload-arch={ARCH}', '-shared', '-fPIC', *objs, '-o', lib]
         if verbose:
             print(' '.join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f'hipcc link failed:\n{r.stdout}\n{r.stderr}')
-    return LIB
+    return lib
 
 
 if __name__ == '__main__':
-    print(build(force='--force' in sys.argv, verbose=True))
+    print(build(force='--force' in sys.argv, verbose=True, stamps='--stamps' in sys.argv))

@@ -65,3 +65,4 @@ int pgm_param_layout(int32_t O, int32_t A, int32_t K, int32_t H, int32_t* offset
 }
 
 }  // extern "C"
+

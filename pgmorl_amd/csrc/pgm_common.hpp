@@ -55,3 +55,37 @@ __device__ __forceinline__ float counter_normal(uint64_t seed, uint64_t i) {
 }
 
 }  // namespace pgm
+
+// ---------------------------------------------------------------- diagnostic phase stamps
+// Built only into libpgm_stamps.so (-DPGM_STAMPS): workgroup 0 / thread 0 accumulates s_memtime
+// deltas per phase id into pgm_stamp_acc; read back with pgm_debug_stamps().  Never in the shipped .so.
+#ifdef PGM_STAMPS
+// one accumulator array + reader per translation unit (no relocatable device code)
+#define PGM_STAMP_UNIT(name)                                                                          \
+    static __device__ unsigned long long pgm_stamp_acc[64];                                           \
+    extern "C" int pgm_debug_stamps_##name(unsigned long long* out, int reset) {                      \
+        if (hipMemcpyFromSymbol(out, HIP_SYMBOL(pgm_stamp_acc), sizeof(unsigned long long) * 64) !=  \
+            hipSuccess)                                                                               \
+            return PGM_E_HIP;                                                                         \
+        if (reset) {                                                                                  \
+            unsigned long long z[64] = {0};                                                           \
+            if (hipMemcpyToSymbol(HIP_SYMBOL(pgm_stamp_acc), z, sizeof(z)) != hipSuccess) return PGM_E_HIP; \
+        }                                                                                             \
+        return PGM_OK;                                                                                \
+    }
+#define PGM_STAMP_DECL unsigned long long pgm_stamp_last = __builtin_amdgcn_s_memtime();
+#define PGM_STAMP(id)                                                            \
+    do {                                                                         \
+        if (blockIdx.x == 0 && threadIdx.x == 0) {                               \
+            unsigned long long now_ = __builtin_amdgcn_s_memtime();              \
+            atomicAdd(&pgm_stamp_acc[id], now_ - pgm_stamp_last);              \
+            pgm_stamp_last = now_;                                               \
+        }                                                                        \
+    } while (0)
+#else
+#define PGM_STAMP_UNIT(name)
+#define PGM_STAMP_DECL
+#define PGM_STAMP(id) \
+    do {              \
+    } while (0)
+#endif

@@ -1,6 +1,8 @@
 // Policy forward, synthetic env + VecNormalize, the fused rollout and the deterministic
 // evaluation.  One workgroup (256 threads) per task; everything a task touches per step lives
-// in LDS, so a T-step rollout is one launch with only workgroup barriers (tasks never interact).
+// in LDS (weights, env constants, env state, running statistics, the current obs rows), so a
+// T-step rollout is one launch whose steps synchronise with LDS-only barriers: the per-step
+// rollout-storage stores to HBM stay in flight across barriers instead of being drained.
 //
 // Reference semantics (paths relative to the reference tree):
 //   Policy.act / get_value                 a2c_ppo_acktr/model.py:57-73, 237-246
@@ -14,6 +16,8 @@
 //   evaluation()                           morl/mopg.py:25-46
 #include "pgm_dispatch.hpp"
 
+PGM_STAMP_UNIT(rollout)
+
 namespace pgm {
 
 constexpr int NMAX = 8;    // envs per task handled by one workgroup
@@ -23,6 +27,12 @@ template <int O>
 constexpr int opad() { return (O + 3) & ~3; }
 template <int O>
 constexpr bool w1_in_lds() { return O <= 128; }
+template <int O>
+constexpr bool spec_in_lds() { return O <= 128; }
+
+// LDS-only barrier: waits for this wave's LDS traffic, not for its outstanding HBM stores
+// (__syncthreads() would also drain vmcnt, i.e. wait for every rollout-storage store).
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // ------------------------------------------------------------------------------------------
 // LDS images
@@ -46,15 +56,23 @@ struct PolSmem {
 };
 
 template <int O, int A, int K>
+struct SpecSmem {  // fp64 env constants (only for O <= 128; Humanoid reads them from HBM/L2)
+    static constexpr int OL = spec_in_lds<O>() ? O : 1;
+    double U[OL][A], V[K][OL], d[OL], c[OL], s0[NMAX][OL];
+    double ebase[K], ecoef[K], lo[A], hi[A];
+};
+
+template <int O, int A, int K>
 struct EnvSmem {
+    SpecSmem<O, A, K> sp;
     double s[NMAX][O];        // env state
     double snew[NMAX][O];     // observation returned by step (post auto-reset)
     double ac[NMAX][A];       // clipped action
     double objraw[NMAX][K];   // info['obj'] before obj_rms scaling
     double obj_acc[NMAX][K];  // VecNormalize.obj
     double ret[NMAX];         // VecNormalize.ret
-    double ob_mean[O], ob_var[O];
-    double obj_mean[K], obj_var[K];
+    double ob_mean[O], ob_var[O], ob_inv[O];
+    double obj_mean[K], obj_var[K], obj_inv[K];
     double ob_count, obj_count, ret_mean, ret_var, ret_count;
     double objsum[K];         // evaluation accumulator
     int elapsed[NMAX], done[NMAX], bad[NMAX];
@@ -67,6 +85,45 @@ struct NormCfg {
 };
 __host__ __device__ inline NormCfg norm_cfg(const pgm_norm_state& ns) {
     return NormCfg{ns.gamma, ns.clipob, ns.cliprew, ns.epsilon, ns.use_ob_rms, ns.use_obj_rms};
+}
+
+// env-constant accessors: LDS copy when it fits, HBM otherwise
+template <int O, int A, int K>
+struct Spec {
+    const EnvSmem<O, A, K>& E;
+    const pgm_env_spec& g;
+    const double* s0g;
+    __device__ double U(int o, int a) const { if constexpr (spec_in_lds<O>()) return E.sp.U[o][a]; else return g.U[o * A + a]; }
+    __device__ double V(int k, int o) const { if constexpr (spec_in_lds<O>()) return E.sp.V[k][o]; else return g.V[k * O + o]; }
+    __device__ double d(int o) const { if constexpr (spec_in_lds<O>()) return E.sp.d[o]; else return g.d[o]; }
+    __device__ double c(int o) const { if constexpr (spec_in_lds<O>()) return E.sp.c[o]; else return g.c[o]; }
+    __device__ double s0(int n, int o) const { if constexpr (spec_in_lds<O>()) return E.sp.s0[n][o]; else return s0g[n * O + o]; }
+    __device__ double ebase(int k) const { return E.sp.ebase[k]; }
+    __device__ double ecoef(int k) const { return E.sp.ecoef[k]; }
+    __device__ double lo(int a) const { return E.sp.lo[a]; }
+    __device__ double hi(int a) const { return E.sp.hi[a]; }
+};
+
+template <int O, int A, int K>
+__device__ void load_spec(EnvSmem<O, A, K>& E, const pgm_env_spec& g, const double* s0, int N) {
+    const int t = threadIdx.x;
+    if constexpr (spec_in_lds<O>()) {
+        for (int i = t; i < O * A; i += RT) E.sp.U[i / A][i % A] = g.U[i];
+        for (int i = t; i < K * O; i += RT) E.sp.V[i / O][i % O] = g.V[i];
+        for (int i = t; i < O; i += RT) {
+            E.sp.d[i] = g.d[i];
+            E.sp.c[i] = g.c[i];
+        }
+        for (int i = t; i < N * O; i += RT) E.sp.s0[i / O][i % O] = s0[i];
+    }
+    if (t < K) {
+        E.sp.ebase[t] = g.ebase[t];
+        E.sp.ecoef[t] = g.ecoef[t];
+    }
+    if (t < A) {
+        E.sp.lo[t] = g.act_lo[t];
+        E.sp.hi[t] = g.act_hi[t];
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -108,6 +165,7 @@ __device__ void policy_forward(PolSmem<O, A, K>& S, int N, const float* __restri
 #pragma unroll
         for (int i = 0; i < RPT; ++i) acc[i] = b;
         const float* gw = prm + (c < H ? L.off[PGM_P_CRITIC_W1] : L.off[PGM_P_ACTOR_W1]) + (c & (H - 1));
+#pragma unroll 4
         for (int k = 0; k < O; ++k) {
             float w;
             if constexpr (w1_in_lds<O>()) w = S.W1t[k][c];
@@ -120,13 +178,15 @@ __device__ void policy_forward(PolSmem<O, A, K>& S, int N, const float* __restri
         for (int i = 0; i < RPT; ++i)
             if (rg + 2 * i < N) S.h1[rg + 2 * i][c] = tanh_f(acc[i]);
     }
-    __syncthreads();
+    lds_sync();
+    PGM_STAMP_DECL
     {   // tower layer 2
         const int m = c >> 6, j = c & (H - 1);
         float acc[RPT];
         const float b = S.b2[c];
 #pragma unroll
         for (int i = 0; i < RPT; ++i) acc[i] = b;
+#pragma unroll 8
         for (int k = 0; k < H; ++k) {
             const float w = S.W2t[m][k][j];
 #pragma unroll
@@ -137,7 +197,8 @@ __device__ void policy_forward(PolSmem<O, A, K>& S, int N, const float* __restri
         for (int i = 0; i < RPT; ++i)
             if (rg + 2 * i < N) S.h2[rg + 2 * i][c] = tanh_f(acc[i]);
     }
-    __syncthreads();
+    lds_sync();
+    PGM_STAMP(10);
     {   // heads: 8 lanes per output dot
         const int sub = t & 7;
         const int nout = N * (K + A);
@@ -158,7 +219,7 @@ __device__ void policy_forward(PolSmem<O, A, K>& S, int N, const float* __restri
             }
         }
     }
-    __syncthreads();
+    lds_sync();
 }
 
 // ------------------------------------------------------------------------------------------
@@ -166,7 +227,7 @@ __device__ void policy_forward(PolSmem<O, A, K>& S, int N, const float* __restri
 template <int O, int A, int K>
 __device__ void load_env(EnvSmem<O, A, K>& E, const pgm_env_state& st, const pgm_norm_state& ns, int p, int N) {
     const int t = threadIdx.x;
-    for (int i = t; i < N * O; i += RT) (&E.s[0][0])[i] = st.s[(size_t)p * N * O + i];
+    for (int i = t; i < N * O; i += RT) E.s[i / O][i % O] = st.s[(size_t)p * N * O + i];
     for (int i = t; i < N * K; i += RT) E.obj_acc[i / K][i % K] = st.obj_acc[(size_t)p * N * K + i];
     if (t < N) {
         E.elapsed[t] = st.elapsed[p * N + t];
@@ -193,7 +254,7 @@ __device__ void load_env(EnvSmem<O, A, K>& E, const pgm_env_state& st, const pgm
 template <int O, int A, int K>
 __device__ void store_env(const EnvSmem<O, A, K>& E, const pgm_env_state& st, const pgm_norm_state& ns, int p, int N) {
     const int t = threadIdx.x;
-    for (int i = t; i < N * O; i += RT) st.s[(size_t)p * N * O + i] = (&E.s[0][0])[i];
+    for (int i = t; i < N * O; i += RT) st.s[(size_t)p * N * O + i] = E.s[i / O][i % O];
     for (int i = t; i < N * K; i += RT) st.obj_acc[(size_t)p * N * K + i] = E.obj_acc[i / K][i % K];
     if (t < N) {
         st.elapsed[p * N + t] = E.elapsed[t];
@@ -227,52 +288,55 @@ __device__ __forceinline__ void chan_merge(double& mean, double& var, double cou
     var = m2 / tot;
 }
 
-// s' = tanh(d*s + U a_c + c); objectives; time limit; DummyVecEnv auto-reset to s0.
-// Needs E.ac filled and E.s current.  Ends with a barrier.
+__device__ __forceinline__ double clipd(double x, double lo, double hi) { return fmin(fmax(x, lo), hi); }
+
+// s' = tanh(d*s + U a_c + c); objectives; time limit (E.ac filled, E.s current).  Two barriers.
 template <int O, int A, int K>
-__device__ void env_dynamics(EnvSmem<O, A, K>& E, int N, const pgm_env_spec& sp, const double* __restrict__ s0) {
+__device__ void env_dynamics(EnvSmem<O, A, K>& E, const Spec<O, A, K>& sp, int N, int max_steps) {
     const int t = threadIdx.x;
     for (int i = t; i < N * O; i += RT) {
         const int n = i / O, o = i % O;
         double ua = 0.0;
 #pragma unroll
-        for (int a = 0; a < A; ++a) ua += sp.U[o * A + a] * E.ac[n][a];
-        E.snew[n][o] = tanh(sp.d[o] * E.s[n][o] + ua + sp.c[o]);
+        for (int a = 0; a < A; ++a) ua += sp.U(o, a) * E.ac[n][a];
+        E.snew[n][o] = tanh(sp.d(o) * E.s[n][o] + ua + sp.c(o));
     }
-    __syncthreads();
+    lds_sync();
     for (int i = t; i < N * K; i += RT) {
         const int n = i / K, k = i % K;
         double v = 0.0, e2 = 0.0;
-        for (int o = 0; o < O; ++o) v += sp.V[k * O + o] * E.snew[n][o];
+        for (int o = 0; o < O; ++o) v += sp.V(k, o) * E.snew[n][o];
 #pragma unroll
         for (int a = 0; a < A; ++a) e2 += E.ac[n][a] * E.ac[n][a];
-        E.objraw[n][k] = v + sp.ebase[k] - sp.ecoef[k] * e2;
+        E.objraw[n][k] = v + sp.ebase(k) - sp.ecoef(k) * e2;
     }
-    if (t < N) {
-        const int el = E.elapsed[t] + 1;
-        const int d = el >= sp.max_episode_steps;
-        E.done[t] = d;
-        E.bad[t] = d && (el == sp.max_episode_steps);
-        E.elapsed[t] = d ? 0 : el;
+    if (t >= RT - N) {
+        const int n = t - (RT - N);
+        const int el = E.elapsed[n] + 1;
+        const int d = el >= max_steps;
+        E.done[n] = d;
+        E.bad[n] = d && (el == max_steps);
+        E.elapsed[n] = d ? 0 : el;
     }
-    __syncthreads();
-    for (int i = t; i < N * O; i += RT) {
-        const int n = i / O, o = i % O;
-        if (E.done[n]) E.snew[n][o] = s0[n * O + o];
-        E.s[n][o] = E.snew[n][o];
-    }
-    __syncthreads();
+    lds_sync();
 }
 
-// VecNormalize.step_wait statistics (ob_rms, obj accumulators + obj_rms, ret_rms).  Ends with a barrier.
+// Auto-reset + VecNormalize statistics: ob_rms on feature threads (bottom of the block), obj
+// accumulators + obj_rms on objective threads (top), ret_rms on one thread; all with the counts
+// from before this step (they advance in vecnorm_emit).  One barrier.
 template <int O, int A, int K>
-__device__ void vecnorm_stats(EnvSmem<O, A, K>& E, int N, const NormCfg& nc) {
+__device__ void vecnorm_stats(EnvSmem<O, A, K>& E, const Spec<O, A, K>& sp, int N, const NormCfg& nc) {
     const int t = threadIdx.x;
     const double dn = (double)N;
-    if (nc.use_ob) {
-        for (int o = t; o < O; o += RT) {
-            double sum = 0.0;
-            for (int n = 0; n < N; ++n) sum += E.snew[n][o];
+    for (int o = t; o < O; o += RT) {
+        double sum = 0.0;
+        for (int n = 0; n < N; ++n) {
+            const double v = E.done[n] ? sp.s0(n, o) : E.snew[n][o];
+            E.snew[n][o] = v;
+            E.s[n][o] = v;
+            sum += v;
+        }
+        if (nc.use_ob) {
             const double bm = sum / dn;
             double sq = 0.0;
             for (int n = 0; n < N; ++n) {
@@ -280,9 +344,11 @@ __device__ void vecnorm_stats(EnvSmem<O, A, K>& E, int N, const NormCfg& nc) {
                 sq += dd * dd;
             }
             chan_merge(E.ob_mean[o], E.ob_var[o], E.ob_count, bm, sq / dn, dn);
+            E.ob_inv[o] = 1.0 / sqrt(E.ob_var[o] + nc.eps);
         }
     }
-    for (int k = t; k < K; k += RT) {
+    const int k = RT - 1 - t;
+    if (k < K) {
         for (int n = 0; n < N; ++n)
             E.obj_acc[n][k] = E.obj_valid ? E.obj_acc[n][k] * nc.gamma + E.objraw[n][k] : E.objraw[n][k];
         if (nc.use_obj) {
@@ -295,9 +361,10 @@ __device__ void vecnorm_stats(EnvSmem<O, A, K>& E, int N, const NormCfg& nc) {
                 sq += dd * dd;
             }
             chan_merge(E.obj_mean[k], E.obj_var[k], E.obj_count, bm, sq / dn, dn);
+            E.obj_inv[k] = 1.0 / sqrt(E.obj_var[k] + nc.eps);
         }
     }
-    if (t == RT - 1) {  // ret_rms on the (always zero-reward) discounted return, vec_normalize.py:32,41-43
+    if (t == RT - 1 - K) {  // ret_rms on the (always zero-reward) discounted return, vec_normalize.py:32,41-43
         double sum = 0.0;
         for (int n = 0; n < N; ++n) {
             E.ret[n] = E.ret[n] * nc.gamma + 0.0;
@@ -309,19 +376,11 @@ __device__ void vecnorm_stats(EnvSmem<O, A, K>& E, int N, const NormCfg& nc) {
         chan_merge(E.ret_mean, E.ret_var, E.ret_count, bm, sq / dn, dn);
         E.ret_count += dn;
     }
-    __syncthreads();
-    if (t == 0) {
-        if (nc.use_ob) E.ob_count += dn;
-        if (nc.use_obj) E.obj_count += dn;
-        E.obj_valid = 1;
-    }
-    __syncthreads();
+    lds_sync();
 }
 
-__device__ __forceinline__ double clipd(double x, double lo, double hi) { return fmin(fmax(x, lo), hi); }
-
-// Writes the normalised fp32 obs (into xs rows and obs_out), scaled objectives, masks; zeroes the
-// accumulators of done envs.  Ends with a barrier.
+// Normalised fp32 obs (-> xs rows and obs_out), scaled objectives, masks; zero the accumulators of
+// done envs; advance the counts.  One barrier.
 template <int O, int A, int K, int XS>
 __device__ void vecnorm_emit(EnvSmem<O, A, K>& E, int N, const NormCfg& nc, float (*xs)[XS], float* obs_out,
                              float* rew_out, float* mask_out, float* bad_out) {
@@ -329,26 +388,48 @@ __device__ void vecnorm_emit(EnvSmem<O, A, K>& E, int N, const NormCfg& nc, floa
     for (int i = t; i < N * O; i += RT) {
         const int n = i / O, o = i % O;
         double v = E.snew[n][o];
-        if (nc.use_ob) v = clipd((v - E.ob_mean[o]) / sqrt(E.ob_var[o] + nc.eps), -nc.clipob, nc.clipob);
+        if (nc.use_ob) v = clipd((v - E.ob_mean[o]) * E.ob_inv[o], -nc.clipob, nc.clipob);
         const float f = (float)v;  // VecPyTorch .float() (envs.py:192)
         xs[n][o] = f;
         if (obs_out) obs_out[i] = f;
     }
-    for (int i = t; i < N * K; i += RT) {
+    const int i = RT - 1 - t;
+    if (i < N * K) {
         const int n = i / K, k = i % K;
         double r = E.objraw[n][k];
-        if (nc.use_obj) r = clipd(r / sqrt(E.obj_var[k] + nc.eps), -nc.cliprew, nc.cliprew);
+        if (nc.use_obj) r = clipd(r * E.obj_inv[k], -nc.cliprew, nc.cliprew);
         if (rew_out) rew_out[i] = (float)r;
+        if (E.done[n]) E.obj_acc[n][k] = 0.0;
     }
-    __syncthreads();
-    if (t < N) {
-        if (mask_out) mask_out[t] = E.done[t] ? 0.f : 1.f;
-        if (bad_out) bad_out[t] = E.bad[t] ? 0.f : 1.f;
-        if (E.done[t]) E.ret[t] = 0.0;
+    const int n = RT - 1 - N * K - t;
+    if (n >= 0 && n < N) {
+        if (mask_out) mask_out[n] = E.done[n] ? 0.f : 1.f;
+        if (bad_out) bad_out[n] = E.bad[n] ? 0.f : 1.f;
+        if (E.done[n]) E.ret[n] = 0.0;
     }
-    for (int i = t; i < N * K; i += RT)
-        if (E.done[i / K]) E.obj_acc[i / K][i % K] = 0.0;
-    __syncthreads();
+    if (t == 0) {
+        if (nc.use_ob) E.ob_count += (double)N;
+        if (nc.use_obj) E.obj_count += (double)N;
+        E.obj_valid = 1;
+    }
+    lds_sync();
+}
+
+// Draw actions (torch.normal(mean, std) = z*std + mean), log-prob terms, clipped env action.
+template <int O, int A, int K>
+__device__ void sample_actions(PolSmem<O, A, K>& P, EnvSmem<O, A, K>& E, const Spec<O, A, K>& sp, int N, float eps,
+                               float* act_out) {
+    const int t = threadIdx.x;
+    if (t < N * A) {
+        const int n = t / A, j = t % A;
+        const float mu = P.mu[n][j], ls = P.logstd[j], sd = expf(ls);
+        const float av = fmaf(eps, sd, mu);
+        const float dz = (av - mu) / sd;
+        P.lp[n][j] = -0.5f * dz * dz - ls - LOG_SQRT_2PI;
+        if (act_out) act_out[t] = av;
+        E.ac[n][j] = clipd((double)av, sp.lo(j), sp.hi(j));
+    }
+    lds_sync();
 }
 
 // ------------------------------------------------------------------------------------------
@@ -413,48 +494,49 @@ __global__ __launch_bounds__(RT) void env_kernel(EnvArgs a) {
     auto& E = S.env;
     const int p = blockIdx.x, t = threadIdx.x, N = a.N;
     const NormCfg nc = norm_cfg(a.ns);
+    const Spec<O, A, K> sp{E, a.spec, a.st.s0};
+    load_spec(E, a.spec, a.st.s0, N);
     load_env(E, a.st, a.ns, p, N);
     __syncthreads();
     if (a.reset) {  // fresh make_vec_envs + reset(): vec_normalize.py:10-27,63-66
-        for (int i = t; i < N * O; i += RT) {
-            const double v = a.st.s0[i];
-            (&E.s[0][0])[i] = v;
-            (&E.snew[0][0])[i] = v;
-        }
         if (t < N) {
             E.elapsed[t] = 0;
             E.ret[t] = 0.0;
         }
         if (t == 0) E.obj_valid = 0;
-        __syncthreads();
-        if (nc.use_ob) {
-            const double dn = (double)N;
-            for (int o = t; o < O; o += RT) {
-                double sum = 0.0;
-                for (int n = 0; n < N; ++n) sum += E.snew[n][o];
+        const double dn = (double)N;
+        for (int o = t; o < O; o += RT) {
+            double sum = 0.0;
+            for (int n = 0; n < N; ++n) {
+                const double v = sp.s0(n, o);
+                E.snew[n][o] = v;
+                E.s[n][o] = v;
+                sum += v;
+            }
+            if (nc.use_ob) {
                 const double bm = sum / dn;
                 double sq = 0.0;
                 for (int n = 0; n < N; ++n) sq += (E.snew[n][o] - bm) * (E.snew[n][o] - bm);
                 chan_merge(E.ob_mean[o], E.ob_var[o], E.ob_count, bm, sq / dn, dn);
+                E.ob_inv[o] = 1.0 / sqrt(E.ob_var[o] + nc.eps);
             }
-            __syncthreads();
-            if (t == 0) E.ob_count += dn;
-            __syncthreads();
         }
+        __syncthreads();
+        if (t == 0 && nc.use_ob) E.ob_count += dn;
         for (int i = t; i < N * O; i += RT) {
             const int o = i % O;
-            double v = (&E.snew[0][0])[i];
-            if (nc.use_ob) v = clipd((v - E.ob_mean[o]) / sqrt(E.ob_var[o] + nc.eps), -nc.clipob, nc.clipob);
+            double v = E.snew[i / O][o];
+            if (nc.use_ob) v = clipd((v - E.ob_mean[o]) * E.ob_inv[o], -nc.clipob, nc.clipob);
             a.obs_out[(size_t)p * N * O + i] = (float)v;
         }
     } else {
         for (int i = t; i < N * A; i += RT) {
             const int j = i % A;
-            E.ac[i / A][j] = clipd((double)a.action[(size_t)p * N * A + i], a.spec.act_lo[j], a.spec.act_hi[j]);
+            E.ac[i / A][j] = clipd((double)a.action[(size_t)p * N * A + i], sp.lo(j), sp.hi(j));
         }
         __syncthreads();
-        env_dynamics(E, N, a.spec, a.st.s0);
-        vecnorm_stats(E, N, nc);
+        env_dynamics(E, sp, N, a.spec.max_episode_steps);
+        vecnorm_stats(E, sp, N, nc);
         vecnorm_emit<O, A, K, opad<O>()>(E, N, nc, S.pol.x, a.obs_out + (size_t)p * N * O,
                                          a.rew_out + (size_t)p * N * K, a.mask_out + (size_t)p * N,
                                          a.bad_out + (size_t)p * N);
@@ -484,6 +566,7 @@ __global__ __launch_bounds__(RT) void rollout_kernel(RolloutArgs a) {
     auto& E = S.env;
     const int p = blockIdx.x, t = threadIdx.x, N = a.N, T = a.T;
     const NormCfg nc = norm_cfg(a.ns);
+    const Spec<O, A, K> sp{E, a.spec, a.st.s0};
     const float* prm = a.params + (size_t)p * a.L.total;
     float* obs = a.rb.obs + (size_t)p * (T + 1) * N * O;
     float* act = a.rb.actions + (size_t)p * T * N * A;
@@ -494,47 +577,53 @@ __global__ __launch_bounds__(RT) void rollout_kernel(RolloutArgs a) {
     float* bad = a.rb.bad_masks + (size_t)p * (T + 1) * N;
 
     load_policy(P, prm, a.L);
+    load_spec(E, a.spec, a.st.s0, N);
     load_env(E, a.st, a.ns, p, N);
-    if (a.carry) {  // after_update(): slot T -> slot 0 (storage.py:71-75)
+    if (a.carry) {  // after_update(): slot T -> slot 0 (storage.py:71-75); each thread re-reads its own writes
         for (int i = t; i < N * O; i += RT) obs[i] = obs[(size_t)T * N * O + i];
         if (t < N) {
             masks[t] = masks[(size_t)T * N + t];
             bad[t] = bad[(size_t)T * N + t];
         }
-        // each thread re-reads only the obs[0] elements it wrote itself
     }
     for (int i = t; i < N * O; i += RT) P.x[i / O][i % O] = obs[i];
     __syncthreads();
 
+    // the lane drawing (n, a) of each step keeps its noise one step ahead in a register
+    const bool drawer = t < N * A;
+    float eps_next = 0.f;
+    if (drawer) eps_next = a.noise ? a.noise[t] : counter_normal(a.seed, (uint64_t)t);
+    PGM_STAMP_DECL
     for (int step = 0; step < T; ++step) {
-        policy_forward(P, N, prm, a.L);
-        for (int i = t; i < N * K; i += RT) val[(size_t)step * N * K + i] = P.val[i / K][i % K];
-        for (int i = t; i < N * A; i += RT) {
-            const int n = i / A, j = i % A;
-            const size_t idx = (size_t)step * N * A + i;
-            const float eps = a.noise ? a.noise[idx] : counter_normal(a.seed, idx);
-            const float mu = P.mu[n][j], ls = P.logstd[j], sd = expf(ls);
-            const float av = fmaf(eps, sd, mu);  // torch.normal(mean, std) = z*std + mean
-            const float dz = (av - mu) / sd;
-            P.lp[n][j] = -0.5f * dz * dz - ls - LOG_SQRT_2PI;
-            act[idx] = av;
-            E.ac[n][j] = clipd((double)av, a.spec.act_lo[j], a.spec.act_hi[j]);
+        const float eps = eps_next;
+        if (drawer && step + 1 < T) {
+            const size_t idx = (size_t)(step + 1) * N * A + t;
+            eps_next = a.noise ? a.noise[idx] : counter_normal(a.seed, idx);
         }
-        __syncthreads();
+        PGM_STAMP(0);
+        policy_forward(P, N, prm, a.L);
+        PGM_STAMP(1);
+        for (int i = t; i < N * K; i += RT) val[(size_t)step * N * K + i] = P.val[i / K][i % K];
+        sample_actions(P, E, sp, N, eps, act + (size_t)step * N * A);
+        PGM_STAMP(2);
         if (t < N) {
             float s = 0.f;
             for (int j = 0; j < A; ++j) s += P.lp[t][j];
             logp[(size_t)step * N + t] = s;
         }
-        env_dynamics(E, N, a.spec, a.st.s0);
-        vecnorm_stats(E, N, nc);
+        env_dynamics(E, sp, N, a.spec.max_episode_steps);
+        PGM_STAMP(3);
+        vecnorm_stats(E, sp, N, nc);
+        PGM_STAMP(4);
         vecnorm_emit<O, A, K, opad<O>()>(E, N, nc, P.x, obs + (size_t)(step + 1) * N * O,
                                          rew + (size_t)step * N * K, masks + (size_t)(step + 1) * N,
                                          bad + (size_t)(step + 1) * N);
+        PGM_STAMP(5);
     }
     // bootstrap value (mopg.py:132-135) -> value_preds[T] (storage.py:85)
     policy_forward(P, N, prm, a.L);
     for (int i = t; i < N * K; i += RT) val[(size_t)T * N * K + i] = P.val[i / K][i % K];
+    __syncthreads();
     store_env(E, a.st, a.ns, p, N);
 }
 
@@ -555,41 +644,43 @@ __global__ __launch_bounds__(RT) void eval_kernel(EvalArgs a) {
     auto& S = *reinterpret_cast<StepSmem<O, A, K>*>(smem_raw);
     auto& P = S.pol;
     auto& E = S.env;
-    double* objsum = E.objsum;
     const int p = blockIdx.x, t = threadIdx.x;
     const float* prm = a.params + (size_t)p * a.L.total;
     load_policy(P, prm, a.L);
-    for (int o = t; o < O; o += RT) {
-        E.ob_mean[o] = a.ob_mean[(size_t)p * O + o];
-        E.ob_var[o] = a.ob_var[(size_t)p * O + o];
+    load_spec(E, a.spec, a.s0_eval, 1);
+    for (int o = t; o < O; o += RT) {  // mopg.py:37-38: fp64 normalisation with fixed eps/clip
+        E.ob_mean[o] = a.use_ob ? a.ob_mean[(size_t)p * O + o] : 0.0;
+        E.ob_inv[o] = a.use_ob ? 1.0 / sqrt(a.ob_var[(size_t)p * O + o] + 1e-8) : 1.0;
     }
-    if (t < K) objsum[t] = 0.0;
+    if (t < K) E.objsum[t] = 0.0;
     __syncthreads();
     for (int e = 0; e < a.eval_num; ++e) {
         const double* s0 = a.s0_eval + (size_t)e * O;
+        const Spec<O, A, K> sp{E, a.spec, s0};
         for (int o = t; o < O; o += RT) E.s[0][o] = s0[o];
         if (t == 0) E.elapsed[0] = 0;
         double g = 1.0;
         __syncthreads();
         while (true) {
-            for (int o = t; o < O; o += RT) {  // mopg.py:37-38 (fp64 normalisation, no fp32 round of the env obs)
+            for (int o = t; o < O; o += RT) {  // obs is NOT rounded through fp32 before normalising
                 double v = E.s[0][o];
-                if (a.use_ob) v = clipd((v - E.ob_mean[o]) / sqrt(E.ob_var[o] + 1e-8), -10.0, 10.0);
+                if (a.use_ob) v = clipd((v - E.ob_mean[o]) * E.ob_inv[o], -10.0, 10.0);
                 P.x[0][o] = (float)v;
             }
-            __syncthreads();
+            lds_sync();
             policy_forward(P, 1, prm, a.L);
-            if (t < A) E.ac[0][t] = clipd((double)P.mu[0][t], a.spec.act_lo[t], a.spec.act_hi[t]);
-            __syncthreads();
-            env_dynamics(E, 1, a.spec, s0);
-            if (t < K) objsum[t] += g * E.objraw[0][t];
+            if (t < A) E.ac[0][t] = clipd((double)P.mu[0][t], sp.lo(t), sp.hi(t));
+            lds_sync();
+            env_dynamics(E, sp, 1, a.spec.max_episode_steps);
+            if (t < K) E.objsum[t] += g * E.objraw[0][t];
             if (!a.raw) g *= a.gamma;
             const int done = E.done[0];
-            __syncthreads();
+            for (int o = t; o < O; o += RT) E.s[0][o] = E.snew[0][o];
+            lds_sync();
             if (done) break;
         }
     }
-    if (t < K) a.objs[(size_t)p * K + t] = objsum[t] / (double)a.eval_num;
+    if (t < K) a.objs[(size_t)p * K + t] = E.objsum[t] / (double)a.eval_num;
 }
 
 // ------------------------------------------------------------------------------------------

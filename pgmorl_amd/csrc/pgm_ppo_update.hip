@@ -14,6 +14,8 @@
 // torch.min / torch.max / clamp backward (ties split the gradient in half) are reproduced exactly.
 #include "pgm_dispatch.hpp"
 
+PGM_STAMP_UNIT(update)
+
 namespace pgm {
 
 constexpr int UT = 512;  // threads: column c = t & 127 (critic < 64 <= actor), row group g = t >> 7
@@ -33,9 +35,9 @@ struct UpdSmem {
     float Wv[H][K];
     float Wm[H][A];
     float bv[K], bm[A], logstd[A];
-    float X[UR][upad<O>()];
-    float H1[UR][H2];   // tanh(layer 1), then dZ1; reused as reduction scratch at minibatch end
-    float H2[UR][H2];   // tanh(layer 2), then dZ2
+    alignas(16) float X[UR][upad<O>()];
+    alignas(16) float H1[UR][H2];   // tanh(layer 1), then dZ1; reused as reduction scratch at minibatch end
+    alignas(16) float H2[UR][H2];   // tanh(layer 2), then dZ2
     float act[UR][A];
     float dls[UR][A];
     float mu[UR][A];    // action mean, then dL/dmu
@@ -58,11 +60,14 @@ struct UpdArgs {
     float* stats;
 };
 
+// LDS-only barrier: HBM stores (Adam state) stay in flight; every HBM re-read is by the writing thread
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 __device__ __forceinline__ float block_sum_f(float x, float* red) {
     x = group_sum<64>(x);
-    __syncthreads();
+    lds_sync();
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = x;
-    __syncthreads();
+    lds_sync();
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < UT / 64; ++i) s += red[i];
@@ -166,6 +171,7 @@ __global__ __launch_bounds__(UT) void ppo_update_kernel(UpdArgs a) {
     float st_v = 0.f, st_a = 0.f, st_e = 0.f;
     int nstep = 0;
 
+    PGM_STAMP_DECL
     for (int e = 0; e < E; ++e) {
         const int32_t* perm = a.perms + (size_t)e * B;
         for (int bb = 0; bb < nb; ++bb) {
@@ -201,39 +207,57 @@ __global__ __launch_bounds__(UT) void ppo_update_kernel(UpdArgs a) {
                         S.ret[r][q] = ok ? returns[(size_t)idx * K + q] : 0.f;
                     }
                 }
-                __syncthreads();
+                lds_sync();
+                PGM_STAMP(20);
                 // ---- layer 1 forward
                 {
                     float acc[UG];
                     const float bias = S.b1[c];
 #pragma unroll
                     for (int i = 0; i < UG; ++i) acc[i] = bias;
-#pragma unroll 2
-                    for (int k = 0; k < O; ++k) {
-                        const float w = S.W1t[k][c];
+#pragma unroll 1
+                    for (int k = 0; k < OP; k += 4) {  // X rows are zero-padded to OP
+                        float w[4];
 #pragma unroll
-                        for (int i = 0; i < UG; ++i) acc[i] = fmaf(S.X[g * UG + i][k], w, acc[i]);
+                        for (int kk = 0; kk < 4; ++kk) w[kk] = (k + kk < O) ? S.W1t[k + kk][c] : 0.f;
+#pragma unroll
+                        for (int i = 0; i < UG; ++i) {
+                            const float4 x = *reinterpret_cast<const float4*>(&S.X[g * UG + i][k]);
+                            acc[i] = fmaf(x.x, w[0], acc[i]);
+                            acc[i] = fmaf(x.y, w[1], acc[i]);
+                            acc[i] = fmaf(x.z, w[2], acc[i]);
+                            acc[i] = fmaf(x.w, w[3], acc[i]);
+                        }
                     }
 #pragma unroll
                     for (int i = 0; i < UG; ++i) S.H1[g * UG + i][c] = tanh_f(acc[i]);
                 }
-                __syncthreads();
+                lds_sync();
+                PGM_STAMP(21);
                 // ---- layer 2 forward
                 {
                     float acc[UG];
                     const float bias = S.b2[c];
 #pragma unroll
                     for (int i = 0; i < UG; ++i) acc[i] = bias;
-#pragma unroll 2
-                    for (int k = 0; k < H; ++k) {
-                        const float w = S.W2t[m][k][j];
+#pragma unroll 1
+                    for (int k = 0; k < H; k += 4) {
+                        const float w0 = S.W2t[m][k][j], w1 = S.W2t[m][k + 1][j];
+                        const float w2 = S.W2t[m][k + 2][j], w3 = S.W2t[m][k + 3][j];
 #pragma unroll
-                        for (int i = 0; i < UG; ++i) acc[i] = fmaf(S.H1[g * UG + i][m * H + k], w, acc[i]);
+                        for (int i = 0; i < UG; ++i) {
+                            const float4 h = *reinterpret_cast<const float4*>(&S.H1[g * UG + i][m * H + k]);
+                            acc[i] = fmaf(h.x, w0, acc[i]);
+                            acc[i] = fmaf(h.y, w1, acc[i]);
+                            acc[i] = fmaf(h.z, w2, acc[i]);
+                            acc[i] = fmaf(h.w, w3, acc[i]);
+                        }
                     }
 #pragma unroll
                     for (int i = 0; i < UG; ++i) S.H2[g * UG + i][c] = tanh_f(acc[i]);
                 }
-                __syncthreads();
+                lds_sync();
+                PGM_STAMP(22);
                 // ---- heads: value [UR][K], mean [UR][A] (8 lanes per dot)
                 {
                     const int sub = t & 7;
@@ -255,7 +279,8 @@ __global__ __launch_bounds__(UT) void ppo_update_kernel(UpdArgs a) {
                         }
                     }
                 }
-                __syncthreads();
+                lds_sync();
+                PGM_STAMP(23);
                 // ---- per-row loss gradients (ppo.py:80-96)
                 if (t < UR) {  // policy (actor) rows
                     const int r = t;
@@ -307,7 +332,8 @@ __global__ __launch_bounds__(UT) void ppo_update_kernel(UpdArgs a) {
                     }
                     S.rowloss[r][0] = ok ? ls : 0.f;
                 }
-                __syncthreads();
+                lds_sync();
+                PGM_STAMP(24);
                 // ---- head-weight grads (row group 0 owns them, all rows), bias/logstd grads, loss sums
                 if (g == 0) {
 #pragma unroll 2
@@ -336,7 +362,8 @@ __global__ __launch_bounds__(UT) void ppo_update_kernel(UpdArgs a) {
                         lsum_a += S.rowloss[r][1];
                     }
                 }
-                __syncthreads();
+                lds_sync();
+                PGM_STAMP(25);
                 // ---- dZ2 = (dOut . W_head) * (1 - h2^2)
 #pragma unroll 4
                 for (int i = 0; i < UG; ++i) {
@@ -352,27 +379,51 @@ __global__ __launch_bounds__(UT) void ppo_update_kernel(UpdArgs a) {
                     }
                     S.H2[r][c] = dh * (1.f - h * h);
                 }
-                __syncthreads();
+                lds_sync();
+                PGM_STAMP(26);
                 // ---- dW2^T[k][j] += sum_r H1[r][k] dZ2[r][j]  (k in [16g, 16g+16)), db2
 #pragma unroll 2
                 for (int r = 0; r < UR; ++r) {
                     const float dz = S.H2[r][c];
                     if (g == 0) accB2 += dz;
 #pragma unroll
-                    for (int i = 0; i < UG; ++i) accW2[i] = fmaf(S.H1[r][m * H + g * UG + i], dz, accW2[i]);
+                    for (int i = 0; i < UG; i += 4) {
+                        const float4 h = *reinterpret_cast<const float4*>(&S.H1[r][m * H + g * UG + i]);
+                        accW2[i] = fmaf(h.x, dz, accW2[i]);
+                        accW2[i + 1] = fmaf(h.y, dz, accW2[i + 1]);
+                        accW2[i + 2] = fmaf(h.z, dz, accW2[i + 2]);
+                        accW2[i + 3] = fmaf(h.w, dz, accW2[i + 3]);
+                    }
                 }
-                __syncthreads();
+                lds_sync();
+                PGM_STAMP(27);
                 // ---- dH1 = dZ2 W2 -> dZ1 = dH1 * (1 - h1^2)   (this thread: tower m, input unit j)
-#pragma unroll 4
-                for (int i = 0; i < UG; ++i) {
-                    const int r = g * UG + i;
-                    float dh = 0.f;
-#pragma unroll 8
-                    for (int q = 0; q < H; ++q) dh = fmaf(S.H2[r][m * H + q], S.W2t[m][j][q], dh);
-                    const float h = S.H1[r][c];
-                    S.H1[r][c] = dh * (1.f - h * h);
+                {
+                    float dh[UG];
+#pragma unroll
+                    for (int i = 0; i < UG; ++i) dh[i] = 0.f;
+#pragma unroll 1
+                    for (int q = 0; q < H; q += 4) {
+                        const float w0 = S.W2t[m][j][q], w1 = S.W2t[m][j][q + 1];
+                        const float w2 = S.W2t[m][j][q + 2], w3 = S.W2t[m][j][q + 3];
+#pragma unroll
+                        for (int i = 0; i < UG; ++i) {
+                            const float4 z = *reinterpret_cast<const float4*>(&S.H2[g * UG + i][m * H + q]);
+                            dh[i] = fmaf(z.x, w0, dh[i]);
+                            dh[i] = fmaf(z.y, w1, dh[i]);
+                            dh[i] = fmaf(z.z, w2, dh[i]);
+                            dh[i] = fmaf(z.w, w3, dh[i]);
+                        }
+                    }
+#pragma unroll
+                    for (int i = 0; i < UG; ++i) {
+                        const int r = g * UG + i;
+                        const float h = S.H1[r][c];
+                        S.H1[r][c] = dh[i] * (1.f - h * h);
+                    }
                 }
-                __syncthreads();
+                lds_sync();
+                PGM_STAMP(28);
                 // ---- dW1^T[k][c] += sum_r X[r][k] dZ1[r][c]  (k = g + 4i), db1
 #pragma unroll 2
                 for (int r = 0; r < UR; ++r) {
@@ -382,7 +433,8 @@ __global__ __launch_bounds__(UT) void ppo_update_kernel(UpdArgs a) {
                     for (int i = 0; i < NW1; ++i)
                         if (g + 4 * i < O) accW1[i] = fmaf(S.X[r][g + 4 * i], dz, accW1[i]);
                 }
-                __syncthreads();
+                lds_sync();
+                PGM_STAMP(29);
             }  // chunks
 
             // ---- stage the owned gradients in parameter layout (G aliases H1|H2, free after the chunks)
@@ -391,7 +443,8 @@ __global__ __launch_bounds__(UT) void ppo_update_kernel(UpdArgs a) {
             float ent = 0.f;
 #pragma unroll
             for (int q = 0; q < A; ++q) ent += 0.5f + LOG_SQRT_2PI + S.logstd[q];
-            __syncthreads();
+            lds_sync();
+            PGM_STAMP(30);
 #pragma unroll
             for (int i = 0; i < UG; ++i) G[offW2 + (g * UG + i) * H + j] = accW2[i];
 #pragma unroll
@@ -411,7 +464,8 @@ __global__ __launch_bounds__(UT) void ppo_update_kernel(UpdArgs a) {
             if (t < K) G[L.off[PGM_P_VALUE_B] + t] = accS;
             else if (t < K + A) G[L.off[PGM_P_MEAN_B] + t - K] = accS;
             else if (t < K + 2 * A) G[L.off[PGM_P_LOGSTD] + t - K - A] = accS - a.hp.entropy_coef;
-            __syncthreads();
+            lds_sync();
+            PGM_STAMP(31);
             // ---- clip_grad_norm_ over every parameter
             float sq = 0.f;
             for (int i = t; i < L.total; i += UT) sq = fmaf(G[i], G[i], sq);
@@ -434,7 +488,8 @@ __global__ __launch_bounds__(UT) void ppo_update_kernel(UpdArgs a) {
                 st_a += lsum_a / (float)mb;
                 st_e += ent;
             }
-            __syncthreads();
+            lds_sync();
+            PGM_STAMP(32);
         }  // minibatches
     }      // epochs
     if (t == 0) {

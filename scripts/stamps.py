@@ -1,0 +1,34 @@
+"""Diagnostic: per-phase cycle shares of the rollout and update kernels (libpgm_stamps.so).
+Usage (GPU box): PGM_LIB=pgmorl_amd/libpgm_stamps.so python scripts/stamps.py"""
+import ctypes as C
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+import torch
+
+from pgmorl_amd import _lib
+from pgmorl_amd.policy import new_policy
+from pgmorl_amd.runtime import TaskBatch
+
+P, N, T = int(os.environ.get('P', 40)), 4, 2048
+tb = TaskBatch('MO-Walker2d-v2', P, num_processes=N, num_steps=T)
+for p in range(P):
+    tb.set_task(p, new_policy(17, 6, 2).state_dict(), {}, None, [0.5, 0.5])
+tb.env_reset()
+L = _lib.lib()
+buf = (C.c_ulonglong * 64)()
+for name in ('rollout', 'update'):
+    getattr(L, f'pgm_debug_stamps_{name}')(buf, 1)
+tb.iteration(0, 3e-4)
+torch.cuda.synchronize()
+names = {0: 'loop/top', 1: 'policy fwd', 2: 'store val + sample', 3: 'logp + dynamics', 4: 'vecnorm stats',
+         5: 'vecnorm emit', 10: 'policy L2 (in fwd)'}
+for name, steps in (('rollout', T), ('update', 320)):
+    getattr(L, f'pgm_debug_stamps_{name}')(buf, 1)
+    v = np.array(list(buf), dtype=np.float64)
+    tot = v.sum()
+    print(f'== {name}: total {tot:.3e} cycles over {steps} iterations ({tot / steps:.0f} cycles/iter)')
+    for i in np.nonzero(v)[0]:
+        print(f'  phase {i:2d} {names.get(i, ""):22s} {v[i] / steps:10.0f} cycles/iter  {100 * v[i] / tot:5.1f}%')

@@ -38,18 +38,11 @@ __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\
 // LDS images
 template <int O, int A, int K>
 struct PolSmem {
-    float W1t[w1_in_lds<O>() ? O : 1][H2];  // [in][col]: col < H critic tower, col >= H actor tower
-    float b1[H2];
-    float W2t[2][H][H];                     // [tower 0=critic,1=actor][in][out]
-    float b2[H2];
-    float Wv[H][K];
     float bv[K];
-    float Wm[H][A];
     float bm[A];
     float logstd[A];
-    float x[NMAX][opad<O>()];               // fp32 policy input rows
-    float h1[NMAX][H2];
-    float h2[NMAX][H2];
+    alignas(16) float x[NMAX][opad<O>()];   // fp32 policy input rows
+    alignas(16) float h1[NMAX][H2];
     float val[NMAX][K];
     float mu[NMAX][A];
     float lp[NMAX][A];
@@ -131,22 +124,6 @@ __device__ void load_spec(EnvSmem<O, A, K>& E, const pgm_env_spec& g, const doub
 template <int O, int A, int K>
 __device__ void load_policy(PolSmem<O, A, K>& S, const float* __restrict__ prm, const Layout& L) {
     const int t = threadIdx.x;
-    if constexpr (w1_in_lds<O>()) {
-        for (int i = t; i < O * H2; i += RT) {
-            const int k = i / H2, c = i % H2;
-            S.W1t[k][c] = prm[(c < H ? L.off[PGM_P_CRITIC_W1] : L.off[PGM_P_ACTOR_W1]) + k * H + (c & (H - 1))];
-        }
-    }
-    for (int c = t; c < H2; c += RT) {
-        S.b1[c] = prm[(c < H ? L.off[PGM_P_CRITIC_B1] : L.off[PGM_P_ACTOR_B1]) + (c & (H - 1))];
-        S.b2[c] = prm[(c < H ? L.off[PGM_P_CRITIC_B2] : L.off[PGM_P_ACTOR_B2]) + (c & (H - 1))];
-    }
-    for (int i = t; i < 2 * H * H; i += RT) {
-        const int m = i / (H * H), r = i % (H * H);
-        (&S.W2t[m][0][0])[r] = prm[(m == 0 ? L.off[PGM_P_CRITIC_W2] : L.off[PGM_P_ACTOR_W2]) + r];
-    }
-    for (int i = t; i < H * K; i += RT) (&S.Wv[0][0])[i] = prm[L.off[PGM_P_VALUE_W] + i];
-    for (int i = t; i < H * A; i += RT) (&S.Wm[0][0])[i] = prm[L.off[PGM_P_MEAN_W] + i];
     if (t < K) S.bv[t] = prm[L.off[PGM_P_VALUE_B] + t];
     if (t < A) {
         S.bm[t] = prm[L.off[PGM_P_MEAN_B] + t];
@@ -154,68 +131,98 @@ __device__ void load_policy(PolSmem<O, A, K>& S, const float* __restrict__ prm, 
     }
 }
 
-// value [N][K] -> S.val, action mean [N][A] -> S.mu, from S.x.  Ends with a barrier.
+// Per-thread register image of the weights one lane needs: column c = (tower m, unit j) of both
+// tower layers and unit j's head row.  Loaded once per launch (weights are constant inside a rollout).
+template <int O>
+constexpr bool w1_in_regs() { return O <= 32; }
+
 template <int O, int A, int K>
-__device__ void policy_forward(PolSmem<O, A, K>& S, int N, const float* __restrict__ prm, const Layout& L) {
-    const int t = threadIdx.x, c = t & (H2 - 1), rg = t >> 7;
-    constexpr int RPT = NMAX / 2;  // rows per thread
-    {   // tower layer 1
-        float acc[RPT];
-        const float b = S.b1[c];
+struct PolReg {
+    float w1[w1_in_regs<O>() ? O : 1];
+    float w2[H];
+    float wh[A > K ? A : K];
+    float b1, b2;
+};
+
+template <int O, int A, int K>
+__device__ void load_polreg(PolReg<O, A, K>& R, const float* __restrict__ prm, const Layout& L) {
+    const int t = threadIdx.x, lane = t & 63, m = (t >> 6) & 1;  // m: 0 critic, 1 actor
+    const int offW1 = m == 0 ? L.off[PGM_P_CRITIC_W1] : L.off[PGM_P_ACTOR_W1];
+    const int offW2 = m == 0 ? L.off[PGM_P_CRITIC_W2] : L.off[PGM_P_ACTOR_W2];
+    if constexpr (w1_in_regs<O>()) {
 #pragma unroll
-        for (int i = 0; i < RPT; ++i) acc[i] = b;
-        const float* gw = prm + (c < H ? L.off[PGM_P_CRITIC_W1] : L.off[PGM_P_ACTOR_W1]) + (c & (H - 1));
-#pragma unroll 4
-        for (int k = 0; k < O; ++k) {
-            float w;
-            if constexpr (w1_in_lds<O>()) w = S.W1t[k][c];
-            else w = gw[k * H];
-#pragma unroll
-            for (int i = 0; i < RPT; ++i)
-                if (rg + 2 * i < N) acc[i] = fmaf(S.x[rg + 2 * i][k], w, acc[i]);
-        }
-#pragma unroll
-        for (int i = 0; i < RPT; ++i)
-            if (rg + 2 * i < N) S.h1[rg + 2 * i][c] = tanh_f(acc[i]);
+        for (int k = 0; k < O; ++k) R.w1[k] = prm[offW1 + k * H + lane];
     }
-    lds_sync();
-    PGM_STAMP_DECL
-    {   // tower layer 2
-        const int m = c >> 6, j = c & (H - 1);
-        float acc[RPT];
-        const float b = S.b2[c];
 #pragma unroll
-        for (int i = 0; i < RPT; ++i) acc[i] = b;
+    for (int k = 0; k < H; ++k) R.w2[k] = prm[offW2 + k * H + lane];
+    constexpr int NQ = A > K ? A : K;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+        R.wh[q] = m == 0 ? (q < K ? prm[L.off[PGM_P_VALUE_W] + lane * K + q] : 0.f)
+                         : (q < A ? prm[L.off[PGM_P_MEAN_W] + lane * A + q] : 0.f);
+    R.b1 = prm[(m == 0 ? L.off[PGM_P_CRITIC_B1] : L.off[PGM_P_ACTOR_B1]) + lane];
+    R.b2 = prm[(m == 0 ? L.off[PGM_P_CRITIC_B2] : L.off[PGM_P_ACTOR_B2]) + lane];
+}
+
+// value [N][K] -> S.val, action mean [N][A] -> S.mu, from S.x.  Wave-local: wave w computes tower
+// m = w & 1 for rows r = (w >> 1) + 2i; layer 1 -> layer 2 exchanges h1 inside the wave through LDS
+// (no workgroup barrier), the heads are 64-lane butterfly sums of h2 * W_head over the tower's units.
+// Ends with one barrier (val/mu visible to every wave).
+template <int O, int A, int K>
+__device__ void policy_forward(PolSmem<O, A, K>& S, const PolReg<O, A, K>& R, int N, const float* __restrict__ prm,
+                               const Layout& L) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, m = w & 1, rg = w >> 1, c = m * H + lane;
+    constexpr int RPT = NMAX / 2;
+    const float* gw = prm + (m == 0 ? L.off[PGM_P_CRITIC_W1] : L.off[PGM_P_ACTOR_W1]) + lane;
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {  // tower layer 1
+        const int r = rg + 2 * i;
+        if (r < N) {
+            float acc = R.b1;
+            if constexpr (w1_in_regs<O>()) {
+#pragma unroll
+                for (int k = 0; k < opad<O>(); k += 4) {
+                    const float4 x = *reinterpret_cast<const float4*>(&S.x[r][k]);
+                    acc = fmaf(x.x, R.w1[k], acc);
+                    if (k + 1 < O) acc = fmaf(x.y, R.w1[k + 1], acc);
+                    if (k + 2 < O) acc = fmaf(x.z, R.w1[k + 2], acc);
+                    if (k + 3 < O) acc = fmaf(x.w, R.w1[k + 3], acc);
+                }
+            } else {
 #pragma unroll 8
-        for (int k = 0; k < H; ++k) {
-            const float w = S.W2t[m][k][j];
-#pragma unroll
-            for (int i = 0; i < RPT; ++i)
-                if (rg + 2 * i < N) acc[i] = fmaf(S.h1[rg + 2 * i][m * H + k], w, acc[i]);
+                for (int k = 0; k < O; ++k) acc = fmaf(S.x[r][k], gw[k * H], acc);
+            }
+            S.h1[r][c] = tanh_f(acc);
         }
-#pragma unroll
-        for (int i = 0; i < RPT; ++i)
-            if (rg + 2 * i < N) S.h2[rg + 2 * i][c] = tanh_f(acc[i]);
     }
-    lds_sync();
-    PGM_STAMP(10);
-    {   // heads: 8 lanes per output dot
-        const int sub = t & 7;
-        const int nout = N * (K + A);
-        for (int o = t >> 3; o < nout; o += RT / 8) {
-            const int r = o / (K + A), q = o % (K + A);
-            float s = 0.f;
-            if (q < K) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // h1 row visible to this wave (lockstep)
+    __builtin_amdgcn_wave_barrier();
 #pragma unroll
-                for (int hh = 0; hh < 8; ++hh) s = fmaf(S.h2[r][sub * 8 + hh], S.Wv[sub * 8 + hh][q], s);
+    for (int i = 0; i < RPT; ++i) {  // tower layer 2 + heads
+        const int r = rg + 2 * i;
+        if (r < N) {
+            float a0 = R.b2, a1 = 0.f, a2 = 0.f, a3 = 0.f;  // four short chains instead of one of 64
+#pragma unroll
+            for (int k = 0; k < H; k += 4) {
+                const float4 h = *reinterpret_cast<const float4*>(&S.h1[r][m * H + k]);
+                a0 = fmaf(h.x, R.w2[k], a0);
+                a1 = fmaf(h.y, R.w2[k + 1], a1);
+                a2 = fmaf(h.z, R.w2[k + 2], a2);
+                a3 = fmaf(h.w, R.w2[k + 3], a3);
+            }
+            const float h2 = tanh_f((a0 + a1) + (a2 + a3));
+            if (m == 0) {
+#pragma unroll
+                for (int q = 0; q < K; ++q) {
+                    const float v = wave_sum64(h2 * R.wh[q]);
+                    if (lane == 0) S.val[r][q] = v + S.bv[q];
+                }
             } else {
 #pragma unroll
-                for (int hh = 0; hh < 8; ++hh) s = fmaf(S.h2[r][H + sub * 8 + hh], S.Wm[sub * 8 + hh][q - K], s);
-            }
-            s = group_sum<8>(s);
-            if (sub == 0) {
-                if (q < K) S.val[r][q] = s + S.bv[q];
-                else S.mu[r][q - K] = s + S.bm[q - K];
+                for (int q = 0; q < A; ++q) {
+                    const float v = wave_sum64(h2 * R.wh[q]);
+                    if (lane == 0) S.mu[r][q] = v + S.bm[q];
+                }
             }
         }
     }
@@ -279,13 +286,14 @@ __device__ void store_env(const EnvSmem<O, A, K>& E, const pgm_env_state& st, co
 }
 
 // Chan merge of a batch (bm, bv, n) into (mean, var, count) -- running_mean_std.py:20-31
+// (one fp64 division: the reference's three divisions by tot_count become a multiply by 1/tot)
 __device__ __forceinline__ void chan_merge(double& mean, double& var, double count, double bm, double bv, double n) {
     const double delta = bm - mean;
-    const double tot = count + n;
-    const double new_mean = mean + delta * n / tot;
-    const double m2 = var * count + bv * n + delta * delta * count * n / tot;
+    const double inv_tot = 1.0 / (count + n);
+    const double new_mean = mean + delta * n * inv_tot;
+    const double m2 = var * count + bv * n + delta * delta * count * n * inv_tot;
     mean = new_mean;
-    var = m2 / tot;
+    var = m2 * inv_tot;
 }
 
 __device__ __forceinline__ double clipd(double x, double lo, double hi) { return fmin(fmax(x, lo), hi); }
@@ -456,10 +464,12 @@ __global__ __launch_bounds__(RT) void act_forward_kernel(ActArgs a) {
     auto& S = *reinterpret_cast<PolSmem<O, A, K>*>(smem_raw);
     const int p = blockIdx.x, t = threadIdx.x, N = a.N;
     const float* prm = a.params + (size_t)p * a.L.total;
+    PolReg<O, A, K> R;
     load_policy(S, prm, a.L);
+    load_polreg(R, prm, a.L);
     for (int i = t; i < N * O; i += RT) S.x[i / O][i % O] = a.obs[(size_t)p * N * O + i];
     __syncthreads();
-    policy_forward(S, N, prm, a.L);
+    policy_forward(S, R, N, prm, a.L);
     for (int i = t; i < N * K; i += RT) a.value[(size_t)p * N * K + i] = S.val[i / K][i % K];
     for (int i = t; i < N * A; i += RT) {
         const int n = i / A, j = i % A;
@@ -576,7 +586,9 @@ __global__ __launch_bounds__(RT) void rollout_kernel(RolloutArgs a) {
     float* masks = a.rb.masks + (size_t)p * (T + 1) * N;
     float* bad = a.rb.bad_masks + (size_t)p * (T + 1) * N;
 
+    PolReg<O, A, K> R;
     load_policy(P, prm, a.L);
+    load_polreg(R, prm, a.L);
     load_spec(E, a.spec, a.st.s0, N);
     load_env(E, a.st, a.ns, p, N);
     if (a.carry) {  // after_update(): slot T -> slot 0 (storage.py:71-75); each thread re-reads its own writes
@@ -601,7 +613,7 @@ __global__ __launch_bounds__(RT) void rollout_kernel(RolloutArgs a) {
             eps_next = a.noise ? a.noise[idx] : counter_normal(a.seed, idx);
         }
         PGM_STAMP(0);
-        policy_forward(P, N, prm, a.L);
+        policy_forward(P, R, N, prm, a.L);
         PGM_STAMP(1);
         for (int i = t; i < N * K; i += RT) val[(size_t)step * N * K + i] = P.val[i / K][i % K];
         sample_actions(P, E, sp, N, eps, act + (size_t)step * N * A);
@@ -621,7 +633,7 @@ __global__ __launch_bounds__(RT) void rollout_kernel(RolloutArgs a) {
         PGM_STAMP(5);
     }
     // bootstrap value (mopg.py:132-135) -> value_preds[T] (storage.py:85)
-    policy_forward(P, N, prm, a.L);
+    policy_forward(P, R, N, prm, a.L);
     for (int i = t; i < N * K; i += RT) val[(size_t)T * N * K + i] = P.val[i / K][i % K];
     __syncthreads();
     store_env(E, a.st, a.ns, p, N);
@@ -646,7 +658,9 @@ __global__ __launch_bounds__(RT) void eval_kernel(EvalArgs a) {
     auto& E = S.env;
     const int p = blockIdx.x, t = threadIdx.x;
     const float* prm = a.params + (size_t)p * a.L.total;
+    PolReg<O, A, K> R;
     load_policy(P, prm, a.L);
+    load_polreg(R, prm, a.L);
     load_spec(E, a.spec, a.s0_eval, 1);
     for (int o = t; o < O; o += RT) {  // mopg.py:37-38: fp64 normalisation with fixed eps/clip
         E.ob_mean[o] = a.use_ob ? a.ob_mean[(size_t)p * O + o] : 0.0;
@@ -668,7 +682,7 @@ __global__ __launch_bounds__(RT) void eval_kernel(EvalArgs a) {
                 P.x[0][o] = (float)v;
             }
             lds_sync();
-            policy_forward(P, 1, prm, a.L);
+            policy_forward(P, R, 1, prm, a.L);
             if (t < A) E.ac[0][t] = clipd((double)P.mu[0][t], sp.lo(t), sp.hi(t));
             lds_sync();
             env_dynamics(E, sp, 1, a.spec.max_episode_steps);

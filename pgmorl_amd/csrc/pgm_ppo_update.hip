@@ -12,6 +12,8 @@
 //   clip_grad_norm_ (coef = max/(norm+1e-6), clamp 1)   torch.nn.utils.clip_grad
 //   Adam (lerp m, v*b2 + (1-b2) g^2, bias-corrected step, eps outside sqrt)   torch.optim.adam
 // torch.min / torch.max / clamp backward (ties split the gradient in half) are reproduced exactly.
+#include <stdlib.h>
+
 #include "pgm_dispatch.hpp"
 
 PGM_STAMP_UNIT(update)
@@ -503,6 +505,12 @@ __global__ __launch_bounds__(UT) void ppo_update_kernel(UpdArgs a) {
 
 }  // namespace pgm
 
+namespace pgm {
+int ppo_update_mfma(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params, float* adam_m, float* adam_v,
+                    int32_t* adam_step, const float* lr, const int32_t* perms, const pgm_rollout_buf* rb, float* stats,
+                    hipStream_t stream);
+}
+
 using namespace pgm;
 
 extern "C" int pgm_ppo_update(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params, float* adam_m,
@@ -519,8 +527,14 @@ extern "C" int pgm_ppo_update(const pgm_dims* d, const pgm_ppo_hparams* hp, floa
         set_error("pgm_ppo_update: need T*N (%d) >= num_mini_batch (%d) > 0 and ppo_epoch > 0", B, hp->num_mini_batch);
         return PGM_E_SHAPE;
     }
+    // f32-MFMA kernel for obs_dim <= 32 (Walker, Cheetah, Hopper, Ant, Swimmer); the VALU kernel is kept
+    // for A/B measurements (PGM_UPDATE_KERNEL=valu) and covers obs_dim <= 64
+    const char* sel = getenv("PGM_UPDATE_KERNEL");
+    const bool valu = sel && sel[0] == 'v';
+    if (!valu && d->O <= 32)
+        return ppo_update_mfma(d, hp, params, adam_m, adam_v, adam_step, lr, perms, rb, stats, (hipStream_t)stream);
     if (d->O > 64) {
-        set_error("pgm_ppo_update: obs_dim %d > 64 not supported by the VALU update kernel", d->O);
+        set_error("pgm_ppo_update: obs_dim %d > 64 not supported by the update kernels", d->O);
         return PGM_E_UNSUPPORTED;
     }
     UpdArgs a{d->N, d->T, make_layout(d->O, d->A, d->K, d->H), *hp, params, adam_m, adam_v, adam_step, lr, perms,

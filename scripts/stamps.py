@@ -19,16 +19,18 @@ for p in range(P):
 tb.env_reset()
 L = _lib.lib()
 buf = (C.c_ulonglong * 64)()
-for name in ('rollout', 'update'):
+for name in ('rollout', 'update', 'mfma'):
     getattr(L, f'pgm_debug_stamps_{name}')(buf, 1)
 tb.iteration(0, 3e-4)
 torch.cuda.synchronize()
-names = {0: 'loop/top', 1: 'policy fwd', 2: 'store val + sample', 3: 'logp + dynamics', 4: 'vecnorm stats',
+names = {0: "loop/top", 1: 'policy fwd', 2: 'store val + sample', 3: 'logp + dynamics', 4: 'vecnorm stats',
          5: 'vecnorm emit', 10: 'policy L2 (in fwd)'}
-for name, steps in (('rollout', T), ('update', 320)):
+for name, steps in (('rollout', T), ('update', 320), ('mfma', 320)):
     getattr(L, f'pgm_debug_stamps_{name}')(buf, 1)
     v = np.array(list(buf), dtype=np.float64)
     tot = v.sum()
+    if tot == 0:
+        continue
     print(f'== {name}: total {tot:.3e} cycles over {steps} iterations ({tot / steps:.0f} cycles/iter)')
     for i in np.nonzero(v)[0]:
         print(f'  phase {i:2d} {names.get(i, ""):22s} {v[i] / steps:10.0f} cycles/iter  {100 * v[i] / tot:5.1f}%')

@@ -92,24 +92,22 @@ struct MArgs {
 __device__ __forceinline__ float wmin2(float a, float b) { return a < b ? 1.f : (a == b ? 0.5f : 0.f); }
 __device__ __forceinline__ float wmax2(float a, float b) { return a > b ? 1.f : (a == b ? 0.5f : 0.f); }
 
-// LDS working-copy slot of flat parameter index i (nullptr for alignment padding)
-template <int O, int A, int K>
-__device__ __forceinline__ float* mslot(MSmem<O, A, K>& S, const Layout& L, int i) {
-    auto in = [&](int tsr, int n) { return i >= L.off[tsr] && i < L.off[tsr] + n; };
-    if (in(PGM_P_CRITIC_W2, H * H)) { const int r = i - L.off[PGM_P_CRITIC_W2]; return &S.W2t[0][r / H][r % H]; }
-    if (in(PGM_P_ACTOR_W2, H * H)) { const int r = i - L.off[PGM_P_ACTOR_W2]; return &S.W2t[1][r / H][r % H]; }
-    if (in(PGM_P_CRITIC_W1, O * H)) return &S.W1t[0][0][0] + (i - L.off[PGM_P_CRITIC_W1]);
-    if (in(PGM_P_ACTOR_W1, O * H)) return &S.W1t[1][0][0] + (i - L.off[PGM_P_ACTOR_W1]);
-    if (in(PGM_P_CRITIC_B1, H)) return &S.b1[0][i - L.off[PGM_P_CRITIC_B1]];
-    if (in(PGM_P_ACTOR_B1, H)) return &S.b1[1][i - L.off[PGM_P_ACTOR_B1]];
-    if (in(PGM_P_CRITIC_B2, H)) return &S.b2[0][i - L.off[PGM_P_CRITIC_B2]];
-    if (in(PGM_P_ACTOR_B2, H)) return &S.b2[1][i - L.off[PGM_P_ACTOR_B2]];
-    if (in(PGM_P_VALUE_W, H * K)) { const int r = i - L.off[PGM_P_VALUE_W]; return &S.Wh[0][r % K][r / K]; }
-    if (in(PGM_P_MEAN_W, H * A)) { const int r = i - L.off[PGM_P_MEAN_W]; return &S.Wh[1][r % A][r / A]; }
-    if (in(PGM_P_VALUE_B, K)) return &S.bh[0][i - L.off[PGM_P_VALUE_B]];
-    if (in(PGM_P_MEAN_B, A)) return &S.bh[1][i - L.off[PGM_P_MEAN_B]];
-    if (in(PGM_P_LOGSTD, A)) return &S.logstd[i - L.off[PGM_P_LOGSTD]];
-    return nullptr;
+// Visit every parameter tensor with its LDS working-copy slot: f(tensor id, count, slot(j)).
+template <int O, int A, int K, class F>
+__device__ __forceinline__ void for_each_tensor(MSmem<O, A, K>& S, F&& f) {
+    f(PGM_P_ACTOR_W1, O * H, [&](int j) { return &S.W1t[1][0][0] + j; });
+    f(PGM_P_ACTOR_B1, H, [&](int j) { return &S.b1[1][j]; });
+    f(PGM_P_ACTOR_W2, H * H, [&](int j) { return &S.W2t[1][j / H][j % H]; });
+    f(PGM_P_ACTOR_B2, H, [&](int j) { return &S.b2[1][j]; });
+    f(PGM_P_CRITIC_W1, O * H, [&](int j) { return &S.W1t[0][0][0] + j; });
+    f(PGM_P_CRITIC_B1, H, [&](int j) { return &S.b1[0][j]; });
+    f(PGM_P_CRITIC_W2, H * H, [&](int j) { return &S.W2t[0][j / H][j % H]; });
+    f(PGM_P_CRITIC_B2, H, [&](int j) { return &S.b2[0][j]; });
+    f(PGM_P_VALUE_W, H * K, [&](int j) { return &S.Wh[0][j % K][j / K]; });
+    f(PGM_P_VALUE_B, K, [&](int j) { return &S.bh[0][j]; });
+    f(PGM_P_MEAN_W, H * A, [&](int j) { return &S.Wh[1][j % A][j / A]; });
+    f(PGM_P_MEAN_B, A, [&](int j) { return &S.bh[1][j]; });
+    f(PGM_P_LOGSTD, A, [&](int j) { return &S.logstd[j]; });
 }
 
 template <int O, int A, int K>
@@ -127,9 +125,9 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
     const int mb = B / M, nb = B / mb;
     const float clip = a.hp.clip_param;
     const Layout& L = a.L;
-    float* P = a.params + (size_t)p * L.total;
-    float* Mo = a.m + (size_t)p * L.total;
-    float* Vo = a.v + (size_t)p * L.total;
+    float* __restrict__ P = a.params + (size_t)p * L.total;
+    float* __restrict__ Mo = a.m + (size_t)p * L.total;
+    float* __restrict__ Vo = a.v + (size_t)p * L.total;
     const float* obs = a.obs + (size_t)p * (T + 1) * N * O;
     const float* actions = a.actions + (size_t)p * B * A;
     const float* logp = a.logp + (size_t)p * B;
@@ -138,10 +136,11 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
     const float* advs = a.adv + (size_t)p * B;
 
     // ---- parameter working copy
-    for (int i = t; i < L.total; i += MT) {
-        float* s = mslot<O, A, K>(S, L, i);
-        if (s) *s = P[i];
-    }
+    for_each_tensor(S, [&](int tsr, int n, auto slot) {
+        const int off = L.off[tsr];
+#pragma unroll 4
+        for (int j = t; j < n; j += MT) *slot(j) = P[off + j];
+    });
     for (int i = t; i < 2 * Q * H; i += MT) {  // head rows beyond K (critic) stay zero
         const int mm = i / (Q * H), q = (i / H) % Q;
         if (q >= (mm == 0 ? K : A)) S.Wh[mm][q][i % H] = 0.f;
@@ -480,6 +479,8 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
             const double bc2 = 1.0 - pow((double)b2c, (double)stepi);
             const float step_size = (float)(lr / bc1);
             const float bc2s = (float)sqrt(bc2);
+            // flat coalesced pass (padding slots: g = m = v = 0 keeps p = 0); new values land in G
+#pragma unroll 4
             for (int i = t; i < L.total; i += MT) {
                 const float g = G[i] * coef;
                 float mm = Mo[i], vv = Vo[i];
@@ -489,9 +490,13 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                 Mo[i] = mm;
                 Vo[i] = vv;
                 P[i] = pn;
-                float* slot = mslot<O, A, K>(S, L, i);
-                if (slot) *slot = pn;
+                G[i] = pn;
             }
+            lds_sync_m();
+            for_each_tensor(S, [&](int tsr, int n, auto slot) {  // refresh the LDS working copy from G
+                const int off = L.off[tsr];
+                for (int j = t; j < n; j += MT) *slot(j) = G[off + j];
+            });
             lds_sync_m();
             PGM_STAMP(3);
         }  // minibatches

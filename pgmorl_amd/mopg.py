@@ -1,0 +1,125 @@
+"""MOPGPopulation: the drop-in replacement of the per-task process fan-out of one generation.
+
+Reference: morl/morl.py:79-99 forks one ``MOPG_worker`` process per task (morl/mopg.py:60-182) and
+gathers ``{'task_id', 'offspring_batch', 'done'}`` dicts from a multiprocessing Queue.  Here every
+task of the generation lives in one ``TaskBatch`` on the GPU and each PPO iteration of all tasks
+is a short sequence of libpgm kernels; ``run`` returns the same ``all_offspring_batch`` structure
+(list over tasks of the per-iteration offspring Samples), so the rest of the generation loop is
+unchanged.
+
+RNG: ``rng='host'`` draws exactly what the reference draws for iteration j (torch.manual_seed(j),
+then T Normal samples of shape [N, A] and ppo_epoch randperms of T*N, morl/mopg.py:96 and
+storage.py:133) and uploads them -- bit-compatible with the CPU oracle; ``rng='device'`` uses the
+counter-based device streams keyed by j (same distribution, no host work; the benchmark mode).
+Like the reference, all tasks of an iteration share one noise stream.
+"""
+import time
+
+import numpy as np
+import torch
+
+from .runtime import TaskBatch
+from .sample import DeviceSnapshot, RunningMeanStd, Sample
+
+
+def host_draws(j, T, N, A, E):
+    torch.manual_seed(j)
+    z = torch.stack([torch.normal(torch.zeros(N, A, dtype=torch.float64), torch.ones(N, A, dtype=torch.float64))
+                     for _ in range(T)])
+    perms = torch.stack([torch.randperm(T * N) for _ in range(E)])
+    return z.float(), perms.to(torch.int32)
+
+
+def linear_lr(j, total_num_updates, lr, ratio=1.0):
+    """update_linear_schedule (a2c_ppo_acktr/utils.py:46-50) as called at morl/mopg.py:97-101."""
+    return lr - lr * (j * ratio / float(total_num_updates))
+
+
+class MOPGPopulation:
+    def __init__(self, args, device='cuda', rng='device'):
+        self.args = args
+        self.device = torch.device(device)
+        self.rng = rng
+        self.tb = None
+
+    def _batch(self, P):
+        a = self.args
+        if self.tb is None or self.tb.P != P:
+            self.tb = TaskBatch(a.env_name, P, num_processes=a.num_processes, num_steps=a.num_steps, seed=a.seed,
+                                eval_num=a.eval_num, gamma=a.gamma, gae_lambda=a.gae_lambda, use_gae=a.use_gae,
+                                use_proper_time_limits=a.use_proper_time_limits, ob_rms=a.ob_rms,
+                                obj_rms=a.obj_rms, raw=a.raw, clip_param=a.clip_param, ppo_epoch=a.ppo_epoch,
+                                num_mini_batch=a.num_mini_batch, value_loss_coef=a.value_loss_coef,
+                                entropy_coef=a.entropy_coef, max_grad_norm=a.max_grad_norm, device=self.device)
+        return self.tb
+
+    def load_task(self, tb, p, sample, weights):
+        snap = sample.snapshot
+        tb.params[p].copy_(snap.params)
+        tb.adam_m[p].copy_(snap.adam_m)
+        tb.adam_v[p].copy_(snap.adam_v)
+        tb.adam_step[p] = snap.adam_step
+        tb.weights[p].copy_(torch.as_tensor(np.asarray(weights, dtype=np.float64)))
+        ep = sample.env_params or {}
+        tb.set_env_params(p, {k: v for k, v in ep.items() if v is not None})
+
+    def _env_params(self, tb, host):
+        """Per-task RunningMeanStd copies (the snapshot of mopg.py:146-149) from one D2H batch."""
+        out = []
+        for p in range(tb.P):
+            ep = {'ob_rms': None, 'ret_rms': None, 'obj_rms': None}
+            if self.args.ob_rms:
+                r = RunningMeanStd(shape=(tb.O,))
+                r.mean, r.var, r.count = host['ob_mean'][p].copy(), host['ob_var'][p].copy(), float(host['ob_count'][p])
+                ep['ob_rms'] = r
+            r = RunningMeanStd(shape=())
+            r.mean, r.var, r.count = np.float64(host['ret_mean'][p]), np.float64(host['ret_var'][p]), float(host['ret_count'][p])
+            ep['ret_rms'] = r
+            if self.args.obj_rms:
+                r = RunningMeanStd(shape=())
+                r.mean, r.var, r.count = host['obj_mean'][p].copy(), host['obj_var'][p].copy(), float(host['obj_count'][p])
+                ep['obj_rms'] = r
+            out.append(ep)
+        return out
+
+    def run(self, task_batch, iteration, num_updates, start_time=None, log=print):
+        a = self.args
+        P = len(task_batch)
+        tb = self._batch(P)
+        tb.reset_stats()
+        for p, task in enumerate(task_batch):
+            self.load_task(tb, p, task.sample, task.scalarization.weights.numpy())
+        tb.env_reset()  # envs are re-created and reset every generation (mopg.py:67-82)
+        total = int(a.num_env_steps) // a.num_steps // a.num_processes
+        offspring = [[] for _ in range(P)]
+        start_time = time.time() if start_time is None else start_time
+        first = True
+        for j in range(iteration, min(iteration + num_updates, total)):
+            lr = linear_lr(j, total, a.lr, a.lr_decay_ratio) if a.use_linear_lr_decay else a.lr
+            noise = perms = None
+            if self.rng == 'host':
+                noise, perms = host_draws(j, a.num_steps, a.num_processes, tb.A, a.ppo_epoch)
+            tb.iteration(j, lr, noise=noise, perms=perms, carry=not first)
+            first = False
+            params, m, v = tb.params.clone(), tb.adam_m.clone(), tb.adam_v.clone()
+            host = {k: getattr(tb, k).cpu().numpy() for k in ('ob_mean', 'ob_var', 'ob_count', 'ret_mean', 'ret_var',
+                                                              'ret_count', 'obj_mean', 'obj_var', 'obj_count',
+                                                              'objs', 'adam_step')}
+            envp = self._env_params(tb, host)
+            for p in range(P):
+                snap = DeviceSnapshot(tb.layout, params[p], m[p], v[p], host['adam_step'][p])
+                offspring[p].append(Sample.from_snapshot(snap, envp[p], host['objs'][p].copy()))
+            if a.rl_log_interval > 0 and (j + 1) % a.rl_log_interval == 0:
+                steps = (j + 1) * a.num_processes * a.num_steps
+                dt = time.time() - start_time
+                log(f'[RL] Updates {j + 1}, num timesteps {steps}, FPS {int(steps / max(dt, 1e-9))}, '
+                    f'time {dt:.2f} seconds (x{P} tasks on {self.device})')
+        return offspring
+
+    def evaluate_samples(self, samples, weights_batch):
+        """Objectives of fresh samples (warm-up evaluation, morl/warm_up.py:69)."""
+        tb = self._batch(len(samples))
+        tb.reset_stats()
+        for p, (s, w) in enumerate(zip(samples, weights_batch)):
+            self.load_task(tb, p, s, w)
+        return tb.evaluate().cpu().numpy().copy()

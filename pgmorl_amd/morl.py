@@ -1,0 +1,173 @@
+"""The PG-MORL generation loop on top of the MI355X MOPG runtime (drop-in for morl/morl.py:28-239).
+
+Warm-up (reference-order policy init, evaluation), then per generation: compose Tasks, run MOPG for
+every task on the GPU (``MOPGPopulation.run`` replaces the process fan-out of morl/morl.py:79-99),
+OptGraph / EP bookkeeping (morl/morl.py:101-125), task selection, and the per-generation text dumps
+and final artefacts with the reference's formats and paths (morl/morl.py:179-239).
+
+Selection: 'ra', 'pfa' and 'moead' are implemented here; 'prediction-guided' and 'random' need the
+reference's Population (morl/population_2d.py / population_3d.py), which is outside the hot-path
+scope of this build: a drop-in user keeps the reference's morl.py with its Population
+and swaps only the fan-out.
+"""
+import os
+import pickle
+import time
+from copy import deepcopy
+
+import numpy as np
+import torch
+
+from . import envspec
+from .mopg import MOPGPopulation
+from .pareto import EP, OptGraph, weight_grid
+from .policy import new_policy
+from .sample import DeviceSnapshot, RunningMeanStd, Sample, Task, WeightedSumScalarization
+
+
+def _fmt(n):
+    return '{:5f}' + (n - 1) * ',{:5f}'
+
+
+def initialize_warm_up_batch(args, runtime):
+    """morl/warm_up.py:24-77: one reference-initialised policy + fresh env_params per weight, evaluated."""
+    spec = envspec.make_spec(args.env_name)
+    weights_batch = weight_grid(args.obj_num, args.delta_weight, args.min_weight, args.max_weight)
+    samples, scal = [], []
+    layout = runtime._batch(len(weights_batch)).layout
+    dev = runtime.device
+    for w in weights_batch:
+        pol = new_policy(spec['obs_dim'], spec['act_dim'], args.obj_num)
+        flat = torch.from_numpy(layout.flatten(pol.state_dict())).to(dev)
+        snap = DeviceSnapshot(layout, flat, torch.zeros_like(flat), torch.zeros_like(flat), 0)
+        env_params = {'ob_rms': RunningMeanStd(shape=(spec['obs_dim'],)) if args.ob_rms else None,
+                      'ret_rms': RunningMeanStd(shape=()),
+                      'obj_rms': RunningMeanStd(shape=()) if args.obj_rms else None}
+        samples.append(Sample.from_snapshot(snap, env_params, optgraph_id=-1))
+        scal.append(WeightedSumScalarization(num_objs=args.obj_num, weights=w))
+    objs = runtime.evaluate_samples(samples, weights_batch)
+    for s, o in zip(samples, objs):
+        s.objs = o
+    return samples, scal
+
+
+def run(args, device='cuda', rng='device', log=print):
+    np.random.seed(args.seed)
+    torch.manual_seed(args.seed)
+    runtime = MOPGPopulation(args, device=device, rng=rng)
+    template = WeightedSumScalarization(num_objs=args.obj_num, weights=np.ones(args.obj_num) / args.obj_num)
+    total_num_updates = int(args.num_env_steps) // args.num_steps // args.num_processes
+    start_time = time.time()
+    ep, opt_graph = EP(), OptGraph()
+    if args.selection_method not in ('ra', 'pfa', 'moead'):
+        raise NotImplementedError(f'selection method {args.selection_method!r} needs the reference Population '
+                                  f'(out of scope here); use ra | pfa | moead or the INTEGRATION.md patch')
+    elite_batch, scalarization_batch = initialize_warm_up_batch(args, runtime)
+    for s, sc in zip(elite_batch, scalarization_batch):
+        s.optgraph_id = opt_graph.insert(deepcopy(sc.weights), deepcopy(s.objs), -1)
+    rl_num_updates = args.warmup_iter
+    episode = iteration = 0
+    fmt = _fmt(args.obj_num)
+    while iteration < total_num_updates:
+        log('\n------------------------------- Warm-up Stage -------------------------------' if episode == 0 else
+            f'\n-------------------- Evolutionary Stage: Generation {episode:3} --------------------')
+        episode += 1
+        task_batch = [Task(e, s) for e, s in zip(elite_batch, scalarization_batch)]
+        all_offspring_batch = runtime.run(task_batch, iteration, rl_num_updates, start_time, log=log)
+        all_sample_batch, offspring_batch = [], []
+        last_offspring_batch = [None] * len(task_batch)
+        for task_id, offsprings in enumerate(all_offspring_batch):
+            prev = task_batch[task_id].sample.optgraph_id
+            w = task_batch[task_id].scalarization.weights.numpy()
+            for i, s in enumerate(offsprings):
+                all_sample_batch.append(s)
+                if (i + 1) % args.update_iter == 0:
+                    prev = opt_graph.insert(w, deepcopy(s.objs), prev)
+                    s.optgraph_id = prev
+                    offspring_batch.append(s)
+            last_offspring_batch[task_id] = offsprings[-1]
+        ep.update(all_sample_batch)
+        population = offspring_batch  # stands in for population.sample_batch in the dumps below
+        # ---------------- task selection (morl/morl.py:128-169)
+        weights_batch = weight_grid(args.obj_num, args.delta_weight, args.min_weight, args.max_weight)
+        if args.selection_method == 'ra':
+            elite_batch = last_offspring_batch
+            scalarization_batch = []
+            for w in weights_batch:
+                sc = deepcopy(template)
+                sc.update_weights(w)
+                scalarization_batch.append(sc)
+        elif args.selection_method == 'pfa':
+            if args.obj_num > 2:
+                raise NotImplementedError('pfa needs 2 objectives')
+            elite_batch = last_offspring_batch
+            scalarization_batch = []
+            ratio = (iteration + rl_num_updates + args.update_iter - args.warmup_iter) / \
+                (total_num_updates - args.warmup_iter)
+            ratio = np.clip(ratio, 0.0, 1.0)
+            for i in np.arange(args.min_weight, args.max_weight + 0.5 * args.delta_weight, args.delta_weight):
+                wv = np.clip(i + ratio * args.delta_weight, args.min_weight, args.max_weight)
+                sc = deepcopy(template)
+                sc.update_weights(np.array([abs(wv), abs(1.0 - wv)]))
+                scalarization_batch.append(sc)
+        else:  # moead over the candidate pool (EP here; population.sample_batch in the reference)
+            elite_batch, scalarization_batch = [], []
+            pool = list(ep.sample_batch) + list(population)
+            for w in weights_batch:
+                sc = deepcopy(template)
+                sc.update_weights(w)
+                scalarization_batch.append(sc)
+                best, best_v = None, -np.inf
+                for s in pool:
+                    v = sc.evaluate(torch.tensor(s.objs))
+                    if v > best_v:
+                        best, best_v = s, v
+                elite_batch.append(best)
+        log('Selected Tasks:')
+        for e, sc in zip(elite_batch, scalarization_batch):
+            log(f'objs = {e.objs}, weight = {sc.weights}')
+        iteration = min(iteration + rl_num_updates, total_num_updates)
+        rl_num_updates = args.update_iter
+        # ---------------- per-generation dumps (morl/morl.py:179-218)
+        base = os.path.join(args.save_dir, str(iteration))
+        os.makedirs(os.path.join(base, 'ep'), exist_ok=True)
+        with open(os.path.join(base, 'ep', 'objs.txt'), 'w') as fp:
+            for obj in ep.obj_batch:
+                fp.write((fmt + '\n').format(*obj))
+        os.makedirs(os.path.join(base, 'population'), exist_ok=True)
+        with open(os.path.join(base, 'population', 'objs.txt'), 'w') as fp:
+            for s in population:
+                fp.write((fmt + '\n').format(*s.objs))
+        with open(os.path.join(base, 'population', 'optgraph.txt'), 'w') as fp:
+            fp.write('{}\n'.format(len(opt_graph.objs)))
+            for i in range(len(opt_graph.objs)):
+                fp.write((fmt + ';' + fmt + ';{}\n').format(*opt_graph.weights[i], *opt_graph.objs[i], opt_graph.prev[i]))
+            fp.write('{}\n'.format(len(population)))
+            for s in population:
+                fp.write('{}\n'.format(s.optgraph_id))
+        os.makedirs(os.path.join(base, 'elites'), exist_ok=True)
+        with open(os.path.join(base, 'elites', 'elites.txt'), 'w') as fp:
+            for e in elite_batch:
+                fp.write((fmt + '\n').format(*e.objs))
+        with open(os.path.join(base, 'elites', 'weights.txt'), 'w') as fp:
+            for sc in scalarization_batch:
+                fp.write((fmt + '\n').format(*sc.weights))
+        with open(os.path.join(base, 'elites', 'offsprings.txt'), 'w') as fp:
+            for offs in all_offspring_batch:
+                for s in offs:
+                    fp.write((fmt + '\n').format(*s.objs))
+    # ---------------- final artefacts (morl/morl.py:220-239)
+    final = os.path.join(args.save_dir, 'final')
+    os.makedirs(final, exist_ok=True)
+    for i, s in enumerate(ep.sample_batch):
+        torch.save(s.actor_critic.state_dict(), os.path.join(final, f'EP_policy_{i}.pt'))
+        with open(os.path.join(final, f'EP_env_params_{i}.pkl'), 'wb') as fp:
+            pickle.dump(s.env_params, fp)
+    with open(os.path.join(final, 'objs.txt'), 'w') as fp:
+        for obj in ep.obj_batch:
+            fp.write((fmt + '\n').format(*obj))
+    if args.obj_rms:
+        with open(os.path.join(final, 'env_params.txt'), 'w') as fp:
+            for s in ep.sample_batch:
+                fp.write('obj_rms: mean: {} var: {}\n'.format(s.env_params['obj_rms'].mean, s.env_params['obj_rms'].var))
+    return ep

@@ -71,7 +71,8 @@ class TaskBatch:
         self.actions, self.logp = z(P, T, N, A), z(P, T, N)
         self.values, self.returns = z(P, T + 1, N, K), z(P, T + 1, N, K)
         self.rewards, self.adv = z(P, T, N, K), z(P, T, N)
-        self.masks, self.bad_masks = torch.ones(P, T + 1, N, device=self.dev), torch.ones(P, T + 1, N, device=self.dev)
+        self.masks = torch.ones(P, T + 1, N, dtype=F32, device=self.dev)
+        self.bad_masks = torch.ones(P, T + 1, N, dtype=F32, device=self.dev)
         self.stats, self.objs = z(P, 3), z(P, K, dt=F64)
         self.perms = z(ppo_epoch, T * N, dt=I32)
         self.noise = z(T, N, A)
@@ -143,7 +144,8 @@ class TaskBatch:
     def rollout(self, seed, noise=None, carry=True):
         nz = None
         if noise is not None:
-            self.noise.copy_(noise.to(dtype=F32))
+            if noise is not self.noise:
+                self.noise.copy_(noise.to(dtype=F32))
             nz = self.noise
         check(lib().pgm_rollout(C.byref(self.dims), _ptr(self.params), C.byref(self.c_spec), C.byref(self.c_state),
                                 C.byref(self.c_norm), C.byref(self.c_rb), _ptr(nz), C.c_uint64(seed),
@@ -183,6 +185,10 @@ class TaskBatch:
         noise/perms: the reference's RNG draws of iteration j (parity mode); None draws the
         device counter streams keyed by j (perf mode)."""
         self.lr.fill_(float(lr))
+        if noise is None:  # perf mode: the counter stream of iteration j, drawn by one wide kernel up front
+            check(lib().pgm_normal_noise(self.noise.numel(), C.c_uint64(j), _ptr(self.noise), _stream()),
+                  'pgm_normal_noise')
+            noise = self.noise
         self.rollout(j, noise=noise, carry=carry)
         self.gae()
         self.adv_normalize()

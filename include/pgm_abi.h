@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define PGM_ABI_VERSION 1
+#define PGM_ABI_VERSION 2
 
 #define PGM_OK 0
 #define PGM_E_INVALID_ARG (-1)
@@ -171,10 +171,16 @@ int pgm_adv_normalize(const pgm_dims* d, const pgm_rollout_buf* rb, const double
 
 /* PPO.update minibatch loop: ppo_epoch x (T*N / (T*N/num_mini_batch)) Adam steps per task, rows
  * perms[e][b*mb:(b+1)*mb].  params/adam_m/adam_v [P][L] updated in place, adam_step [P] int32
- * incremented per step, lr [P].  stats [P][3] = mean (value_loss, action_loss, dist_entropy). */
+ * incremented per step, lr [P].  stats [P][3] = mean (value_loss, action_loss, dist_entropy).
+ * workspace: caller-owned device bytes (pgm_ppo_update_workspace_bytes), reset inside the call on
+ * `stream`; with it the critic and actor towers of a task run on two CUs that exchange the squared
+ * gradient norm per minibatch (used when 2P <= CU count).  NULL: one workgroup per task.
+ * After the call, the 8-byte word at index 2P of the workspace is nonzero iff an exchange timed out
+ * (the towers were not co-resident); the results of such a call are invalid. */
 int pgm_ppo_update(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params, float* adam_m,
                    float* adam_v, int32_t* adam_step, const float* lr, const int32_t* perms,
-                   const pgm_rollout_buf* rb, float* stats, pgm_stream_t stream);
+                   const pgm_rollout_buf* rb, float* stats, void* workspace, pgm_stream_t stream);
+size_t pgm_ppo_update_workspace_bytes(const pgm_dims* d);
 
 /* evaluation(): eval_num deterministic episodes per task from s0_eval [eval_num][O], obs normalised
  * with the snapshot ob_mean/ob_var [P][O] (use_ob_rms), objs_out [P][K] fp64 (discounted by gamma

@@ -21,6 +21,8 @@ struct Layout {
     int32_t total;
 };
 Layout make_layout(int O, int A, int K, int Hd);
+// pgm_ppo_update workspace: [2P] tagged 8-byte granules + 1 flag word, padded to 16 bytes
+inline size_t ppo_workspace_bytes(int P) { return ((size_t)(2 * P + 1) * 8 + 15) / 16 * 16; }
 
 // ---------------------------------------------------------------- device helpers
 // Branch-free fp32 tanh (~12 VALU ops, rel. error ~3e-7): odd Taylor series through x^9 for |x| < 0.25

@@ -19,6 +19,8 @@
 // a2c_ppo_acktr/storage.py:118-154 (minibatch rows), a2c_ppo_acktr/model.py:75-82,
 // a2c_ppo_acktr/distributions.py:29-40 (log_probs / entropy).  torch.min/max/clamp backward
 // (ties split the gradient in half) are reproduced exactly.
+#include <stdlib.h>
+
 #include "pgm_dispatch.hpp"
 
 PGM_STAMP_UNIT(mfma)
@@ -87,6 +89,8 @@ struct MArgs {
     const int32_t* perms;
     const float *obs, *actions, *logp, *values, *returns, *adv;
     float* stats;
+    unsigned long long* ws;  // SPLIT: [2P] tagged granules + [1] timeout flag, zeroed before the launch
+    int P;
 };
 
 __device__ __forceinline__ float wmin2(float a, float b) { return a < b ? 1.f : (a == b ? 0.5f : 0.f); }
@@ -110,15 +114,20 @@ __device__ __forceinline__ void for_each_tensor(MSmem<O, A, K>& S, F&& f) {
     f(PGM_P_LOGSTD, A, [&](int j) { return &S.logstd[j]; });
 }
 
-template <int O, int A, int K>
+template <int O, int A, int K, bool SPLIT>
 __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     auto& S = *reinterpret_cast<MSmem<O, A, K>*>(smem_raw);
     constexpr int Q = qmax<A, K>();
     constexpr int OX = ox<O>();
     constexpr int KS1 = (O + 1) / 2;  // k-steps of layer 1
-    const int p = blockIdx.x, t = threadIdx.x, w = t >> 6, l = t & 63, h = l >> 5, c = l & 31;
-    const int m = w & 1, sh = w >> 1;  // tower, sample half
+    // SPLIT: two workgroups per task (blockIdx = 2 task + tower), all 4 waves on one tower, exchanging
+    // only the squared gradient norm per minibatch.  Otherwise one workgroup: waves 0/2 critic, 1/3 actor.
+    constexpr int NWT = SPLIT ? 4 : 2;  // waves per tower
+    const int t = threadIdx.x, w = t >> 6, l = t & 63, h = l >> 5, c = l & 31;
+    const int p = SPLIT ? (int)(blockIdx.x >> 1) : (int)blockIdx.x;
+    const int m = SPLIT ? (int)(blockIdx.x & 1) : (w & 1);  // tower
+    const int sh = SPLIT ? w : (w >> 1);                      // wave index within the tower
     const int NQ = m == 0 ? K : A;
     const int N = a.N, T = a.T, B = T * N;
     const int E = a.hp.ppo_epoch, M = a.hp.num_mini_batch;
@@ -200,7 +209,7 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                 lds_sync_m();
                 PGM_STAMP(0);
 
-                for (int tile = sh; tile * TS < ns; tile += 2) {
+                for (int tile = sh; tile * TS < ns; tile += NWT) {
                     const int ts0 = tile * TS;
                     // ---- layer 1: Z1[s][h] = X[s][:] . W1t[:][h]
                     f32x16 z[2] = {f32x16{0}, f32x16{0}};
@@ -416,7 +425,7 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
             const int offB2 = m == 0 ? L.off[PGM_P_CRITIC_B2] : L.off[PGM_P_ACTOR_B2];
             const int offWh = m == 0 ? L.off[PGM_P_VALUE_W] : L.off[PGM_P_MEAN_W];
             const int offBh = m == 0 ? L.off[PGM_P_VALUE_B] : L.off[PGM_P_MEAN_B];
-            for (int round = 0; round < 2; ++round) {
+            for (int round = 0; round < NWT; ++round) {
                 if (sh == round) {
 #pragma unroll
                     for (int ib = 0; ib < 2; ++ib)
@@ -459,17 +468,47 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                 lds_sync_m();
             }
             PGM_STAMP(2);
-            // ---- clip_grad_norm_ over every parameter
+            // ---- clip_grad_norm_ over every parameter (G holds zeros outside this workgroup's tensors)
             float sq = 0.f;
             for (int i = t; i < L.total; i += MT) sq = fmaf(G[i], G[i], sq);
             sq = wave_sum64(sq);
             if (l == 0) S.red[w] = sq;
             lds_sync_m();
-            const float total = (S.red[0] + S.red[1]) + (S.red[2] + S.red[3]);
+            float total = (S.red[0] + S.red[1]) + (S.red[2] + S.red[3]);
+            if constexpr (SPLIT) {  // tagged 8-byte granule hand-off with the other tower's workgroup
+                if (t == 0) {
+                    const unsigned tag = (unsigned)(nstep + 1);
+                    unsigned long long* ws = a.ws + 2 * p;
+                    __hip_atomic_store(ws + m, ((unsigned long long)tag << 32) | __float_as_uint(total),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    unsigned long long x = 0;
+                    const bool failed = __hip_atomic_load(a.ws + 2 * a.P, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    for (unsigned spins = 0; !failed; ++spins) {
+                        x = __hip_atomic_load(ws + (1 - m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if ((unsigned)(x >> 32) == tag) break;
+                        if (spins > (1u << 26)) {  // partner never arrived: flag it, continue unclipped-safe
+                            __hip_atomic_store(a.ws + 2 * a.P, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            x = 0;
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                    const float other = __uint_as_float((unsigned)x);
+                    S.red[4] = m == 0 ? total + other : other + total;  // critic + actor in both workgroups
+                }
+                lds_sync_m();
+                total = S.red[4];
+            }
             const float coef = fminf(a.hp.max_grad_norm / (sqrtf(total) + 1e-6f), 1.f);
             if (t == 0) {
-                st_v += 0.5f * (S.red[8] + S.red[10]) / (float)(mb * K);
-                st_a += (S.red[9] + S.red[11]) / (float)mb;
+                if constexpr (SPLIT) {
+                    const float ls = (S.red[8] + S.red[9]) + (S.red[10] + S.red[11]);
+                    if (m == 0) st_v += 0.5f * ls / (float)(mb * K);
+                    else st_a += ls / (float)mb;
+                } else {
+                    st_v += 0.5f * (S.red[8] + S.red[10]) / (float)(mb * K);
+                    st_a += (S.red[9] + S.red[11]) / (float)mb;
+                }
                 st_e += ent;
             }
             // ---- Adam (coalesced over the flat parameter vector; padding slots stay 0)
@@ -479,21 +518,35 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
             const double bc2 = 1.0 - pow((double)b2c, (double)stepi);
             const float step_size = (float)(lr / bc1);
             const float bc2s = (float)sqrt(bc2);
-            // flat coalesced pass (padding slots: g = m = v = 0 keeps p = 0); new values land in G
+            // flat coalesced pass over this workgroup's parameter ranges (padding slots: g = m = v = 0
+            // keeps p = 0); new values land in G.  Critic tensors are [off(critic_w1), off(mean_w)),
+            // the actor owns the rest (layout order: actor tower, critic tower, value head, mean head, logstd).
+            const int cb = L.off[PGM_P_CRITIC_W1], ce = L.off[PGM_P_MEAN_W];
+            for (int rg = 0; rg < 2; ++rg) {
+                int lo = 0, hi = L.total;
+                if constexpr (SPLIT) {
+                    if (m == 0) { lo = rg == 0 ? cb : 0; hi = rg == 0 ? ce : 0; }
+                    else { lo = rg == 0 ? 0 : ce; hi = rg == 0 ? cb : L.total; }
+                } else if (rg == 1) {
+                    hi = 0;
+                }
 #pragma unroll 4
-            for (int i = t; i < L.total; i += MT) {
-                const float g = G[i] * coef;
-                float mm = Mo[i], vv = Vo[i];
-                mm = mm + (1.f - b1c) * (g - mm);
-                vv = vv * b2c + (1.f - b2c) * (g * g);
-                const float pn = P[i] - step_size * (mm / (sqrtf(vv) / bc2s + eps));
-                Mo[i] = mm;
-                Vo[i] = vv;
-                P[i] = pn;
-                G[i] = pn;
+                for (int i = lo + t; i < hi; i += MT) {
+                    const float g = G[i] * coef;
+                    float mm = Mo[i], vv = Vo[i];
+                    mm = mm + (1.f - b1c) * (g - mm);
+                    vv = vv * b2c + (1.f - b2c) * (g * g);
+                    const float pn = P[i] - step_size * (mm / (sqrtf(vv) / bc2s + eps));
+                    Mo[i] = mm;
+                    Vo[i] = vv;
+                    P[i] = pn;
+                    G[i] = pn;
+                }
             }
             lds_sync_m();
             for_each_tensor(S, [&](int tsr, int n, auto slot) {  // refresh the LDS working copy from G
+                const bool mine = !SPLIT || ((tsr >= PGM_P_CRITIC_W1 && tsr < PGM_P_MEAN_W) == (m == 0));
+                if (!mine) return;
                 const int off = L.off[tsr];
                 for (int j = t; j < n; j += MT) *slot(j) = G[off + j];
             });
@@ -502,12 +555,25 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
         }  // minibatches
     }      // epochs
     if (t == 0) {
-        a.step[p] = step0 + nstep;
         const float n = (float)(E * M);
-        a.stats[p * 3 + 0] = st_v / n;
-        a.stats[p * 3 + 1] = st_a / n;
-        a.stats[p * 3 + 2] = st_e / n;
+        if (!SPLIT || m == 0) a.stats[p * 3 + 0] = st_v / n;
+        if (!SPLIT || m == 1) {
+            a.step[p] = step0 + nstep;
+            a.stats[p * 3 + 1] = st_a / n;
+            a.stats[p * 3 + 2] = st_e / n;
+        }
     }
+}
+
+static int device_cus() {
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 1;
+    }
+    return cus;
 }
 
 template <int O, int A, int K>
@@ -521,18 +587,27 @@ int launch_ppo_update_mfma(const pgm_dims* d, const MArgs& a, hipStream_t stream
         set_error("pgm_ppo_update: %d parameters exceed the LDS gradient image", a.L.total);
         return PGM_E_UNSUPPORTED;
     }
-    auto kern = ppo_update_mfma_kernel<O, A, K>;
+    // the split needs both workgroups of a task resident at once: one workgroup per CU (LDS + 512
+    // registers per lane), so 2P must not exceed the CU count; otherwise run one workgroup per task
+    const char* sel = getenv("PGM_UPDATE_SPLIT");
+    const bool split = a.ws && 2 * d->P <= device_cus() && !(sel && sel[0] == '0');
+    auto kern = split ? ppo_update_mfma_kernel<O, A, K, true> : ppo_update_mfma_kernel<O, A, K, false>;
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update");
-    hipLaunchKernelGGL(kern, dim3(d->P), dim3(MT), smem, stream, a);
+    if (split) {
+        e = hipMemsetAsync(a.ws, 0, ppo_workspace_bytes(d->P), stream);
+        if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update (workspace reset)");
+    }
+    hipLaunchKernelGGL(kern, dim3(split ? 2 * d->P : d->P), dim3(MT), smem, stream, a);
     return launch_status("pgm_ppo_update");
 }
 
 int ppo_update_mfma(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params, float* adam_m, float* adam_v,
                     int32_t* adam_step, const float* lr, const int32_t* perms, const pgm_rollout_buf* rb, float* stats,
-                    hipStream_t stream) {
+                    void* workspace, hipStream_t stream) {
     MArgs a{d->N, d->T, make_layout(d->O, d->A, d->K, d->H), *hp, params, adam_m, adam_v, adam_step, lr, perms,
-            rb->obs, rb->actions, rb->logp, rb->values, rb->returns, rb->adv, stats};
+            rb->obs, rb->actions, rb->logp, rb->values, rb->returns, rb->adv, stats,
+            (unsigned long long*)workspace, d->P};
     return dispatch_dims(d->O, d->A, d->K, "pgm_ppo_update", [&](auto o, auto aa, auto k) -> int {
         constexpr int O = decltype(o)::value, A = decltype(aa)::value, K = decltype(k)::value;
         if constexpr (O > 32) {

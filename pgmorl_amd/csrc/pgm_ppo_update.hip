@@ -508,14 +508,16 @@ __global__ __launch_bounds__(UT) void ppo_update_kernel(UpdArgs a) {
 namespace pgm {
 int ppo_update_mfma(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params, float* adam_m, float* adam_v,
                     int32_t* adam_step, const float* lr, const int32_t* perms, const pgm_rollout_buf* rb, float* stats,
-                    hipStream_t stream);
+                    void* workspace, hipStream_t stream);
 }
 
 using namespace pgm;
 
+extern "C" size_t pgm_ppo_update_workspace_bytes(const pgm_dims* d) { return d ? ppo_workspace_bytes(d->P) : 0; }
+
 extern "C" int pgm_ppo_update(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params, float* adam_m,
                               float* adam_v, int32_t* adam_step, const float* lr, const int32_t* perms,
-                              const pgm_rollout_buf* rb, float* stats, pgm_stream_t stream) {
+                              const pgm_rollout_buf* rb, float* stats, void* workspace, pgm_stream_t stream) {
     if (int rc = check_dims(d, "pgm_ppo_update")) return rc;
     if (!hp || !params || !adam_m || !adam_v || !adam_step || !lr || !perms || !rb || !rb->obs || !rb->actions ||
         !rb->logp || !rb->values || !rb->returns || !rb->adv || !stats) {
@@ -532,7 +534,8 @@ extern "C" int pgm_ppo_update(const pgm_dims* d, const pgm_ppo_hparams* hp, floa
     const char* sel = getenv("PGM_UPDATE_KERNEL");
     const bool valu = sel && sel[0] == 'v';
     if (!valu && d->O <= 32)
-        return ppo_update_mfma(d, hp, params, adam_m, adam_v, adam_step, lr, perms, rb, stats, (hipStream_t)stream);
+        return ppo_update_mfma(d, hp, params, adam_m, adam_v, adam_step, lr, perms, rb, stats, workspace,
+                               (hipStream_t)stream);
     if (d->O > 64) {
         set_error("pgm_ppo_update: obs_dim %d > 64 not supported by the update kernels", d->O);
         return PGM_E_UNSUPPORTED;

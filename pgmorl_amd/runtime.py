@@ -82,6 +82,8 @@ class TaskBatch:
                              use_clipped_value_loss=int(use_clipped_value_loss))
         self.reset_stats()
         self._build_structs()
+        nws = lib().pgm_ppo_update_workspace_bytes(C.byref(self.dims))
+        self.update_ws = torch.zeros((nws + 7) // 8, dtype=torch.int64, device=self.dev)
 
     # ------------------------------------------------------------------ structs
     def _build_structs(self):
@@ -169,7 +171,8 @@ class TaskBatch:
             self.perms.copy_(torch.as_tensor(np.asarray(perms), dtype=I32))
         check(lib().pgm_ppo_update(C.byref(self.dims), C.byref(self.hp), _ptr(self.params), _ptr(self.adam_m),
                                    _ptr(self.adam_v), _ptr(self.adam_step), _ptr(self.lr), _ptr(self.perms),
-                                   C.byref(self.c_rb), _ptr(self.stats), _stream()), 'pgm_ppo_update')
+                                   C.byref(self.c_rb), _ptr(self.stats), _ptr(self.update_ws), _stream()),
+              'pgm_ppo_update')
 
     def evaluate(self, ob_mean=None, ob_var=None):
         mean = self.ob_mean if ob_mean is None else ob_mean

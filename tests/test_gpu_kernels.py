@@ -167,17 +167,20 @@ def _update_setup(env, P, T, N, E, M, seed):
     return args, spec, tb, pols, (obs, actions, logp, values, returns, adv), perms
 
 
-@pytest.mark.parametrize('kernel', ['mfma', 'valu'])
+@pytest.mark.parametrize('kernel', ['mfma', 'mfma-joint', 'valu'])
 @pytest.mark.parametrize('env,T,N,E,M', [('MO-Hopper-v2', 64, 4, 2, 4), ('MO-Walker2d-v2', 128, 4, 2, 2),
                                          ('MO-Hopper-v3', 50, 3, 1, 3), ('MO-Swimmer-v2', 64, 1, 1, 1),
                                          ('MO-Ant-v2', 160, 4, 1, 2), ('MO-Walker2d-v2', 2048, 4, 1, 32)])
 def test_ppo_update(gpu, env, T, N, E, M, kernel, monkeypatch):
-    monkeypatch.setenv('PGM_UPDATE_KERNEL', kernel)
+    # mfma: critic/actor towers on two workgroups per task (default); mfma-joint: one workgroup per task
+    monkeypatch.setenv('PGM_UPDATE_KERNEL', kernel.split('-')[0])
+    monkeypatch.setenv('PGM_UPDATE_SPLIT', '0' if kernel == 'mfma-joint' else '1')
     P, lr = 2, 3e-4
     args, spec, tb, pols, data, perms = _update_setup(env, P, T, N, E, M, seed=11)
     obs, actions, logp, values, returns, adv = data
     tb.lr.fill_(lr)
     tb.ppo_update(torch.stack(perms).numpy())
+    assert int(tb.update_ws[2 * P]) == 0, 'tower exchange timed out'
     B = T * N
     for p in range(P):
         agent = oppo.PPO(pols[p], args.clip_param, E, M, args.value_loss_coef, args.entropy_coef, lr=lr, eps=1e-5,

@@ -52,6 +52,12 @@ def mflops_per_row(O, A, K, H=64):
     return 2 * (O * H + H * H) + H * A + H * K
 
 
+def bytes_per_env_step(O, A, K, E):
+    """Algorithmic HBM bytes per train env-step, fp32: rollout write, GAE read/write,
+    advantage pass, E epoch re-reads of obs/action/old logp/old V/R/adv."""
+    return 4 * ((O + A + 2 * K + 3) + (3 * K + 2) + (2 * K + 3) + E * (O + A + 2 * K + 2))
+
+
 def cpu_baseline(args, spec):
     """The oracle (fp64 torch restatement, 1 thread like morl/morl.py:34) on one task."""
     from oracle.mopg import initial_sample, mopg_worker
@@ -72,7 +78,9 @@ def cpu_baseline(args, spec):
     mopg_worker(ns, spec, s0, s0e, sample, w, 0, args.cpu_iters)
     dt = time.perf_counter() - t0
     steps = args.cpu_iters * args.num_processes * args.num_steps
+    busy = min(96, args.tasks * (1 + args.num_processes))  # per-core x min(96, P(1+N))
     return {'value': steps / dt, 'unit': 'env steps/sec', 'cores': 1, 'kind': 'port',
+            'extrapolated_96vcpu': steps / dt * busy, 'extrapolation': f'per-core value x {busy} busy processes',
             'sample': f'1 task x {args.cpu_iters} MOPG iterations ({steps} train env-steps, T={args.num_steps}, '
                       f'N={args.num_processes}, E={args.ppo_epoch}, M={args.num_mini_batch}, + eval) of the fp64 '
                       f'torch/numpy oracle, torch.set_num_threads(1), {dt:.1f} s on {platform.processor() or "host"}'
@@ -93,6 +101,7 @@ def main():
     from pgmorl_amd import envspec
     from pgmorl_amd.policy import new_policy
     from pgmorl_amd.runtime import TaskBatch
+    from pgmorl_amd.shard import allreduce_max
     spec = envspec.make_spec(args.env_name)
     P, N, T, E, M = args.tasks, args.num_processes, args.num_steps, args.ppo_epoch, args.num_mini_batch
     tb = TaskBatch(args.env_name, P, num_processes=N, num_steps=T, ppo_epoch=E, num_mini_batch=M, device=dev)
@@ -143,10 +152,7 @@ def main():
     dt = time.perf_counter() - t0
     tb.ppo_update = orig_update
     upd_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
-    if world > 1:
-        t = torch.tensor([dt, upd_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt, upd_ms = float(t[0]), float(t[1])
+    dt, upd_ms = allreduce_max([dt, upd_ms], dev)  # the slowest rank defines the step
     env_steps = world * P * N * T * args.steps
     value = env_steps / dt
     mf = mflops_per_row(spec['obs_dim'], spec['act_dim'], spec['obj_num'])
@@ -168,12 +174,22 @@ def main():
                                f'num_mini_batch={M}, eval_num=1, perf-mode device RNG',
                    'env': args.env_name, 'tasks_per_gpu': P, 'global_tasks': P * world, 'num_processes': N,
                    'num_steps': T, 'ppo_epoch': E, 'num_mini_batch': M, 'parallelism': f'task-sharded x{world}'},
-        'roofline': {'bound': 'mfma', 'kernel': 'ppo_update_kernel', 'achieved': achieved, 'peak': PEAK_FP32_TFLOPS,
-                     'unit': 'TFLOP/s', 'frac': achieved / PEAK_FP32_TFLOPS, 'traffic': traffic,
-                     'avg_launch_ms': upd_ms, 'flop_per_launch': upd_flop},
+        'roofline': {'bound': 'mfma', 'kernel': 'ppo_update_mfma_kernel', 'achieved': achieved,
+                     'peak': PEAK_FP32_TFLOPS, 'unit': 'TFLOP/s', 'frac': achieved / PEAK_FP32_TFLOPS,
+                     'traffic': traffic, 'avg_launch_ms': upd_ms, 'flop_per_launch': upd_flop,
+                     'algorithmic_bytes_per_launch': P * T * N * E * 4 * (spec['obs_dim'] + spec['act_dim'] +
+                                                                          2 * spec['obj_num'] + 2)},
+        # whole-iteration view: env-steps/s x algorithmic FLOP (or bytes) per env-step vs peak
+        'path_roofline': {'flop_per_env_step': 2 * mf * (1 + 3 * E),
+                          'compute_frac': value * 2 * mf * (1 + 3 * E) / (world * PEAK_FP32_TFLOPS * 1e12),
+                          'bytes_per_env_step': bytes_per_env_step(spec['obs_dim'], spec['act_dim'],
+                                                                   spec['obj_num'], E),
+                          'hbm_frac': value * bytes_per_env_step(spec['obs_dim'], spec['act_dim'], spec['obj_num'],
+                                                                 E) / (world * PEAK_HBM_GBS * 1e9)},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out['cpu_baseline'] = cpu_baseline(args, spec)
+        out['cpu_baseline'] = cb = cpu_baseline(args, spec)
+        out['vs_96vcpu_extrapolated'] = value / cb['extrapolated_96vcpu']
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -20,6 +20,7 @@ import torch
 
 from .runtime import TaskBatch
 from .sample import DeviceSnapshot, RunningMeanStd, Sample
+from .shard import allgather_rows, task_block, world
 
 
 def host_draws(j, T, N, A, E):
@@ -63,57 +64,94 @@ class MOPGPopulation:
         ep = sample.env_params or {}
         tb.set_env_params(p, {k: v for k, v in ep.items() if v is not None})
 
-    def _env_params(self, tb, host):
-        """Per-task RunningMeanStd copies (the snapshot of mopg.py:146-149) from one D2H batch."""
-        out = []
-        for p in range(tb.P):
-            ep = {'ob_rms': None, 'ret_rms': None, 'obj_rms': None}
-            if self.args.ob_rms:
-                r = RunningMeanStd(shape=(tb.O,))
-                r.mean, r.var, r.count = host['ob_mean'][p].copy(), host['ob_var'][p].copy(), float(host['ob_count'][p])
-                ep['ob_rms'] = r
+    def _record_width(self, tb):
+        return 3 * tb.K + 2 * tb.O + 6
+
+    def _records(self, tb):
+        """Per-task fp64 record of one iteration: objs[K], ob_mean/var[O], ob_count, ret mean/var/count,
+        obj_mean/var[K], obj_count, adam_step (the snapshot fields of mopg.py:146-155)."""
+        col = lambda x: x.reshape(tb.P, -1).to(torch.float64)
+        return torch.cat([col(tb.objs), col(tb.ob_mean), col(tb.ob_var), col(tb.ob_count), col(tb.ret_mean),
+                          col(tb.ret_var), col(tb.ret_count), col(tb.obj_mean), col(tb.obj_var), col(tb.obj_count),
+                          col(tb.adam_step)], 1)
+
+    def _unpack(self, rec, O, K):
+        """One host record row -> (objs, env_params RunningMeanStd copies, adam_step)."""
+        o = 0
+
+        def take(n):
+            nonlocal o
+            v = rec[o:o + n].copy()
+            o += n
+            return v
+        objs, ob_mean, ob_var, ob_count = take(K), take(O), take(O), take(1)[0]
+        ret_mean, ret_var, ret_count = take(1)[0], take(1)[0], take(1)[0]
+        obj_mean, obj_var, obj_count, step = take(K), take(K), take(1)[0], take(1)[0]
+        ep = {'ob_rms': None, 'ret_rms': None, 'obj_rms': None}
+        if self.args.ob_rms:
+            r = RunningMeanStd(shape=(O,))
+            r.mean, r.var, r.count = ob_mean, ob_var, float(ob_count)
+            ep['ob_rms'] = r
+        r = RunningMeanStd(shape=())
+        r.mean, r.var, r.count = np.float64(ret_mean), np.float64(ret_var), float(ret_count)
+        ep['ret_rms'] = r
+        if self.args.obj_rms:
             r = RunningMeanStd(shape=())
-            r.mean, r.var, r.count = np.float64(host['ret_mean'][p]), np.float64(host['ret_var'][p]), float(host['ret_count'][p])
-            ep['ret_rms'] = r
-            if self.args.obj_rms:
-                r = RunningMeanStd(shape=())
-                r.mean, r.var, r.count = host['obj_mean'][p].copy(), host['obj_var'][p].copy(), float(host['obj_count'][p])
-                ep['obj_rms'] = r
-            out.append(ep)
-        return out
+            r.mean, r.var, r.count = obj_mean, obj_var, float(obj_count)
+            ep['obj_rms'] = r
+        return objs, ep, int(step)
 
     def run(self, task_batch, iteration, num_updates, start_time=None, log=print):
+        """Every task's MOPG iterations [iteration, iteration + num_updates) -> all_offspring_batch.
+
+        Multi-GPU (torch.distributed initialised, one process per GPU): this rank runs its contiguous
+        block of tasks (shard.task_block); at the end of the generation one all-gather of the offspring
+        snapshots (params / Adam state fp32, records fp64) gives every rank the full result."""
         a = self.args
         P = len(task_batch)
-        tb = self._batch(P)
-        tb.reset_stats()
-        for p, task in enumerate(task_batch):
-            self.load_task(tb, p, task.sample, task.scalarization.weights.numpy())
-        tb.env_reset()  # envs are re-created and reset every generation (mopg.py:67-82)
+        rank, ws = world()
+        lo, hi = task_block(P, rank, ws)
+        Pl = hi - lo
         total = int(a.num_env_steps) // a.num_steps // a.num_processes
-        offspring = [[] for _ in range(P)]
+        its = list(range(iteration, min(iteration + num_updates, total)))
         start_time = time.time() if start_time is None else start_time
-        first = True
-        for j in range(iteration, min(iteration + num_updates, total)):
-            lr = linear_lr(j, total, a.lr, a.lr_decay_ratio) if a.use_linear_lr_decay else a.lr
-            noise = perms = None
-            if self.rng == 'host':
-                noise, perms = host_draws(j, a.num_steps, a.num_processes, tb.A, a.ppo_epoch)
-            tb.iteration(j, lr, noise=noise, perms=perms, carry=not first)
-            first = False
-            params, m, v = tb.params.clone(), tb.adam_m.clone(), tb.adam_v.clone()
-            host = {k: getattr(tb, k).cpu().numpy() for k in ('ob_mean', 'ob_var', 'ob_count', 'ret_mean', 'ret_var',
-                                                              'ret_count', 'obj_mean', 'obj_var', 'obj_count',
-                                                              'objs', 'adam_step')}
-            envp = self._env_params(tb, host)
-            for p in range(P):
-                snap = DeviceSnapshot(tb.layout, params[p], m[p], v[p], host['adam_step'][p])
-                offspring[p].append(Sample.from_snapshot(snap, envp[p], host['objs'][p].copy()))
-            if a.rl_log_interval > 0 and (j + 1) % a.rl_log_interval == 0:
-                steps = (j + 1) * a.num_processes * a.num_steps
-                dt = time.time() - start_time
-                log(f'[RL] Updates {j + 1}, num timesteps {steps}, FPS {int(steps / max(dt, 1e-9))}, '
-                    f'time {dt:.2f} seconds (x{P} tasks on {self.device})')
+        snaps32, recs = [], []
+        tb = None
+        if Pl > 0:
+            tb = self._batch(Pl)
+            tb.reset_stats()
+            for p, task in enumerate(task_batch[lo:hi]):
+                self.load_task(tb, p, task.sample, task.scalarization.weights.numpy())
+            tb.env_reset()  # envs are re-created and reset every generation (mopg.py:67-82)
+            for i, j in enumerate(its):
+                lr = linear_lr(j, total, a.lr, a.lr_decay_ratio) if a.use_linear_lr_decay else a.lr
+                noise = perms = None
+                if self.rng == 'host':
+                    noise, perms = host_draws(j, a.num_steps, a.num_processes, tb.A, a.ppo_epoch)
+                tb.iteration(j, lr, noise=noise, perms=perms, carry=i > 0)
+                snaps32.append(torch.stack([tb.params, tb.adam_m, tb.adam_v], 1))  # [Pl, 3, L] (a copy)
+                recs.append(self._records(tb))
+                if rank == 0 and a.rl_log_interval > 0 and (j + 1) % a.rl_log_interval == 0:
+                    steps = (j + 1) * a.num_processes * a.num_steps
+                    dt = time.time() - start_time
+                    log(f'[RL] Updates {j + 1}, num timesteps {steps}, FPS {int(steps / max(dt, 1e-9))}, '
+                        f'time {dt:.2f} seconds (x{P} tasks on {ws} device(s))')
+        probe = self._batch(1) if tb is None else tb
+        L, O, K = probe.layout.total, probe.O, probe.K
+        if snaps32:
+            s32, r64 = torch.stack(snaps32, 1), torch.stack(recs, 1)  # [Pl, I, 3, L], [Pl, I, S]
+        else:
+            s32 = torch.zeros(Pl, len(its), 3, L, device=self.device)
+            r64 = torch.zeros(Pl, len(its), self._record_width(probe), dtype=torch.float64, device=self.device)
+        if ws > 1:  # generation boundary: the only collective of the path
+            s32, r64 = allgather_rows(s32, P), allgather_rows(r64, P)
+        host = r64.cpu().numpy()
+        offspring = [[] for _ in range(P)]
+        for p in range(P):
+            for i in range(len(its)):
+                objs, envp, step = self._unpack(host[p, i], O, K)
+                snap = DeviceSnapshot(probe.layout, s32[p, i, 0], s32[p, i, 1], s32[p, i, 2], step)
+                offspring[p].append(Sample.from_snapshot(snap, envp, objs))
         return offspring
 
     def evaluate_samples(self, samples, weights_batch):

@@ -1,0 +1,51 @@
+"""Task sharding across GPUs and the generation-boundary exchange.
+
+Tasks never interact inside a generation (morl/mopg.py:60-182 touches only its own task), so each
+rank (one process per GPU) owns a contiguous block of ceil(P/G) tasks for the whole generation and
+the only collective is an all-gather at the generation boundary (morl/morl.py:90-125), where every
+rank needs every task's offspring (objective vectors, running statistics and the policy / Adam
+snapshot) to run the identical host EP / OptGraph / selection.  With the "nccl" backend (RCCL over
+xGMI on ROCm) the payload stays in HBM; the same code runs on "gloo" with CPU tensors (tests).
+"""
+import torch
+import torch.distributed as dist
+
+
+def world():
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
+def task_block(P, rank, world_size):
+    """[lo, hi) of the contiguous block of tasks owned by ``rank`` (ceil(P/G) per rank, last ones short)."""
+    per = -(-P // world_size)
+    lo = min(P, rank * per)
+    return lo, min(P, lo + per)
+
+
+def allgather_rows(local, P, group=None):
+    """Concatenate every rank's ``local`` rows ([P_local, ...], rank order) into [P, ...] on every rank.
+
+    Ranks may own different row counts (task_block); rows are padded to ceil(P/G) for the collective.
+    """
+    rank, ws = (dist.get_rank(group), dist.get_world_size(group)) if group is not None else world()
+    if ws == 1:
+        return local
+    per = -(-P // ws)
+    lo, hi = task_block(P, rank, ws)
+    if local.shape[0] != hi - lo:
+        raise ValueError(f'rank {rank}: {local.shape[0]} rows, block is {hi - lo}')
+    buf = local.new_zeros((per,) + tuple(local.shape[1:]))
+    buf[:hi - lo] = local
+    parts = [torch.empty_like(buf) for _ in range(ws)]
+    dist.all_gather(parts, buf.contiguous(), group=group)
+    return torch.cat([parts[r][:task_block(P, r, ws)[1] - task_block(P, r, ws)[0]] for r in range(ws)])
+
+
+def allreduce_max(values, device):
+    """Max over ranks of a few host floats (timing: the slowest rank defines the step time)."""
+    t = torch.tensor(list(values), dtype=torch.float64, device=device)
+    if world()[1] > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(x) for x in t]

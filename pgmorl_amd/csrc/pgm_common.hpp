@@ -21,20 +21,33 @@ struct Layout {
     int32_t total;
 };
 Layout make_layout(int O, int A, int K, int Hd);
-// pgm_ppo_update workspace: [2P] tagged 8-byte granules + 1 flag word, padded to 16 bytes
-inline size_t ppo_workspace_bytes(int P) { return ((size_t)(2 * P + 1) * 8 + 15) / 16 * 16; }
+// pgm_ppo_update workspace: [2P] tagged 8-byte granules + 1 flag word (padded to 256 bytes), then the
+// packed sample table [P][T*N][RS] fp32 (obs | action | old logp | adv | old value | return, RS a power of 2)
+inline int ppo_row_stride(int O, int A, int K) {
+    const int n = O + A + 2 + 2 * K;
+    return n <= 16 ? 16 : n <= 32 ? 32 : n <= 64 ? 64 : 128;
+}
+inline size_t ppo_flag_bytes(int P) { return ((size_t)(2 * P + 1) * 8 + 255) / 256 * 256; }
+inline size_t ppo_workspace_bytes(const pgm_dims* d) {
+    return ppo_flag_bytes(d->P) + (size_t)d->P * d->T * d->N * ppo_row_stride(d->O, d->A, d->K) * sizeof(float);
+}
 
 // ---------------------------------------------------------------- device helpers
-// Branch-free fp32 tanh (~12 VALU ops, rel. error ~3e-7): odd Taylor series through x^9 for |x| < 0.25
-// (truncation < 3e-9), 1 - 2/(exp(2|x|) + 1) above, with the sign restored.
+// Branch-free fp32 tanh (~14 VALU ops, rel. error ~3e-7): odd Taylor series through x^9 for |x| < 0.25
+// (truncation < 3e-9), 1 - 2/(exp(2|x|) + 1) above, with the sign restored.  Both branches are always
+// evaluated and blended arithmetically (s in {0, 1}: big + (poly - big) is exactly poly, the two being
+// within a factor 2) -- a select would be turned into control flow around the exp / rcp, which
+// serialises the surrounding MFMA work.  The polynomial argument is clamped so it stays finite.
 __device__ __forceinline__ float tanh_f(float x) {
     const float ax = fabsf(x);
-    const float x2 = x * x;
-    const float poly = x * fmaf(x2, fmaf(x2, fmaf(x2, fmaf(x2, 0.021869488536155203f, -0.05396825396825397f),
-                                                  0.13333333333333333f), -0.3333333333333333f), 1.0f);
+    const float xp = __builtin_amdgcn_fmed3f(x, -0.25f, 0.25f);
+    const float x2 = xp * xp;
+    const float poly = xp * fmaf(x2, fmaf(x2, fmaf(x2, fmaf(x2, 0.021869488536155203f, -0.05396825396825397f),
+                                                   0.13333333333333333f), -0.3333333333333333f), 1.0f);
     const float e = __expf(2.0f * ax);
-    const float big = 1.0f - 2.0f * __builtin_amdgcn_rcpf(e + 1.0f);
-    return ax < 0.25f ? poly : copysignf(big, x);
+    const float big = copysignf(1.0f - 2.0f * __builtin_amdgcn_rcpf(e + 1.0f), x);
+    const float s = ax < 0.25f ? 1.0f : 0.0f;
+    return fmaf(s, poly - big, big);
 }
 
 // xor-butterfly sum over aligned groups of W lanes (W power of two <= 64)
@@ -93,6 +106,10 @@ __device__ __forceinline__ float counter_normal(uint64_t seed, uint64_t i) {
 // one accumulator array + reader per translation unit (no relocatable device code)
 #define PGM_STAMP_UNIT(name)                                                                          \
     static __device__ unsigned long long pgm_stamp_acc[64];                                           \
+    static __device__ int pgm_stamp_block;                                                            \
+    extern "C" int pgm_debug_stamp_block_##name(int b) {                                              \
+        return hipMemcpyToSymbol(HIP_SYMBOL(pgm_stamp_block), &b, sizeof(int)) == hipSuccess ? PGM_OK : PGM_E_HIP; \
+    }                                                                                                 \
     extern "C" int pgm_debug_stamps_##name(unsigned long long* out, int reset) {                      \
         if (hipMemcpyFromSymbol(out, HIP_SYMBOL(pgm_stamp_acc), sizeof(unsigned long long) * 64) !=  \
             hipSuccess)                                                                               \
@@ -106,7 +123,7 @@ __device__ __forceinline__ float counter_normal(uint64_t seed, uint64_t i) {
 #define PGM_STAMP_DECL unsigned long long pgm_stamp_last = __builtin_amdgcn_s_memtime();
 #define PGM_STAMP(id)                                                            \
     do {                                                                         \
-        if (blockIdx.x == 0 && threadIdx.x == 0) {                               \
+        if ((int)blockIdx.x == pgm_stamp_block && threadIdx.x == 0) {                               \
             unsigned long long now_ = __builtin_amdgcn_s_memtime();              \
             atomicAdd(&pgm_stamp_acc[id], now_ - pgm_stamp_last);              \
             pgm_stamp_last = now_;                                               \

@@ -1,19 +1,26 @@
 // Scalarised clipped-PPO update on the f32 matrix cores (v_mfma_f32_32x32x2_f32, exact fp32).
 //
-// One 256-thread workgroup per task, 4 waves: wave w runs tower m = w & 1 (0 critic, 1 actor) on
-// the sample tiles (32 samples each) t = (w >> 1) + 2i of the minibatch.  Orientation: samples are
-// the accumulator ROWS (registers), features the COLUMNS (lanes), i.e. for a 32-sample tile every
-// activation H1, H2, dZ2, dZ1 lives in the standard C layout
+// Work split.  SPLIT mode (default while 2P <= CUs): two 256-thread workgroups per task, one per tower
+// (critic / actor), each on its own CU; the only coupling inside a minibatch step is the global grad
+// norm, exchanged as one tagged 8-byte granule per step.  Parameters AND Adam moments of the tower stay
+// in LDS for the whole launch (one HBM read at the start, one write at the end).  Joint mode: one
+// workgroup per task, waves 0/2 critic and 1/3 actor, Adam moments in HBM.
+//
+// Staging.  pack_rows_kernel first writes a packed sample table, one RS-float row per sample
+// (obs | action | old logp | adv | old value | return; 128 B for Walker).  The update consumes the
+// permuted rows of each minibatch in passes of SBk samples, staged HBM -> LDS by global_load_lds
+// (16 B per lane, no VGPRs) one pass AHEAD into a second buffer, with the permutation indices of the
+// pass after that staged the same way (4-B LDS-DMA) one pass earlier still.
+//
+// Tiles.  32 samples per MFMA tile; samples are the accumulator ROWS (registers), features the
+// COLUMNS (lanes), i.e. every activation H1, H2, dZ2, dZ1 lives in the standard C layout
 //     lane l, register r  <->  (sample rowof(r, l>>5), feature l & 31),  rowof(r,h) = (r&3)+8(r>>2)+4h.
-// Consequences:
-//   * every weight gradient (dW2^T = H1^T dZ2, dW1^T = X^T dZ1) sums over the sample index, i.e.
-//     over registers: MFMA(A = H1 reg r, B = dZ2 reg r) with no data movement at all;
-//   * the two products that sum over a FEATURE index (Z2 = H1 W2^T and dH1 = dZ2 W2) take their A
-//     operand from a per-wave [32][65] LDS tile written from the C layout (one ds_write per register);
-//   * the value / mean heads and the per-sample losses run on the VALU, one sample per lane.
-// Gradients accumulate in registers over the minibatch; the two waves of a tower then add theirs
-// into an LDS gradient image in parameter layout (fixed order => deterministic), followed by
-// clip_grad_norm_ and Adam as one coalesced pass over the flat parameter vector.
+//   * weight gradients (dW2^T = H1^T dZ2, dW1^T = X^T dZ1) sum over samples = over registers:
+//     MFMA(A = H1 reg r, B = dZ2 reg r), no data movement;
+//   * the products summing over a FEATURE (Z2 = H1 W2^T, dH1 = dZ2 W2) take A from a per-wave [32][65]
+//     LDS transpose tile; the value / mean heads and the per-sample losses run on the VALU.
+// Gradients accumulate in registers over the minibatch and are reduced across the tower's waves into
+// two LDS images in a fixed order (deterministic); clip_grad_norm_ and Adam are flat passes.
 //
 // Reference semantics: a2c_ppo_acktr/algo/ppo.py:58-115 (losses, clip_grad_norm_, Adam),
 // a2c_ppo_acktr/storage.py:118-154 (minibatch rows), a2c_ppo_acktr/model.py:75-82,
@@ -28,16 +35,19 @@ PGM_STAMP_UNIT(mfma)
 namespace pgm {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) void lds_void_t;
 
 constexpr int MT = 256;     // threads: 4 waves
-constexpr int SB = 256;     // samples staged per pass (minibatches larger than this loop over passes)
 constexpr int TS = 32;      // samples per MFMA tile
 constexpr int SCR = H + 1;  // per-wave transpose tile row stride (conflict-free column reads)
 
-template <int O>
-constexpr int ox() { return O | 1; }  // odd X-image stride: conflict-free A-operand reads
 template <int A, int K>
 constexpr int qmax() { return A > K ? A : K; }
+template <int O, int A, int K>
+constexpr int row_stride() {
+    constexpr int n = O + A + 2 + 2 * K;
+    return n <= 16 ? 16 : n <= 32 ? 32 : n <= 64 ? 64 : 128;
+}
 
 __device__ __forceinline__ int rowof(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 __device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
@@ -47,37 +57,111 @@ __device__ __forceinline__ void wave_lds_fence() {  // this wave's LDS writes ar
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
 }
+// workgroup barrier that leaves in-flight LDS-DMA (vmcnt) alone
 __device__ __forceinline__ void lds_sync_m() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+// retire this wave's LDS-DMA / loads, then the barrier
+__device__ __forceinline__ void dma_sync_m() {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
 __device__ __forceinline__ float xhalf(float v) {  // value of lane l ^ 32
     return __shfl_xor(v, 32, 64);
 }
 
-template <int O, int A, int K>
-struct MSmem {
-    static constexpr int Q = qmax<A, K>();
-    // parameter working copy (LDS images, fp32)
-    float W1t[2][O][H];        // [tower][in][out]
-    float W2t[2][H][SCR];      // [tower][in][out], padded rows
-    float Wh[2][Q][H];         // [tower][head output][unit]  (critic: value, actor: mean)
-    float b1[2][H], b2[2][H], bh[2][Q], logstd[A];
-    // per-pass staged rows
-    float act[SB][A];
-    float oldlp[SB], adv[SB];
-    float vold[SB][K], ret[SB][K];
-    float dout[4][TS][Q];      // per-wave dL/d(head output) of the current tile
-    float red[16];
-    // big region: X image + per-wave transpose tiles during the passes, gradient image at the end
-    union Big {
-        struct {
-            float X[SB][ox<O>()];
-            float scr[4][TS][SCR];
-        } s;
-        float G[1];
-    } big;
+// ---------------------------------------------------------------- packed sample table
+struct PackArgs {
+    int P, N, T;
+    const float *obs, *actions, *logp, *adv, *values, *returns;
+    float* rows;  // [P][T*N][RS]
 };
 
 template <int O, int A, int K>
-constexpr size_t big_floats() { return sizeof(typename MSmem<O, A, K>::Big) / sizeof(float); }
+__global__ __launch_bounds__(256) void pack_rows_kernel(PackArgs a) {
+    constexpr int RS = row_stride<O, A, K>();
+    const int B = a.T * a.N, BV = (a.T + 1) * a.N;  // rows per task; obs / value slots per task
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;  // one float4 of one row
+    if (i >= (long long)a.P * B * (RS / 4)) return;
+    const long long row = i / (RS / 4);
+    const int k0 = (int)(i - row * (RS / 4)) * 4;
+    const int p = (int)(row / B), b = (int)(row - (long long)p * B);
+    float4 v;
+    float* vp = &v.x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int k = k0 + j;
+        float x = 0.f;
+        if (k < O) x = a.obs[((size_t)p * BV + b) * O + k];
+        else if (k < O + A) x = a.actions[((size_t)p * B + b) * A + (k - O)];
+        else if (k == O + A) x = a.logp[(size_t)p * B + b];
+        else if (k == O + A + 1) x = a.adv[(size_t)p * B + b];
+        else if (k < O + A + 2 + K) x = a.values[((size_t)p * BV + b) * K + (k - O - A - 2)];
+        else if (k < O + A + 2 + 2 * K) x = a.returns[((size_t)p * BV + b) * K + (k - O - A - 2 - K)];
+        vp[j] = x;
+    }
+    *reinterpret_cast<float4*>(a.rows + (size_t)row * RS + k0) = v;
+}
+
+// ---------------------------------------------------------------- tower images
+// One tower's parameters as an LDS image: W1^T [in][out], W2^T [in][out] with a padded row stride,
+// head weights [output][unit], biases, logstd (actor only).  Padding slots and head rows beyond the
+// tower's output count hold zeros for the whole launch (their gradient, Adam moments and update are 0).
+// The same image type holds gradients and (SPLIT) the Adam moments, so clip_grad_norm_ and Adam are
+// flat passes over images, and the working copy IS the master copy until the launch writes it back.
+template <int O, int A, int K>
+struct TowerImg {
+    static constexpr int Q = qmax<A, K>();
+    float W1t[O][H];
+    float W2t[H][SCR];
+    float Wh[Q][H];
+    float b1[H], b2[H], bh[Q], logstd[A];
+};
+template <int O, int A, int K>
+constexpr int img_floats() { return (int)(sizeof(TowerImg<O, A, K>) / sizeof(float)); }
+
+// image slot -> flat parameter index (pgm_param_layout order), -1 for padding / unused slots
+template <int O, int A, int K>
+__device__ __forceinline__ int img_to_flat(int i, int m, const Layout& L) {
+    constexpr int Q = qmax<A, K>();
+    constexpr int s1 = O * H, s2 = s1 + H * SCR, s3 = s2 + Q * H, s4 = s3 + H, s5 = s4 + H, s6 = s5 + Q, s7 = s6 + A;
+    const int NQ = m == 0 ? K : A;
+    if (i < s1) return L.off[m ? PGM_P_ACTOR_W1 : PGM_P_CRITIC_W1] + i;
+    if (i < s2) {
+        const int j = i - s1, in = j / SCR, o = j - in * SCR;
+        return o < H ? L.off[m ? PGM_P_ACTOR_W2 : PGM_P_CRITIC_W2] + in * H + o : -1;
+    }
+    if (i < s3) {  // reference head weight [NQ][H] stored transposed [H][NQ]
+        const int j = i - s2, q = j / H, u = j - q * H;
+        return q < NQ ? L.off[m ? PGM_P_MEAN_W : PGM_P_VALUE_W] + u * NQ + q : -1;
+    }
+    if (i < s4) return L.off[m ? PGM_P_ACTOR_B1 : PGM_P_CRITIC_B1] + (i - s3);
+    if (i < s5) return L.off[m ? PGM_P_ACTOR_B2 : PGM_P_CRITIC_B2] + (i - s4);
+    if (i < s6) return (i - s5) < NQ ? L.off[m ? PGM_P_MEAN_B : PGM_P_VALUE_B] + (i - s5) : -1;
+    if (i < s7) return m ? L.off[PGM_P_LOGSTD] + (i - s6) : -1;
+    return -1;
+}
+
+template <int O, int A, int K, bool SPLIT, int NBUF>
+struct MSmemT {
+    static constexpr int Q = qmax<A, K>();
+    static constexpr int NT = SPLIT ? 1 : 2;  // tower images held by the workgroup
+    static constexpr int IMG = img_floats<O, A, K>();
+    static constexpr int RS = row_stride<O, A, K>();
+    static constexpr int SBk = RS <= 32 ? 128 : 64;  // samples staged per pass
+    TowerImg<O, A, K> Pm[NT];              // parameters
+    float MV[SPLIT ? 2 * IMG : 1];         // SPLIT: Adam exp_avg | exp_avg_sq images (else in HBM)
+    alignas(16) float RB[NBUF][SBk * RS];  // packed rows of the current / next pass (swizzled chunks)
+    int32_t IB[2][SBk];                    // sample indices of the next two passes
+    float dout[4][TS][Q];                  // per-wave dL/d(head output) of the current tile
+    float red[16];
+    union Big {                            // transpose tiles during the passes, gradient images after
+        float scr[4][TS][SCR];
+        float GA[2][IMG];
+    } big;
+};
+
+template <int O, int A, int K, bool SPLIT>
+constexpr int nbuf() { return sizeof(MSmemT<O, A, K, SPLIT, 2>) <= 160 * 1024 ? 2 : 1; }
+template <int O, int A, int K, bool SPLIT>
+using MSmem = MSmemT<O, A, K, SPLIT, nbuf<O, A, K, SPLIT>()>;
 
 struct MArgs {
     int N, T;
@@ -87,7 +171,7 @@ struct MArgs {
     int32_t* step;
     const float* lr;
     const int32_t* perms;
-    const float *obs, *actions, *logp, *values, *returns, *adv;
+    const float* rows;       // packed sample table [P][T*N][RS]
     float* stats;
     unsigned long long* ws;  // SPLIT: [2P] tagged granules + [1] timeout flag, zeroed before the launch
     int P;
@@ -96,67 +180,81 @@ struct MArgs {
 __device__ __forceinline__ float wmin2(float a, float b) { return a < b ? 1.f : (a == b ? 0.5f : 0.f); }
 __device__ __forceinline__ float wmax2(float a, float b) { return a > b ? 1.f : (a == b ? 0.5f : 0.f); }
 
-// Visit every parameter tensor with its LDS working-copy slot: f(tensor id, count, slot(j)).
-template <int O, int A, int K, class F>
-__device__ __forceinline__ void for_each_tensor(MSmem<O, A, K>& S, F&& f) {
-    f(PGM_P_ACTOR_W1, O * H, [&](int j) { return &S.W1t[1][0][0] + j; });
-    f(PGM_P_ACTOR_B1, H, [&](int j) { return &S.b1[1][j]; });
-    f(PGM_P_ACTOR_W2, H * H, [&](int j) { return &S.W2t[1][j / H][j % H]; });
-    f(PGM_P_ACTOR_B2, H, [&](int j) { return &S.b2[1][j]; });
-    f(PGM_P_CRITIC_W1, O * H, [&](int j) { return &S.W1t[0][0][0] + j; });
-    f(PGM_P_CRITIC_B1, H, [&](int j) { return &S.b1[0][j]; });
-    f(PGM_P_CRITIC_W2, H * H, [&](int j) { return &S.W2t[0][j / H][j % H]; });
-    f(PGM_P_CRITIC_B2, H, [&](int j) { return &S.b2[0][j]; });
-    f(PGM_P_VALUE_W, H * K, [&](int j) { return &S.Wh[0][j % K][j / K]; });
-    f(PGM_P_VALUE_B, K, [&](int j) { return &S.bh[0][j]; });
-    f(PGM_P_MEAN_W, H * A, [&](int j) { return &S.Wh[1][j % A][j / A]; });
-    f(PGM_P_MEAN_B, A, [&](int j) { return &S.bh[1][j]; });
-    f(PGM_P_LOGSTD, A, [&](int j) { return &S.logstd[j]; });
-}
-
 template <int O, int A, int K, bool SPLIT>
 __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-    auto& S = *reinterpret_cast<MSmem<O, A, K>*>(smem_raw);
+    using Sm = MSmem<O, A, K, SPLIT>;
+    auto& S = *reinterpret_cast<Sm*>(smem_raw);
     constexpr int Q = qmax<A, K>();
-    constexpr int OX = ox<O>();
     constexpr int KS1 = (O + 1) / 2;  // k-steps of layer 1
-    // SPLIT: two workgroups per task (blockIdx = 2 task + tower), all 4 waves on one tower, exchanging
-    // only the squared gradient norm per minibatch.  Otherwise one workgroup: waves 0/2 critic, 1/3 actor.
+    constexpr int IMG = Sm::IMG, NT = Sm::NT, SBk = Sm::SBk, RS = Sm::RS;
+    constexpr int NBUF = nbuf<O, A, K, SPLIT>();
+    constexpr int CR = RS / 4;           // 16-B chunks per row
+    constexpr int RPI = 64 / CR;         // rows per LDS-DMA wave instruction
+    constexpr int NDMA = SBk / RPI / 4;  // LDS-DMA instructions per wave per pass
+    static_assert(NDMA >= 1 && NDMA * RPI * 4 == SBk, "staging split");
+    constexpr int oW2 = O * H, oWh = oW2 + H * SCR, oB1 = oWh + Q * H, oB2 = oB1 + H, oBh = oB2 + H, oLs = oBh + Q;
     constexpr int NWT = SPLIT ? 4 : 2;  // waves per tower
     const int t = threadIdx.x, w = t >> 6, l = t & 63, h = l >> 5, c = l & 31;
     const int p = SPLIT ? (int)(blockIdx.x >> 1) : (int)blockIdx.x;
-    const int m = SPLIT ? (int)(blockIdx.x & 1) : (w & 1);  // tower
+    const int m = SPLIT ? (int)(blockIdx.x & 1) : (w & 1);  // tower of this wave
     const int sh = SPLIT ? w : (w >> 1);                      // wave index within the tower
     const int NQ = m == 0 ? K : A;
     const int N = a.N, T = a.T, B = T * N;
     const int E = a.hp.ppo_epoch, M = a.hp.num_mini_batch;
     const int mb = B / M, nb = B / mb;
+    const int npm = (mb + SBk - 1) / SBk;  // passes per minibatch
+    const int npass = E * nb * npm;
     const float clip = a.hp.clip_param;
     const Layout& L = a.L;
     float* __restrict__ P = a.params + (size_t)p * L.total;
     float* __restrict__ Mo = a.m + (size_t)p * L.total;
     float* __restrict__ Vo = a.v + (size_t)p * L.total;
-    const float* obs = a.obs + (size_t)p * (T + 1) * N * O;
-    const float* actions = a.actions + (size_t)p * B * A;
-    const float* logp = a.logp + (size_t)p * B;
-    const float* values = a.values + (size_t)p * (T + 1) * N * K;
-    const float* returns = a.returns + (size_t)p * (T + 1) * N * K;
-    const float* advs = a.adv + (size_t)p * B;
+    const float* rows = a.rows + (size_t)p * B * RS;
+    auto img_tower = [&](int mi) { return SPLIT ? m : mi; };  // tower of image mi
 
-    // ---- parameter working copy
-    for_each_tensor(S, [&](int tsr, int n, auto slot) {
-        const int off = L.off[tsr];
-#pragma unroll 4
-        for (int j = t; j < n; j += MT) *slot(j) = P[off + j];
-    });
-    for (int i = t; i < 2 * Q * H; i += MT) {  // head rows beyond K (critic) stay zero
-        const int mm = i / (Q * H), q = (i / H) % Q;
-        if (q >= (mm == 0 ? K : A)) S.Wh[mm][q][i % H] = 0.f;
+    // ---- staging: pass gp = ((e * nb) + bb) * npm + j covers minibatch rows [j*SBk, j*SBk + ns).
+    // The pass's permutation indices go first into IB (4-B LDS-DMA, one pass earlier than the rows).
+    // Row DMA: lane l of wave w, instruction d: row (w*NDMA + d)*RPI + l/CR, 16-B chunk l%CR.
+    auto issue_idx = [&](int g, int buf) {
+        const int e = g / (nb * npm), rem = g - e * nb * npm, bb = rem / npm, j = rem - bb * npm;
+        const int ns = min(SBk, mb - j * SBk);
+        const int32_t* src = a.perms + (size_t)e * B + bb * mb + j * SBk;
+        for (int r0 = w * 64; r0 < SBk; r0 += 256)  // rows beyond ns re-read the last valid index
+            __builtin_amdgcn_global_load_lds((const void*)(src + min(r0 + l, ns - 1)),
+                                             (lds_void_t*)&S.IB[buf][r0], 4, 0, 0);
+    };
+    auto issue_rows = [&](int buf, int ibuf) {
+        float* base = &S.RB[buf][0];
+#pragma unroll
+        for (int d = 0; d < NDMA; ++d) {
+            const int row = (w * NDMA + d) * RPI + l / CR;
+            const float* src = rows + (size_t)S.IB[ibuf][row] * RS + (l % CR) * 4;
+            float* dst = base + (w * NDMA + d) * RPI * RS;  // wave-uniform
+            __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_t*)dst, 16, 0, 0);
+        }
+    };
+    // element k of row cs of a tile starting at rt (plain row-major: one address register per lane;
+    // the per-sample column reads of a tile are 16-way bank conflicted, ~25 reads per tile)
+    auto rowf = [&](const float* rt, int cs, int k) { return rt[cs * RS + k]; };
+
+    // ---- parameter (and SPLIT: Adam moment) images from the flat HBM vectors
+    float* Pf = &S.Pm[0].W1t[0][0];
+    for (int i = t; i < NT * IMG; i += MT) {
+        const int mi = i / IMG, f = img_to_flat<O, A, K>(i - mi * IMG, img_tower(mi), L);
+        Pf[i] = f >= 0 ? P[f] : 0.f;
+        if constexpr (SPLIT) {
+            S.MV[i] = f >= 0 ? Mo[f] : 0.f;
+            S.MV[IMG + i] = f >= 0 ? Vo[f] : 0.f;
+        }
     }
-    for (int i = t; i < 2 * Q; i += MT)
-        if (i % Q >= (i / Q == 0 ? K : A)) S.bh[i / Q][i % Q] = 0.f;
-    __syncthreads();
+    issue_idx(0, 0);
+    if (npass > 1) issue_idx(1, 1);
+    dma_sync_m();
+    issue_rows(0, 0);
+    dma_sync_m();
+    auto& W = S.Pm[SPLIT ? 0 : m];                   // this wave's tower
+    const float* lstd = S.Pm[SPLIT ? 0 : 1].logstd;  // actor logstd (SPLIT critic: zeros, unused)
 
     const int step0 = a.step[p];
     const double lr = a.lr[p];
@@ -164,12 +262,12 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
     const float vscale = a.hp.value_loss_coef * 0.5f / (float)(mb * K);
     const float ascale = -1.f / (float)mb;
     float st_v = 0.f, st_a = 0.f, st_e = 0.f;
-    int nstep = 0;
-    float* scr = &S.big.s.scr[w][0][0];
+    int nstep = 0, gp = 0;
+    double b1p = pow((double)b1c, (double)step0), b2p = pow((double)b2c, (double)step0);
+    float* scr = &S.big.scr[w][0][0];
     PGM_STAMP_DECL
 
     for (int e = 0; e < E; ++e) {
-        const int32_t* perm = a.perms + (size_t)e * B;
         for (int bb = 0; bb < nb; ++bb) {
             f32x16 gW2[2][2], gW1[2];  // [in tile][out tile], [out tile] (O <= 32: one in tile)
             float gWh[2][Q], gB1[2], gB2[2], gBh[Q], gLs[A];
@@ -188,45 +286,33 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
             for (int q = 0; q < A; ++q) gLs[q] = 0.f;
             float lsum = 0.f;
 
-            for (int s0 = 0; s0 < mb; s0 += SB) {
-                const int ns = min(SB, mb - s0);
-                // ---- stage rows perm[bb*mb + s0 + i]: X image and per-sample data
-                for (int i = t; i < SB; i += MT) {
-                    const bool ok = i < ns;
-                    const int idx = ok ? perm[bb * mb + s0 + i] : 0;
-#pragma unroll
-                    for (int k = 0; k < OX; ++k) S.big.s.X[i][k] = (ok && k < O) ? obs[(size_t)idx * O + k] : 0.f;
-                    S.oldlp[i] = ok ? logp[idx] : 0.f;
-                    S.adv[i] = ok ? advs[idx] : 0.f;
-#pragma unroll
-                    for (int q = 0; q < A; ++q) S.act[i][q] = ok ? actions[(size_t)idx * A + q] : 0.f;
-#pragma unroll
-                    for (int q = 0; q < K; ++q) {
-                        S.vold[i][q] = ok ? values[(size_t)idx * K + q] : 0.f;
-                        S.ret[i][q] = ok ? returns[(size_t)idx * K + q] : 0.f;
-                    }
+            for (int s0 = 0; s0 < mb; s0 += SBk, ++gp) {
+                const int ns = min(SBk, mb - s0);
+                const int cur = NBUF == 2 ? (gp & 1) : 0;
+                if constexpr (NBUF == 2) {  // stage the next pass while this one computes
+                    if (gp + 1 < npass) issue_rows(cur ^ 1, (gp + 1) & 1);
+                    if (gp + 2 < npass) issue_idx(gp + 2, gp & 1);
                 }
-                lds_sync_m();
+                const float* rb = &S.RB[cur][0];
                 PGM_STAMP(0);
 
                 for (int tile = sh; tile * TS < ns; tile += NWT) {
                     const int ts0 = tile * TS;
-                    // ---- layer 1: Z1[s][h] = X[s][:] . W1t[:][h]
+                    const float* rt = rb + ts0 * RS;  // this tile's staged rows
+                    // ---- layer 1: Z1[s][h] = X[s][:] . W1t[:][h]  (two independent accumulator chains
+                    // interleaved: the 32x32x2 f32 MFMA has a 64-cycle dependent-accumulator latency)
                     f32x16 z[2] = {f32x16{0}, f32x16{0}};
 #pragma unroll
                     for (int ks = 0; ks < KS1; ++ks) {
                         const int k = 2 * ks + h;
-                        const float av = k < O ? S.big.s.X[ts0 + c][k] : 0.f;
+                        const float av = k < O ? rowf(rt, c, k) : 0.f;
 #pragma unroll
-                        for (int hb = 0; hb < 2; ++hb) {
-                            const float bv = k < O ? S.W1t[m][k][hb * TS + c] : 0.f;
-                            z[hb] = mfma(av, bv, z[hb]);
-                        }
+                        for (int hb = 0; hb < 2; ++hb) z[hb] = mfma(av, k < O ? W.W1t[k][hb * TS + c] : 0.f, z[hb]);
                     }
                     f32x16 H1[2];
 #pragma unroll
                     for (int hb = 0; hb < 2; ++hb) {
-                        const float bias = S.b1[m][hb * TS + c];
+                        const float bias = W.b1[hb * TS + c];
 #pragma unroll
                         for (int r = 0; r < 16; ++r) {
                             H1[hb][r] = tanh_f(z[hb][r] + bias);
@@ -241,15 +327,16 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                         const int k = 2 * ks + h;
                         const float av = scr[c * SCR + k];
 #pragma unroll
-                        for (int ob = 0; ob < 2; ++ob) z[ob] = mfma(av, S.W2t[m][k][ob * TS + c], z[ob]);
+                        for (int ob = 0; ob < 2; ++ob) z[ob] = mfma(av, W.W2t[k][ob * TS + c], z[ob]);
                     }
                     f32x16 H2[2];
 #pragma unroll
                     for (int ob = 0; ob < 2; ++ob) {
-                        const float bias = S.b2[m][ob * TS + c];
+                        const float bias = W.b2[ob * TS + c];
 #pragma unroll
                         for (int r = 0; r < 16; ++r) H2[ob][r] = tanh_f(z[ob][r] + bias);
                     }
+                    PGM_STAMP(4);
                     wave_lds_fence();  // every lane finished reading the H1 tile
 #pragma unroll
                     for (int ob = 0; ob < 2; ++ob)
@@ -264,10 +351,10 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                     for (int u = 0; u < TS; ++u) {
                         const float hv = scr[c * SCR + h * TS + u];
 #pragma unroll
-                        for (int q = 0; q < Q; ++q) outv[q] = fmaf(hv, S.Wh[m][q][h * TS + u], outv[q]);
+                        for (int q = 0; q < Q; ++q) outv[q] = fmaf(hv, W.Wh[q][h * TS + u], outv[q]);
                     }
 #pragma unroll
-                    for (int q = 0; q < Q; ++q) outv[q] += xhalf(outv[q]) + S.bh[m][q];
+                    for (int q = 0; q < Q; ++q) outv[q] += xhalf(outv[q]) + W.bh[q];
                     // ---- per-sample loss gradients (ppo.py:80-96); both halves compute the same sample
                     const int si = ts0 + c;
                     const bool ok = si < ns;
@@ -278,7 +365,8 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                         float ls = 0.f;
 #pragma unroll
                         for (int q = 0; q < K; ++q) {
-                            const float V = outv[q], Vo = S.vold[si][q], R = S.ret[si][q];
+                            const float V = outv[q], Vo = rowf(rt, c, O + A + 2 + q);
+                            const float R = rowf(rt, c, O + A + 2 + K + q);
                             float gv;
                             if (a.hp.use_clipped_value_loss) {
                                 const float dv = V - Vo;
@@ -298,12 +386,11 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                         float lp = 0.f;
 #pragma unroll
                         for (int q = 0; q < A; ++q) {
-                            const float sd = expf(S.logstd[q]);
-                            const float dz = (S.act[si][q] - outv[q]) / sd;
-                            lp += -0.5f * dz * dz - S.logstd[q] - LOG_SQRT_2PI;
+                            const float dz = (rowf(rt, c, O + q) - outv[q]) / expf(lstd[q]);
+                            lp += -0.5f * dz * dz - lstd[q] - LOG_SQRT_2PI;
                         }
-                        const float ratio = expf(lp - S.oldlp[si]);
-                        const float ad = S.adv[si];
+                        const float ratio = expf(lp - rowf(rt, c, O + A));
+                        const float ad = rowf(rt, c, O + A + 1);
                         const float s1 = ratio * ad;
                         const float s2 = fminf(fmaxf(ratio, 1.f - clip), 1.f + clip) * ad;
                         const float inr = (ratio >= 1.f - clip && ratio <= 1.f + clip) ? 1.f : 0.f;
@@ -312,8 +399,8 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                         if (ok && h == 0) lsum += -fminf(s1, s2);
 #pragma unroll
                         for (int q = 0; q < A; ++q) {
-                            const float sd = expf(S.logstd[q]);
-                            const float diff = S.act[si][q] - outv[q];
+                            const float sd = expf(lstd[q]);
+                            const float diff = rowf(rt, c, O + q) - outv[q];
                             const float iv = 1.f / (sd * sd);
                             dO[q] = dlp * diff * iv;
                             if (h == 0) gLs[q] += dlp * (diff * diff * iv - 1.f);
@@ -327,6 +414,7 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                         }
                     }
                     wave_lds_fence();
+                    PGM_STAMP(5);
                     // ---- head-weight grads (VALU, C layout): gWh[ob][q] += sum_r H2[s][u] dO[s][q]
 #pragma unroll
                     for (int ob = 0; ob < 2; ++ob)
@@ -343,7 +431,7 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                         const int q = 2 * ks + h;
                         const float av = h ? (2 * ks + 1 < Q ? dO[2 * ks + 1] : 0.f) : dO[2 * ks];
 #pragma unroll
-                        for (int ob = 0; ob < 2; ++ob) z[ob] = mfma(av, q < Q ? S.Wh[m][q][ob * TS + c] : 0.f, z[ob]);
+                        for (int ob = 0; ob < 2; ++ob) z[ob] = mfma(av, q < Q ? W.Wh[q][ob * TS + c] : 0.f, z[ob]);
                     }
                     f32x16 dZ2[2];
 #pragma unroll
@@ -360,6 +448,7 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                         for (int ib = 0; ib < 2; ++ib)
 #pragma unroll
                             for (int ob = 0; ob < 2; ++ob) gW2[ib][ob] = mfma(H1[ib][r], dZ2[ob][r], gW2[ib][ob]);
+                    PGM_STAMP(6);
                     // ---- dH1 = dZ2 W2  (A = dZ2 through the transpose tile, B = W2t[in][o] column)
                     wave_lds_fence();  // heads finished reading the H2 tile
 #pragma unroll
@@ -373,7 +462,7 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                         const int k = 2 * ks + h;  // output unit o
                         const float av = scr[c * SCR + k];
 #pragma unroll
-                        for (int ib = 0; ib < 2; ++ib) z[ib] = mfma(av, S.W2t[m][ib * TS + c][k], z[ib]);
+                        for (int ib = 0; ib < 2; ++ib) z[ib] = mfma(av, W.W2t[ib * TS + c][k], z[ib]);
                     }
                     f32x16 dZ1[2];
 #pragma unroll
@@ -386,13 +475,23 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                     // ---- dW1^T[k][h] += X^T dZ1  (A = X[s(r)][k = lane], B = dZ1 reg r)
 #pragma unroll
                     for (int r = 0; r < 16; ++r) {
-                        const float av = S.big.s.X[ts0 + rowof(r, h)][c < OX ? c : 0];
+                        const float av = c < O ? rowf(rt, rowof(r, h), c) : 0.f;
 #pragma unroll
-                        for (int hb = 0; hb < 2; ++hb) gW1[hb] = mfma(c < O ? av : 0.f, dZ1[hb][r], gW1[hb]);
+                        for (int hb = 0; hb < 2; ++hb) gW1[hb] = mfma(av, dZ1[hb][r], gW1[hb]);
                     }
                     wave_lds_fence();  // dH1 finished reading the dZ2 tile before the next tile's writes
+                    PGM_STAMP(7);
                 }  // tiles
-                lds_sync_m();  // X / per-sample rows are re-staged by the next pass
+                if constexpr (NBUF == 2) {
+                    dma_sync_m();  // next pass landed (issued a pass ago); this buffer free for reuse
+                } else {
+                    lds_sync_m();
+                    if (gp + 1 < npass) {
+                        issue_rows(0, (gp + 1) & 1);
+                        if (gp + 2 < npass) issue_idx(gp + 2, gp & 1);
+                        dma_sync_m();
+                    }
+                }
                 PGM_STAMP(1);
             }  // passes
 
@@ -413,67 +512,105 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
             // entropy with the logstd of this step (before Adam)
             float ent = 0.f;
 #pragma unroll
-            for (int q = 0; q < A; ++q) ent += 0.5f + LOG_SQRT_2PI + S.logstd[q];
+            for (int q = 0; q < A; ++q) ent += 0.5f + LOG_SQRT_2PI + lstd[q];
 
-            // ---- gradient image in parameter layout: zero, sample-half 0 stores, sample-half 1 adds
-            float* G = S.big.G;
-            for (int i = t; i < L.total; i += MT) G[i] = 0.f;
-            lds_sync_m();
-            const int offW1 = m == 0 ? L.off[PGM_P_CRITIC_W1] : L.off[PGM_P_ACTOR_W1];
-            const int offB1 = m == 0 ? L.off[PGM_P_CRITIC_B1] : L.off[PGM_P_ACTOR_B1];
-            const int offW2 = m == 0 ? L.off[PGM_P_CRITIC_W2] : L.off[PGM_P_ACTOR_W2];
-            const int offB2 = m == 0 ? L.off[PGM_P_CRITIC_B2] : L.off[PGM_P_ACTOR_B2];
-            const int offWh = m == 0 ? L.off[PGM_P_VALUE_W] : L.off[PGM_P_MEAN_W];
-            const int offBh = m == 0 ? L.off[PGM_P_VALUE_B] : L.off[PGM_P_MEAN_B];
-            for (int round = 0; round < NWT; ++round) {
-                if (sh == round) {
+            // ---- gradient images.  SPLIT: waves 1 / 3 store their partials into GA[0] / GA[1], then
+            // waves 0 / 2 add theirs; g = GA[0] + GA[1].  Joint: the sh=1 wave of tower m stores into
+            // GA[m], the sh=0 wave adds; g = GA[m].  Fixed order => deterministic sums.
+            for (int stage = 0; stage < 2; ++stage) {
+                const bool mine = SPLIT ? ((w & 1) != stage) : (sh != stage);
+                if (mine) {
+                    float* Gt = S.big.GA[SPLIT ? (w >> 1) : m];
+                    const bool add = stage == 1;
+                    auto acc = [&](int idx, float val) { Gt[idx] = add ? Gt[idx] + val : val; };
+                    // 16-register blocks: all reads of a block are issued before its writes, so the
+                    // read-modify-write pays one LDS latency per block, not one per element
+                    auto acc16 = [&](auto idx, const f32x16& val) {
+                        if (add) {
+                            float tmp[16];
+#pragma unroll
+                            for (int r = 0; r < 16; ++r) tmp[r] = Gt[idx(r)];
+#pragma unroll
+                            for (int r = 0; r < 16; ++r) Gt[idx(r)] = tmp[r] + val[r];
+                        } else {
+#pragma unroll
+                            for (int r = 0; r < 16; ++r) Gt[idx(r)] = val[r];
+                        }
+                    };
 #pragma unroll
                     for (int ib = 0; ib < 2; ++ib)
 #pragma unroll
                         for (int ob = 0; ob < 2; ++ob)
-#pragma unroll
-                            for (int r = 0; r < 16; ++r) {
-                                const int gi = offW2 + (ib * TS + rowof(r, h)) * H + ob * TS + c;
-                                G[gi] += gW2[ib][ob][r];
-                            }
+                            acc16([&](int r) { return oW2 + (ib * TS + rowof(r, h)) * SCR + ob * TS + c; }, gW2[ib][ob]);
+                    // rows k >= O of dW1 are exactly zero (A operand 0); they go to distinct W2 padding
+                    // slots (column H of row k), which are re-zeroed below
 #pragma unroll
                     for (int hb = 0; hb < 2; ++hb)
-#pragma unroll
-                        for (int r = 0; r < 16; ++r) {
+                        acc16([&](int r) {
                             const int k = rowof(r, h);
-                            if (k < O) G[offW1 + k * H + hb * TS + c] += gW1[hb][r];
-                        }
-                    if (h == 0) {
+                            return k < O ? k * H + hb * TS + c : oW2 + k * SCR + H;
+                        }, gW1[hb]);
+                    if (h == 0) {  // per-unit sums: b1, b2 and the head weights (2 x (2 + Q) values)
+                        constexpr int NU = 2 * (2 + Q);
+                        float val[NU], tmp[NU];
+                        int idx[NU];
 #pragma unroll
                         for (int i = 0; i < 2; ++i) {
-                            G[offB1 + i * TS + c] += gB1[i];
-                            G[offB2 + i * TS + c] += gB2[i];
+                            idx[i * (2 + Q)] = oB1 + i * TS + c;
+                            val[i * (2 + Q)] = gB1[i];
+                            idx[i * (2 + Q) + 1] = oB2 + i * TS + c;
+                            val[i * (2 + Q) + 1] = gB2[i];
 #pragma unroll
-                            for (int q = 0; q < Q; ++q)
-                                if (q < NQ) G[offWh + (i * TS + c) * NQ + q] += gWh[i][q];
+                            for (int q = 0; q < Q; ++q) {  // rows q >= NQ are padding (zeroed below)
+                                idx[i * (2 + Q) + 2 + q] = oWh + q * H + i * TS + c;
+                                val[i * (2 + Q) + 2 + q] = q < NQ ? gWh[i][q] : 0.f;
+                            }
+                        }
+                        if (add) {
+#pragma unroll
+                            for (int j = 0; j < NU; ++j) tmp[j] = Gt[idx[j]];
+#pragma unroll
+                            for (int j = 0; j < NU; ++j) Gt[idx[j]] = tmp[j] + val[j];
+                        } else {
+#pragma unroll
+                            for (int j = 0; j < NU; ++j) Gt[idx[j]] = val[j];
                         }
                     }
                     if (l == 0) {
 #pragma unroll
                         for (int q = 0; q < Q; ++q)
-                            if (q < NQ) G[offBh + q] += gBh[q];
-                        if (m == 1) {
+                            if (q < NQ) acc(oBh + q, gBh[q]);
+                        if (m == 1) {  // -entropy_coef * d(mean entropy)/d logstd enters once (ppo.py:98)
+                            const float ec = add ? 0.f : a.hp.entropy_coef;
 #pragma unroll
-                            for (int q = 0; q < A; ++q)
-                                G[L.off[PGM_P_LOGSTD] + q] += gLs[q] - (round == 0 ? a.hp.entropy_coef : 0.f);
+                            for (int q = 0; q < A; ++q) acc(oLs + q, gLs[q] - ec);
                         }
                         S.red[8 + w] = lsum;
+                    }
+                    if (!add) {  // padding slots of a freshly written image
+                        Gt[oW2 + l * SCR + H] = 0.f;
+                        for (int q = NQ; q < Q; ++q) Gt[oWh + q * H + l] = 0.f;
+                        if (l >= NQ && l < Q) Gt[oBh + l] = 0.f;
+                        if (m == 0 && l < A) Gt[oLs + l] = 0.f;
                     }
                 }
                 lds_sync_m();
             }
             PGM_STAMP(2);
-            // ---- clip_grad_norm_ over every parameter (G holds zeros outside this workgroup's tensors)
+            // ---- clip_grad_norm_ over every parameter (padding slots hold zeros)
+            constexpr int NG = SPLIT ? IMG : 2 * IMG;
+            const float* GA0 = S.big.GA[0];
+            const float* GA1 = S.big.GA[1];
+            auto gval = [&](int i) { return SPLIT ? GA0[i] + GA1[i] : GA0[i]; };  // joint: GA[0..1] contiguous
             float sq = 0.f;
-            for (int i = t; i < L.total; i += MT) sq = fmaf(G[i], G[i], sq);
+            for (int i = t; i < NG; i += MT) {
+                const float g = gval(i);
+                sq = fmaf(g, g, sq);
+            }
             sq = wave_sum64(sq);
             if (l == 0) S.red[w] = sq;
             lds_sync_m();
+            PGM_STAMP(8);
             float total = (S.red[0] + S.red[1]) + (S.red[2] + S.red[3]);
             if constexpr (SPLIT) {  // tagged 8-byte granule hand-off with the other tower's workgroup
                 if (t == 0) {
@@ -486,7 +623,7 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                     for (unsigned spins = 0; !failed; ++spins) {
                         x = __hip_atomic_load(ws + (1 - m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         if ((unsigned)(x >> 32) == tag) break;
-                        if (spins > (1u << 26)) {  // partner never arrived: flag it, continue unclipped-safe
+                        if (spins > (1u << 26)) {  // partner never arrived: flag the launch as failed
                             __hip_atomic_store(a.ws + 2 * a.P, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                             x = 0;
                             break;
@@ -499,6 +636,7 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                 lds_sync_m();
                 total = S.red[4];
             }
+            PGM_STAMP(9);
             const float coef = fminf(a.hp.max_grad_norm / (sqrtf(total) + 1e-6f), 1.f);
             if (t == 0) {
                 if constexpr (SPLIT) {
@@ -511,49 +649,70 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                 }
                 st_e += ent;
             }
-            // ---- Adam (coalesced over the flat parameter vector; padding slots stay 0)
+            // ---- Adam, one flat pass over the images (padding: g = m = v = 0 keeps p = 0)
             ++nstep;
-            const int stepi = step0 + nstep;
-            const double bc1 = 1.0 - pow((double)b1c, (double)stepi);
-            const double bc2 = 1.0 - pow((double)b2c, (double)stepi);
+            b1p *= (double)b1c;  // beta^step, carried in fp64 (torch: 1 - beta ** step)
+            b2p *= (double)b2c;
+            const double bc1 = 1.0 - b1p;
+            const double bc2 = 1.0 - b2p;
             const float step_size = (float)(lr / bc1);
             const float bc2s = (float)sqrt(bc2);
-            // flat coalesced pass over this workgroup's parameter ranges (padding slots: g = m = v = 0
-            // keeps p = 0); new values land in G.  Critic tensors are [off(critic_w1), off(mean_w)),
-            // the actor owns the rest (layout order: actor tower, critic tower, value head, mean head, logstd).
-            const int cb = L.off[PGM_P_CRITIC_W1], ce = L.off[PGM_P_MEAN_W];
-            for (int rg = 0; rg < 2; ++rg) {
-                int lo = 0, hi = L.total;
-                if constexpr (SPLIT) {
-                    if (m == 0) { lo = rg == 0 ? cb : 0; hi = rg == 0 ? ce : 0; }
-                    else { lo = rg == 0 ? 0 : ce; hi = rg == 0 ? cb : L.total; }
-                } else if (rg == 1) {
-                    hi = 0;
+            if constexpr (SPLIT) {
+                // batches of 4 elements per thread: every LDS read of a batch before any write
+                for (int i0 = t; i0 < IMG; i0 += 4 * MT) {
+                    float g[4], mm[4], vv[4], pp[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int i = min(i0 + j * MT, IMG - 1);
+                        g[j] = gval(i);
+                        mm[j] = S.MV[i];
+                        vv[j] = S.MV[IMG + i];
+                        pp[j] = Pf[i];
+                    }
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const float gc = g[j] * coef;
+                        mm[j] = mm[j] + (1.f - b1c) * (gc - mm[j]);
+                        vv[j] = vv[j] * b2c + (1.f - b2c) * (gc * gc);
+                        pp[j] -= step_size * (mm[j] / (sqrtf(vv[j]) / bc2s + eps));
+                    }
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int i = i0 + j * MT;
+                        if (i < IMG) {
+                            S.MV[i] = mm[j];
+                            S.MV[IMG + i] = vv[j];
+                            Pf[i] = pp[j];
+                        }
+                    }
                 }
-#pragma unroll 4
-                for (int i = lo + t; i < hi; i += MT) {
-                    const float g = G[i] * coef;
-                    float mm = Mo[i], vv = Vo[i];
+            } else {  // moments in HBM (flat layout)
+                for (int i = t; i < NG; i += MT) {
+                    const int mi = i / IMG, f = img_to_flat<O, A, K>(i - mi * IMG, mi, L);
+                    if (f < 0) continue;
+                    const float g = gval(i) * coef;
+                    float mm = Mo[f], vv = Vo[f];
                     mm = mm + (1.f - b1c) * (g - mm);
                     vv = vv * b2c + (1.f - b2c) * (g * g);
-                    const float pn = P[i] - step_size * (mm / (sqrtf(vv) / bc2s + eps));
-                    Mo[i] = mm;
-                    Vo[i] = vv;
-                    P[i] = pn;
-                    G[i] = pn;
+                    Mo[f] = mm;
+                    Vo[f] = vv;
+                    Pf[i] -= step_size * (mm / (sqrtf(vv) / bc2s + eps));
                 }
             }
-            lds_sync_m();
-            for_each_tensor(S, [&](int tsr, int n, auto slot) {  // refresh the LDS working copy from G
-                const bool mine = !SPLIT || ((tsr >= PGM_P_CRITIC_W1 && tsr < PGM_P_MEAN_W) == (m == 0));
-                if (!mine) return;
-                const int off = L.off[tsr];
-                for (int j = t; j < n; j += MT) *slot(j) = G[off + j];
-            });
-            lds_sync_m();
+            lds_sync_m();  // parameters updated before the next minibatch; GA region reused as scr
             PGM_STAMP(3);
         }  // minibatches
     }      // epochs
+    // ---- write back (parameters; SPLIT also the moments)
+    for (int i = t; i < NT * IMG; i += MT) {
+        const int mi = i / IMG, f = img_to_flat<O, A, K>(i - mi * IMG, img_tower(mi), L);
+        if (f < 0) continue;
+        P[f] = Pf[i];
+        if constexpr (SPLIT) {
+            Mo[f] = S.MV[i];
+            Vo[f] = S.MV[IMG + i];
+        }
+    }
     if (t == 0) {
         const float n = (float)(E * M);
         if (!SPLIT || m == 0) a.stats[p * 3 + 0] = st_v / n;
@@ -576,45 +735,59 @@ static int device_cus() {
     return cus;
 }
 
-template <int O, int A, int K>
-int launch_ppo_update_mfma(const pgm_dims* d, const MArgs& a, hipStream_t stream) {
-    const size_t smem = sizeof(MSmem<O, A, K>);
+template <int O, int A, int K, bool SPLIT>
+int launch_mode(const pgm_dims* d, const MArgs& a, hipStream_t stream) {
+    const size_t smem = sizeof(MSmem<O, A, K, SPLIT>);
     if (smem > 160 * 1024) {
         set_error("pgm_ppo_update: LDS image %zu bytes exceeds 160 KiB", smem);
         return PGM_E_UNSUPPORTED;
     }
-    if ((size_t)a.L.total > big_floats<O, A, K>()) {
-        set_error("pgm_ppo_update: %d parameters exceed the LDS gradient image", a.L.total);
-        return PGM_E_UNSUPPORTED;
-    }
-    // the split needs both workgroups of a task resident at once: one workgroup per CU (LDS + 512
-    // registers per lane), so 2P must not exceed the CU count; otherwise run one workgroup per task
-    const char* sel = getenv("PGM_UPDATE_SPLIT");
-    const bool split = a.ws && 2 * d->P <= device_cus() && !(sel && sel[0] == '0');
-    auto kern = split ? ppo_update_mfma_kernel<O, A, K, true> : ppo_update_mfma_kernel<O, A, K, false>;
+    auto kern = ppo_update_mfma_kernel<O, A, K, SPLIT>;
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update");
-    if (split) {
-        e = hipMemsetAsync(a.ws, 0, ppo_workspace_bytes(d->P), stream);
+    if (SPLIT) {
+        e = hipMemsetAsync(a.ws, 0, ppo_flag_bytes(d->P), stream);
         if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update (workspace reset)");
     }
-    hipLaunchKernelGGL(kern, dim3(split ? 2 * d->P : d->P), dim3(MT), smem, stream, a);
+    hipLaunchKernelGGL(kern, dim3(SPLIT ? 2 * d->P : d->P), dim3(MT), smem, stream, a);
     return launch_status("pgm_ppo_update");
+}
+
+template <int O, int A, int K>
+int launch_ppo_update_mfma(const pgm_dims* d, const MArgs& a, const pgm_rollout_buf* rb, hipStream_t stream) {
+    // packed sample table, then the update
+    constexpr int RS = row_stride<O, A, K>();
+    PackArgs pa{d->P, d->N, d->T, rb->obs, rb->actions, rb->logp, rb->adv, rb->values, rb->returns,
+                const_cast<float*>(a.rows)};
+    const long long n4 = (long long)d->P * d->T * d->N * (RS / 4);
+    auto pack = pack_rows_kernel<O, A, K>;
+    hipLaunchKernelGGL(pack, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, stream, pa);
+    if (int rc = launch_status("pgm_ppo_update (pack rows)")) return rc;
+    // the split needs both workgroups of a task resident at once: one workgroup per CU (LDS > 80 KiB,
+    // 512 registers per lane), so 2P must not exceed the CU count; otherwise one workgroup per task
+    static_assert(sizeof(MSmem<O, A, K, true>) > 80 * 1024, "split residency argument needs > 80 KiB LDS");
+    const char* sel = getenv("PGM_UPDATE_SPLIT");
+    const bool split = 2 * d->P <= device_cus() && !(sel && sel[0] == '0');
+    return split ? launch_mode<O, A, K, true>(d, a, stream) : launch_mode<O, A, K, false>(d, a, stream);
 }
 
 int ppo_update_mfma(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params, float* adam_m, float* adam_v,
                     int32_t* adam_step, const float* lr, const int32_t* perms, const pgm_rollout_buf* rb, float* stats,
                     void* workspace, hipStream_t stream) {
+    if (!workspace) {
+        set_error("pgm_ppo_update: the MFMA update needs the workspace (pgm_ppo_update_workspace_bytes)");
+        return PGM_E_INVALID_ARG;
+    }
+    char* ws = (char*)workspace;
     MArgs a{d->N, d->T, make_layout(d->O, d->A, d->K, d->H), *hp, params, adam_m, adam_v, adam_step, lr, perms,
-            rb->obs, rb->actions, rb->logp, rb->values, rb->returns, rb->adv, stats,
-            (unsigned long long*)workspace, d->P};
+            (const float*)(ws + ppo_flag_bytes(d->P)), stats, (unsigned long long*)ws, d->P};
     return dispatch_dims(d->O, d->A, d->K, "pgm_ppo_update", [&](auto o, auto aa, auto k) -> int {
         constexpr int O = decltype(o)::value, A = decltype(aa)::value, K = decltype(k)::value;
         if constexpr (O > 32) {
             set_error("pgm_ppo_update: obs_dim %d > 32 not supported by the MFMA update kernel", O);
             return PGM_E_UNSUPPORTED;
         } else {
-            return launch_ppo_update_mfma<O, A, K>(d, a, stream);
+            return launch_ppo_update_mfma<O, A, K>(d, a, rb, stream);
         }
     });
 }

@@ -513,7 +513,7 @@ int ppo_update_mfma(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params,
 
 using namespace pgm;
 
-extern "C" size_t pgm_ppo_update_workspace_bytes(const pgm_dims* d) { return d ? ppo_workspace_bytes(d->P) : 0; }
+extern "C" size_t pgm_ppo_update_workspace_bytes(const pgm_dims* d) { return d ? ppo_workspace_bytes(d) : 0; }
 
 extern "C" int pgm_ppo_update(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params, float* adam_m,
                               float* adam_v, int32_t* adam_step, const float* lr, const int32_t* perms,

@@ -19,13 +19,19 @@ for p in range(P):
 tb.env_reset()
 L = _lib.lib()
 buf = (C.c_ulonglong * 64)()
+SB = int(os.environ.get('STAMP_BLOCK', 0))  # workgroup sampled (update SPLIT: 2p = critic, 2p+1 = actor)
 for name in ('rollout', 'update', 'mfma'):
     getattr(L, f'pgm_debug_stamps_{name}')(buf, 1)
+    getattr(L, f'pgm_debug_stamp_block_{name}')(SB)
 tb.iteration(0, 3e-4)
 torch.cuda.synchronize()
 names = {0: "loop/top", 1: 'policy fwd', 2: 'store val + sample', 3: 'logp + dynamics', 4: 'vecnorm stats',
          5: 'vecnorm emit', 10: 'policy L2 (in fwd)'}
+mnames = {0: 'stage rows', 1: 'pass end sync', 2: 'grad image rounds', 3: 'Adam', 8: 'sumsq', 9: 'norm exchange',
+          4: 'tile: L1 + L2 fwd', 5: 'tile: heads + loss', 6: 'tile: gWh, dH2, gW2', 7: 'tile: dH1, gW1'}
 for name, steps in (('rollout', T), ('update', 320), ('mfma', 320)):
+    if name == 'mfma':
+        names = mnames
     getattr(L, f'pgm_debug_stamps_{name}')(buf, 1)
     v = np.array(list(buf), dtype=np.float64)
     tot = v.sum()

@@ -298,6 +298,14 @@ __device__ __forceinline__ void chan_merge(double& mean, double& var, double cou
 
 __device__ __forceinline__ double clipd(double x, double lo, double hi) { return fmin(fmax(x, lo), hi); }
 
+// fp64 tanh as expm1(2y) / (expm1(2y) + 2): a few ulp (the env state's precision is fp64, the
+// observation leaves as fp32), half the instructions of the double-double libm tanh.  |y| is clamped at
+// 20, where tanh is 1 to fp64 precision.
+__device__ __forceinline__ double tanh_d(double y) {
+    const double e = expm1(2.0 * fmin(fmax(y, -20.0), 20.0));
+    return e / (e + 2.0);
+}
+
 // s' = tanh(d*s + U a_c + c); objectives; time limit (E.ac filled, E.s current).  Two barriers.
 template <int O, int A, int K>
 __device__ void env_dynamics(EnvSmem<O, A, K>& E, const Spec<O, A, K>& sp, int N, int max_steps) {
@@ -307,7 +315,7 @@ __device__ void env_dynamics(EnvSmem<O, A, K>& E, const Spec<O, A, K>& sp, int N
         double ua = 0.0;
 #pragma unroll
         for (int a = 0; a < A; ++a) ua += sp.U(o, a) * E.ac[n][a];
-        E.snew[n][o] = tanh(sp.d(o) * E.s[n][o] + ua + sp.c(o));
+        E.snew[n][o] = tanh_d(sp.d(o) * E.s[n][o] + ua + sp.c(o));
     }
     lds_sync();
     for (int i = t; i < N * K; i += RT) {
@@ -336,6 +344,10 @@ template <int O, int A, int K>
 __device__ void vecnorm_stats(EnvSmem<O, A, K>& E, const Spec<O, A, K>& sp, int N, const NormCfg& nc) {
     const int t = threadIdx.x;
     const double dn = (double)N;
+    // numpy's x.mean(0) / x.var(0) divide by N; for N a power of two the reciprocal is exact
+    const bool pow2 = (N & (N - 1)) == 0;
+    const double rn = 1.0 / dn;
+    auto divn = [&](double x) { return pow2 ? x * rn : x / dn; };
     for (int o = t; o < O; o += RT) {
         double sum = 0.0;
         for (int n = 0; n < N; ++n) {
@@ -345,13 +357,13 @@ __device__ void vecnorm_stats(EnvSmem<O, A, K>& E, const Spec<O, A, K>& sp, int 
             sum += v;
         }
         if (nc.use_ob) {
-            const double bm = sum / dn;
+            const double bm = divn(sum);
             double sq = 0.0;
             for (int n = 0; n < N; ++n) {
                 const double dd = E.snew[n][o] - bm;
                 sq += dd * dd;
             }
-            chan_merge(E.ob_mean[o], E.ob_var[o], E.ob_count, bm, sq / dn, dn);
+            chan_merge(E.ob_mean[o], E.ob_var[o], E.ob_count, bm, divn(sq), dn);
             E.ob_inv[o] = 1.0 / sqrt(E.ob_var[o] + nc.eps);
         }
     }
@@ -362,13 +374,13 @@ __device__ void vecnorm_stats(EnvSmem<O, A, K>& E, const Spec<O, A, K>& sp, int 
         if (nc.use_obj) {
             double sum = 0.0;
             for (int n = 0; n < N; ++n) sum += E.obj_acc[n][k];
-            const double bm = sum / dn;
+            const double bm = divn(sum);
             double sq = 0.0;
             for (int n = 0; n < N; ++n) {
                 const double dd = E.obj_acc[n][k] - bm;
                 sq += dd * dd;
             }
-            chan_merge(E.obj_mean[k], E.obj_var[k], E.obj_count, bm, sq / dn, dn);
+            chan_merge(E.obj_mean[k], E.obj_var[k], E.obj_count, bm, divn(sq), dn);
             E.obj_inv[k] = 1.0 / sqrt(E.obj_var[k] + nc.eps);
         }
     }
@@ -378,10 +390,10 @@ __device__ void vecnorm_stats(EnvSmem<O, A, K>& E, const Spec<O, A, K>& sp, int 
             E.ret[n] = E.ret[n] * nc.gamma + 0.0;
             sum += E.ret[n];
         }
-        const double bm = sum / dn;
+        const double bm = divn(sum);
         double sq = 0.0;
         for (int n = 0; n < N; ++n) sq += (E.ret[n] - bm) * (E.ret[n] - bm);
-        chan_merge(E.ret_mean, E.ret_var, E.ret_count, bm, sq / dn, dn);
+        chan_merge(E.ret_mean, E.ret_var, E.ret_count, bm, divn(sq), dn);
         E.ret_count += dn;
     }
     lds_sync();

@@ -63,8 +63,11 @@ __device__ __forceinline__ void lds_sync_m() { asm volatile("s_waitcnt lgkmcnt(0
 __device__ __forceinline__ void dma_sync_m() {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
-__device__ __forceinline__ float xhalf(float v) {  // value of lane l ^ 32
-    return __shfl_xor(v, 32, 64);
+// v[l] + v[l ^ 32] in every lane: one v_permlane32_swap (VALU, no LDS round trip); the sum is
+// commutative, so both halves get bit-identical results
+__device__ __forceinline__ float half_sum(float v) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
 // ---------------------------------------------------------------- packed sample table
@@ -148,9 +151,11 @@ struct MSmemT {
     static constexpr int SBk = RS <= 32 ? 128 : 64;  // samples staged per pass
     TowerImg<O, A, K> Pm[NT];              // parameters
     float MV[SPLIT ? 2 * IMG : 1];         // SPLIT: Adam exp_avg | exp_avg_sq images (else in HBM)
-    alignas(16) float RB[NBUF][SBk * RS];  // packed rows of the current / next pass (swizzled chunks)
+    static constexpr int RSL = RS + 4;     // LDS row stride: 2-way bank conflicts on per-sample column reads
+    alignas(16) float RB[NBUF][SBk * RSL]; // packed rows of the current / next pass
     int32_t IB[2][SBk];                    // sample indices of the next two passes
     float dout[4][TS][Q];                  // per-wave dL/d(head output) of the current tile
+    float aiv[A];                          // actor 1 / std^2 = exp(-2 logstd), refreshed by Adam
     float red[16];
     union Big {                            // transpose tiles during the passes, gradient images after
         float scr[4][TS][SCR];
@@ -189,10 +194,10 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
     constexpr int KS1 = (O + 1) / 2;  // k-steps of layer 1
     constexpr int IMG = Sm::IMG, NT = Sm::NT, SBk = Sm::SBk, RS = Sm::RS;
     constexpr int NBUF = nbuf<O, A, K, SPLIT>();
-    constexpr int CR = RS / 4;           // 16-B chunks per row
-    constexpr int RPI = 64 / CR;         // rows per LDS-DMA wave instruction
-    constexpr int NDMA = SBk / RPI / 4;  // LDS-DMA instructions per wave per pass
-    static_assert(NDMA >= 1 && NDMA * RPI * 4 == SBk, "staging split");
+    constexpr int RSL = Sm::RSL;
+    constexpr int CR = RS / 4;                         // 16-B chunks per packed row
+    constexpr int NDT = (SBk * RSL) / 256;             // LDS-DMA wave instructions per pass (1 KiB each)
+    static_assert(NDT * 256 == SBk * RSL, "staging split");
     constexpr int oW2 = O * H, oWh = oW2 + H * SCR, oB1 = oWh + Q * H, oB2 = oB1 + H, oBh = oB2 + H, oLs = oBh + Q;
     constexpr int NWT = SPLIT ? 4 : 2;  // waves per tower
     const int t = threadIdx.x, w = t >> 6, l = t & 63, h = l >> 5, c = l & 31;
@@ -215,7 +220,9 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
 
     // ---- staging: pass gp = ((e * nb) + bb) * npm + j covers minibatch rows [j*SBk, j*SBk + ns).
     // The pass's permutation indices go first into IB (4-B LDS-DMA, one pass earlier than the rows).
-    // Row DMA: lane l of wave w, instruction d: row (w*NDMA + d)*RPI + l/CR, 16-B chunk l%CR.
+    // Row DMA: instruction d (waves take d = w, w+4, ...) fills LDS floats [256 d, 256 d + 256); lane l's
+    // 16 B land at float 256 d + 4 l = row * RSL + 4 chunk.  The pad chunk of a row (chunk == CR)
+    // re-reads the row's first chunk.
     auto issue_idx = [&](int g, int buf) {
         const int e = g / (nb * npm), rem = g - e * nb * npm, bb = rem / npm, j = rem - bb * npm;
         const int ns = min(SBk, mb - j * SBk);
@@ -226,20 +233,29 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
     };
     auto issue_rows = [&](int buf, int ibuf) {
         float* base = &S.RB[buf][0];
+        constexpr int NI = (NDT + 3) / 4;  // instructions per wave (the last round is partial)
+        int idx[NI];
 #pragma unroll
-        for (int d = 0; d < NDMA; ++d) {
-            const int row = (w * NDMA + d) * RPI + l / CR;
-            const float* src = rows + (size_t)S.IB[ibuf][row] * RS + (l % CR) * 4;
-            float* dst = base + (w * NDMA + d) * RPI * RS;  // wave-uniform
-            __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_t*)dst, 16, 0, 0);
+        for (int i = 0; i < NI; ++i) {  // all index reads first: one LDS latency for the batch
+            const int d = w + 4 * i, pos = d * 256 + 4 * l, row = min(pos / RSL, SBk - 1);
+            idx[i] = S.IB[ibuf][row];
+        }
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int d = w + 4 * i;
+            if (d < NDT) {
+                const int pos = d * 256 + 4 * l, row = pos / RSL, chunk = (pos - row * RSL) >> 2;
+                const float* src = rows + (size_t)idx[i] * RS + (chunk < CR ? chunk : 0) * 4;
+                __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_t*)(base + d * 256), 16, 0, 0);
+            }
         }
     };
-    // element k of row cs of a tile starting at rt (plain row-major: one address register per lane;
-    // the per-sample column reads of a tile are 16-way bank conflicted, ~25 reads per tile)
-    auto rowf = [&](const float* rt, int cs, int k) { return rt[cs * RS + k]; };
+    // element k of row cs of a tile starting at rt
+    auto rowf = [&](const float* rt, int cs, int k) { return rt[cs * RSL + k]; };
 
     // ---- parameter (and SPLIT: Adam moment) images from the flat HBM vectors
     float* Pf = &S.Pm[0].W1t[0][0];
+    if (t < A) S.aiv[t] = expf(-2.f * P[L.off[PGM_P_LOGSTD] + t]);
     for (int i = t; i < NT * IMG; i += MT) {
         const int mi = i / IMG, f = img_to_flat<O, A, K>(i - mi * IMG, img_tower(mi), L);
         Pf[i] = f >= 0 ? P[f] : 0.f;
@@ -298,7 +314,7 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
 
                 for (int tile = sh; tile * TS < ns; tile += NWT) {
                     const int ts0 = tile * TS;
-                    const float* rt = rb + ts0 * RS;  // this tile's staged rows
+                    const float* rt = rb + ts0 * RSL;  // this tile's staged rows
                     // ---- layer 1: Z1[s][h] = X[s][:] . W1t[:][h]  (two independent accumulator chains
                     // interleaved: the 32x32x2 f32 MFMA has a 64-cycle dependent-accumulator latency)
                     f32x16 z[2] = {f32x16{0}, f32x16{0}};
@@ -354,7 +370,7 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                         for (int q = 0; q < Q; ++q) outv[q] = fmaf(hv, W.Wh[q][h * TS + u], outv[q]);
                     }
 #pragma unroll
-                    for (int q = 0; q < Q; ++q) outv[q] += xhalf(outv[q]) + W.bh[q];
+                    for (int q = 0; q < Q; ++q) outv[q] = half_sum(outv[q]) + W.bh[q];
                     // ---- per-sample loss gradients (ppo.py:80-96); both halves compute the same sample
                     const int si = ts0 + c;
                     const bool ok = si < ns;
@@ -386,8 +402,8 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                         float lp = 0.f;
 #pragma unroll
                         for (int q = 0; q < A; ++q) {
-                            const float dz = (rowf(rt, c, O + q) - outv[q]) / expf(lstd[q]);
-                            lp += -0.5f * dz * dz - lstd[q] - LOG_SQRT_2PI;
+                            const float diff = rowf(rt, c, O + q) - outv[q];
+                            lp += -0.5f * diff * diff * S.aiv[q] - lstd[q] - LOG_SQRT_2PI;
                         }
                         const float ratio = expf(lp - rowf(rt, c, O + A));
                         const float ad = rowf(rt, c, O + A + 1);
@@ -399,9 +415,8 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                         if (ok && h == 0) lsum += -fminf(s1, s2);
 #pragma unroll
                         for (int q = 0; q < A; ++q) {
-                            const float sd = expf(lstd[q]);
                             const float diff = rowf(rt, c, O + q) - outv[q];
-                            const float iv = 1.f / (sd * sd);
+                            const float iv = S.aiv[q];
                             dO[q] = dlp * diff * iv;
                             if (h == 0) gLs[q] += dlp * (diff * diff * iv - 1.f);
                         }
@@ -498,10 +513,10 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
             // ---- combine the lane halves of the per-column partial sums
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                gB1[i] += xhalf(gB1[i]);
-                gB2[i] += xhalf(gB2[i]);
+                gB1[i] = half_sum(gB1[i]);
+                gB2[i] = half_sum(gB2[i]);
 #pragma unroll
-                for (int q = 0; q < Q; ++q) gWh[i][q] += xhalf(gWh[i][q]);
+                for (int q = 0; q < Q; ++q) gWh[i][q] = half_sum(gWh[i][q]);
             }
             // per-sample partials (held by half 0 lanes): 64-lane sums (half 1 holds zeros)
 #pragma unroll
@@ -657,6 +672,7 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
             const double bc2 = 1.0 - b2p;
             const float step_size = (float)(lr / bc1);
             const float bc2s = (float)sqrt(bc2);
+            const float inv_bc2s = 1.f / bc2s;
             if constexpr (SPLIT) {
                 // batches of 4 elements per thread: every LDS read of a batch before any write
                 for (int i0 = t; i0 < IMG; i0 += 4 * MT) {
@@ -674,7 +690,10 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                         const float gc = g[j] * coef;
                         mm[j] = mm[j] + (1.f - b1c) * (gc - mm[j]);
                         vv[j] = vv[j] * b2c + (1.f - b2c) * (gc * gc);
-                        pp[j] -= step_size * (mm[j] / (sqrtf(vv[j]) / bc2s + eps));
+                        // torch: p -= step_size * m / (sqrt(v) / sqrt(bc2) + eps); hardware sqrt / rcp
+                        // (<= 2 ulp on the step, against an fp64 reference anyway)
+                        const float den = __builtin_amdgcn_sqrtf(vv[j]) * inv_bc2s + eps;
+                        pp[j] -= step_size * mm[j] * __builtin_amdgcn_rcpf(den);
                     }
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
@@ -683,6 +702,7 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                             S.MV[i] = mm[j];
                             S.MV[IMG + i] = vv[j];
                             Pf[i] = pp[j];
+                            if (m == 1 && i >= oLs && i < oLs + A) S.aiv[i - oLs] = expf(-2.f * pp[j]);
                         }
                     }
                 }
@@ -696,7 +716,9 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                     vv = vv * b2c + (1.f - b2c) * (g * g);
                     Mo[f] = mm;
                     Vo[f] = vv;
-                    Pf[i] -= step_size * (mm / (sqrtf(vv) / bc2s + eps));
+                    const float pn = Pf[i] - step_size * (mm / (sqrtf(vv) / bc2s + eps));
+                    Pf[i] = pn;
+                    if (i >= IMG + oLs && i < IMG + oLs + A) S.aiv[i - IMG - oLs] = expf(-2.f * pn);
                 }
             }
             lds_sync_m();  // parameters updated before the next minibatch; GA region reused as scr

@@ -43,6 +43,16 @@ class MOPGPopulation:
         self.rng = rng
         self.tb = None
 
+    @property
+    def layout(self):
+        """The flat parameter layout of this run's env dims (pgm_param_layout)."""
+        from .envspec import make_spec
+        from .layout import ParamLayout
+        if self.tb is not None:
+            return self.tb.layout
+        spec = make_spec(self.args.env_name)
+        return ParamLayout(spec['obs_dim'], spec['act_dim'], spec['obj_num'])
+
     def _batch(self, P):
         a = self.args
         if self.tb is None or self.tb.P != P:

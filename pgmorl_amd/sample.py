@@ -112,6 +112,20 @@ class Sample:
         return cls(env_params, PolicyHandle(snap), AgentHandle(snap), objs, optgraph_id)
 
     @classmethod
+    def from_reference(cls, ref_sample, layout, device='cuda'):
+        """Adopt a reference Sample (morl/sample.py: actor_critic module, agent with a torch Adam,
+        env_params dict) as a device-resident one: parameters and Adam state move to HBM in the
+        flat layout, env_params / objs / optgraph_id are kept."""
+        sd = ref_sample.actor_critic.state_dict()
+        opt = ref_sample.agent.optimizer.state_dict().get('state', {})
+        m, v, step = layout.adam_from_optimizer_state(opt)
+        dev = torch.device(device)
+        snap = DeviceSnapshot(layout, torch.from_numpy(layout.flatten(sd)).to(dev), torch.from_numpy(m).to(dev),
+                              torch.from_numpy(v).to(dev), step)
+        return cls.from_snapshot(snap, copy.deepcopy(ref_sample.env_params), copy.deepcopy(ref_sample.objs),
+                                 ref_sample.optgraph_id)
+
+    @classmethod
     def copy_from(cls, sample):
         snap = sample.snapshot.clone()
         return cls.from_snapshot(snap, copy.deepcopy(sample.env_params), copy.deepcopy(sample.objs),

@@ -82,6 +82,25 @@ __device__ __forceinline__ float wave_sum64(float v) {
     return (r0 + r1) + (r2 + r3);
 }
 
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), lane),
+                            __builtin_amdgcn_readlane(__double2loint(v), lane));
+}
+// fp64 64-lane sum, same reduction tree as wave_sum64 (deterministic)
+__device__ __forceinline__ double wave_sum64_d(double v) {
+    v += dpp_d<0x128>(v);
+    v += dpp_d<0x124>(v);
+    v += dpp_d<0x122>(v);
+    v += dpp_d<0x121>(v);
+    return (readlane_d(v, 0) + readlane_d(v, 16)) + (readlane_d(v, 32) + readlane_d(v, 48));
+}
+
 // ---------------------------------------------------------------- counter RNG (perf mode)
 __host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     x += 0x9E3779B97F4A7C15ull;

@@ -237,8 +237,10 @@ def _oracle_rollout(pol, envs, ro, noise):
         ro.value_preds[-1] = pol.get_value(ro.obs[-1])
 
 
-@pytest.mark.parametrize('env,N,T', [('MO-Hopper-v2', 4, 48), ('MO-Walker2d-v2', 2, 520)])
-def test_rollout(gpu, env, N, T):
+@pytest.mark.parametrize('kernel', ['wave', 'block'])
+@pytest.mark.parametrize('env,N,T', [('MO-Hopper-v2', 4, 48), ('MO-Walker2d-v2', 2, 520), ('MO-Hopper-v3', 6, 40)])
+def test_rollout(gpu, env, N, T, kernel, monkeypatch):
+    monkeypatch.setenv('PGM_ROLLOUT_KERNEL', kernel)  # wave: one wave per env (default); block: workgroup step
     P = 2
     spec, tb, pols = _batch_with_policies(env, P, N, T, seed=3, scale=0.05)
     s0 = envspec.reset_table(spec['obs_dim'], 0, N)

@@ -82,6 +82,42 @@ __device__ __forceinline__ float wave_sum64(float v) {
     return (r0 + r1) + (r2 + r3);
 }
 
+// M <= 8 simultaneous 64-lane sums, results wave-uniform.  Transposing reduction: v_permlane32_swap folds
+// lane halves of PAIRS of values (value a in lanes 0-31, b in 32-63 of one register), v_permlane16_swap
+// folds rows of pairs of those (4 values, one per 16-lane row), then 4 DPP row rotations finish each
+// row and one readlane per value makes it uniform: ~3.5 instructions per value instead of ~12.
+__device__ __forceinline__ float pl32_fold(float a, float b) {  // lanes 0-31: a_lo + a_hi, 32-63: b_lo + b_hi
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float pl16_fold(float a, float b) {  // rows (0,1,2,3) <- a r0+r1, b r0+r1, a r2+r3, b r2+r3
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float row_sum16(float v) {
+    v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x128, 0xf, 0xf, false));  // row_ror:8
+    v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x124, 0xf, 0xf, false));  // row_ror:4
+    v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x122, 0xf, 0xf, false));  // row_ror:2
+    v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x121, 0xf, 0xf, false));  // row_ror:1
+    return v;
+}
+template <int M>
+__device__ __forceinline__ void wave_sum64_multi(const float (&v)[M], float (&out)[M]) {
+    static_assert(M >= 1 && M <= 8, "1..8 values");
+    auto at = [&](int i) { return i < M ? v[i] : 0.f; };
+    // level 1: pairs (0,1) (2,3) (4,5) (6,7); level 2: (s01, s23) -> rows [v0, v2, v1, v3], (s45, s67) likewise
+    const float r0 = row_sum16(pl16_fold(pl32_fold(at(0), at(1)), pl32_fold(at(2), at(3))));
+    const int lane_of[4] = {0, 32, 16, 48};  // value i of a group sits in row {0, 2, 1, 3}[i]
+#pragma unroll
+    for (int i = 0; i < (M < 4 ? M : 4); ++i)
+        out[i] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r0), lane_of[i]));
+    if constexpr (M > 4) {
+        const float r1 = row_sum16(pl16_fold(pl32_fold(at(4), at(5)), pl32_fold(at(6), at(7))));
+#pragma unroll
+        for (int i = 4; i < M; ++i) out[i] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r1), lane_of[i - 4]));
+    }
+}
+
 template <int CTRL>
 __device__ __forceinline__ double dpp_d(double v) {
     const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xf, 0xf, false);
@@ -119,8 +155,8 @@ __device__ __forceinline__ float counter_normal(uint64_t seed, uint64_t i) {
 }  // namespace pgm
 
 // ---------------------------------------------------------------- diagnostic phase stamps
-// Built only into libpgm_stamps.so (-DPGM_STAMPS): workgroup 0 / thread 0 accumulates s_memtime
-// deltas per phase id into pgm_stamp_acc; read back with pgm_debug_stamps().  Never in the shipped .so.
+// Built only into libpgm_stamps.so (-DPGM_STAMPS): every wave accumulates s_memtime deltas per phase id
+// (< 16); thread 0 of the sampled workgroup adds its totals to pgm_stamp_acc at the end; read back with pgm_debug_stamps().  Never in the shipped .so.
 #ifdef PGM_STAMPS
 // one accumulator array + reader per translation unit (no relocatable device code)
 #define PGM_STAMP_UNIT(name)                                                                          \
@@ -139,19 +175,30 @@ __device__ __forceinline__ float counter_normal(uint64_t seed, uint64_t i) {
         }                                                                                             \
         return PGM_OK;                                                                                \
     }
-#define PGM_STAMP_DECL unsigned long long pgm_stamp_last = __builtin_amdgcn_s_memtime();
+// deltas accumulate in registers (no memory traffic inside the measured loop: a global access there would
+// add vmcnt waits that drain the kernel's own stores); PGM_STAMP_FLUSH at the kernel's end publishes them
+#define PGM_STAMP_DECL                                                           \
+    unsigned long long pgm_stamp_last = __builtin_amdgcn_s_memtime();            \
+    unsigned long long pgm_stamp_reg[16] = {0};
 #define PGM_STAMP(id)                                                            \
     do {                                                                         \
-        if ((int)blockIdx.x == pgm_stamp_block && threadIdx.x == 0) {                               \
-            unsigned long long now_ = __builtin_amdgcn_s_memtime();              \
-            atomicAdd(&pgm_stamp_acc[id], now_ - pgm_stamp_last);              \
-            pgm_stamp_last = now_;                                               \
-        }                                                                        \
+        const unsigned long long now_ = __builtin_amdgcn_s_memtime();            \
+        pgm_stamp_reg[id] += now_ - pgm_stamp_last;                              \
+        pgm_stamp_last = now_;                                                   \
+    } while (0)
+#define PGM_STAMP_FLUSH                                                          \
+    do {                                                                         \
+        if ((int)blockIdx.x == pgm_stamp_block && threadIdx.x == 0)              \
+            for (int i_ = 0; i_ < 16; ++i_)                                      \
+                if (pgm_stamp_reg[i_]) atomicAdd(&pgm_stamp_acc[i_], pgm_stamp_reg[i_]); \
     } while (0)
 #else
 #define PGM_STAMP_UNIT(name)
 #define PGM_STAMP_DECL
 #define PGM_STAMP(id) \
     do {              \
+    } while (0)
+#define PGM_STAMP_FLUSH \
+    do {                \
     } while (0)
 #endif

@@ -17,24 +17,18 @@
 #include <stdlib.h>
 
 #include "pgm_dispatch.hpp"
+#include "pgm_rollout.hpp"
 
 PGM_STAMP_UNIT(rollout)
 
 namespace pgm {
 
-constexpr int NMAX = 8;    // envs per task handled by one workgroup
-constexpr int RT = 256;    // threads per workgroup
 
-template <int O>
-constexpr int opad() { return (O + 3) & ~3; }
 template <int O>
 constexpr bool w1_in_lds() { return O <= 128; }
 template <int O>
 constexpr bool spec_in_lds() { return O <= 128; }
 
-// LDS-only barrier: waits for this wave's LDS traffic, not for its outstanding HBM stores
-// (__syncthreads() would also drain vmcnt, i.e. wait for every rollout-storage store).
-__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // ------------------------------------------------------------------------------------------
 // LDS images
@@ -74,13 +68,6 @@ struct EnvSmem {
     int obj_valid;
 };
 
-struct NormCfg {
-    double gamma, clipob, cliprew, eps;
-    int use_ob, use_obj;
-};
-__host__ __device__ inline NormCfg norm_cfg(const pgm_norm_state& ns) {
-    return NormCfg{ns.gamma, ns.clipob, ns.cliprew, ns.epsilon, ns.use_ob_rms, ns.use_obj_rms};
-}
 
 // env-constant accessors: LDS copy when it fits, HBM otherwise
 template <int O, int A, int K>
@@ -287,26 +274,8 @@ __device__ void store_env(const EnvSmem<O, A, K>& E, const pgm_env_state& st, co
     }
 }
 
-// Chan merge of a batch (bm, bv, n) into (mean, var, count) -- running_mean_std.py:20-31
-// (one fp64 division: the reference's three divisions by tot_count become a multiply by 1/tot)
-__device__ __forceinline__ void chan_merge(double& mean, double& var, double count, double bm, double bv, double n) {
-    const double delta = bm - mean;
-    const double inv_tot = 1.0 / (count + n);
-    const double new_mean = mean + delta * n * inv_tot;
-    const double m2 = var * count + bv * n + delta * delta * count * n * inv_tot;
-    mean = new_mean;
-    var = m2 * inv_tot;
-}
 
-__device__ __forceinline__ double clipd(double x, double lo, double hi) { return fmin(fmax(x, lo), hi); }
 
-// fp64 tanh as expm1(2y) / (expm1(2y) + 2): a few ulp (the env state's precision is fp64, the
-// observation leaves as fp32), half the instructions of the double-double libm tanh.  |y| is clamped at
-// 20, where tanh is 1 to fp64 precision.
-__device__ __forceinline__ double tanh_d(double y) {
-    const double e = expm1(2.0 * fmin(fmax(y, -20.0), 20.0));
-    return e / (e + 2.0);
-}
 
 // s' = tanh(d*s + U a_c + c); objectives; time limit (E.ac filled, E.s current).  Two barriers.
 template <int O, int A, int K>
@@ -569,18 +538,6 @@ __global__ __launch_bounds__(RT) void env_kernel(EnvArgs a) {
     store_env(E, a.st, a.ns, p, N);
 }
 
-struct RolloutArgs {
-    int P, N, T;
-    Layout L;
-    const float* params;
-    pgm_env_spec spec;
-    pgm_env_state st;
-    pgm_norm_state ns;
-    pgm_rollout_buf rb;
-    const float* noise;
-    uint64_t seed;
-    int carry;
-};
 
 template <int O, int A, int K>
 __global__ __launch_bounds__(RT) void rollout_kernel(RolloutArgs a) {
@@ -651,389 +608,8 @@ __global__ __launch_bounds__(RT) void rollout_kernel(RolloutArgs a) {
     for (int i = t; i < N * K; i += RT) val[(size_t)T * N * K + i] = P.val[i / K][i % K];
     __syncthreads();
     store_env(E, a.st, a.ns, p, N);
+    PGM_STAMP_FLUSH;
 }
-
-// ------------------------------------------------------------------------------------------
-// Rollout with ONE WAVE PER ENV (obs_dim <= 32, the default path).  Env n lives on wave n % 4: its
-// lanes hold unit l of both towers' weights, feature l of the env state / constants, and run the
-// policy forward, the Gaussian draw, the fp64 dynamics and the objective sums with wave-local
-// exchanges only.  Two workgroup barriers per step bracket the one cross-env step, the VecNormalize
-// running statistics (ob_rms on wave 0, obj_rms on wave 1, ret_rms on wave 2).  Same semantics and
-// buffers as rollout_kernel above (kept for obs_dim > 32).
-template <int O, int A, int K>
-struct WaveSmem {
-    alignas(16) float x[NMAX][opad<O>()];  // normalised fp32 obs row of env n (its wave writes / reads)
-    alignas(16) float h1[4][H2];           // per-wave layer-1 activations (critic | actor)
-    double snew[NMAX][O];                  // post-reset observation (statistics input)
-    double objacc[NMAX][K];                // VecNormalize.obj after this step's accumulation
-    double ret[NMAX];
-    double ob_mean[O], ob_var[O], ob_inv[O], obj_mean[K], obj_var[K], obj_inv[K];
-    double ob_count, obj_count, ret_mean, ret_var, ret_count;
-};
-
-template <int N_>
-__device__ __forceinline__ float sel_lane(const float (&v)[N_], int l) {
-    float r = 0.f;
-#pragma unroll
-    for (int q = 0; q < N_; ++q) r = l == q ? v[q] : r;
-    return r;
-}
-template <int N_>
-__device__ __forceinline__ double sel_lane_d(const double (&v)[N_], int l) {
-    double r = 0.0;
-#pragma unroll
-    for (int q = 0; q < N_; ++q) r = l == q ? v[q] : r;
-    return r;
-}
-
-template <int O, int A, int K>
-__global__ __launch_bounds__(RT) void rollout_wave_kernel(RolloutArgs a) {
-    static_assert(O <= 32, "wave-per-env rollout keeps W1 columns in registers");
-    constexpr int NE = NMAX / 4;  // env slots per wave
-    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-    auto& S = *reinterpret_cast<WaveSmem<O, A, K>*>(smem_raw);
-    const int p = blockIdx.x, t = threadIdx.x, w = t >> 6, l = t & 63, N = a.N, T = a.T;
-    const NormCfg nc = norm_cfg(a.ns);
-    const Layout& L = a.L;
-    const float* prm = a.params + (size_t)p * L.total;
-    float* obs = a.rb.obs + (size_t)p * (T + 1) * N * O;
-    float* act = a.rb.actions + (size_t)p * T * N * A;
-    float* logp = a.rb.logp + (size_t)p * T * N;
-    float* val = a.rb.values + (size_t)p * (T + 1) * N * K;
-    float* rew = a.rb.rewards + (size_t)p * T * N * K;
-    float* masks = a.rb.masks + (size_t)p * (T + 1) * N;
-    float* bad = a.rb.bad_masks + (size_t)p * (T + 1) * N;
-    const int maxs = a.spec.max_episode_steps;
-
-    // ---- per-lane weights: unit l of the critic and actor towers, head rows of unit l
-    float w1c[O], w1a[O], w2c[H], w2a[H], wv[K], wm[A], bv[K], bm[A];
-#pragma unroll
-    for (int k = 0; k < O; ++k) {
-        w1c[k] = prm[L.off[PGM_P_CRITIC_W1] + k * H + l];
-        w1a[k] = prm[L.off[PGM_P_ACTOR_W1] + k * H + l];
-    }
-#pragma unroll
-    for (int k = 0; k < H; ++k) {
-        w2c[k] = prm[L.off[PGM_P_CRITIC_W2] + k * H + l];
-        w2a[k] = prm[L.off[PGM_P_ACTOR_W2] + k * H + l];
-    }
-#pragma unroll
-    for (int q = 0; q < K; ++q) {
-        wv[q] = prm[L.off[PGM_P_VALUE_W] + l * K + q];
-        bv[q] = prm[L.off[PGM_P_VALUE_B] + q];
-    }
-#pragma unroll
-    for (int j = 0; j < A; ++j) {
-        wm[j] = prm[L.off[PGM_P_MEAN_W] + l * A + j];
-        bm[j] = prm[L.off[PGM_P_MEAN_B] + j];
-    }
-    const float b1c = prm[L.off[PGM_P_CRITIC_B1] + l], b1a = prm[L.off[PGM_P_ACTOR_B1] + l];
-    const float b2c = prm[L.off[PGM_P_CRITIC_B2] + l], b2a = prm[L.off[PGM_P_ACTOR_B2] + l];
-    const float ls = l < A ? prm[L.off[PGM_P_LOGSTD] + l] : 0.f;
-    const float sd = expf(ls);
-
-    // ---- per-lane env constants (feature o = l) and state of this wave's envs
-    const bool fl = l < O;
-    const int lo = fl ? l : 0;
-    double Uo[A], Vo[K];
-#pragma unroll
-    for (int j = 0; j < A; ++j) Uo[j] = a.spec.U[lo * A + j];
-#pragma unroll
-    for (int q = 0; q < K; ++q) Vo[q] = fl ? a.spec.V[q * O + lo] : 0.0;
-    const double d_o = a.spec.d[lo], c_o = a.spec.c[lo];
-    const double alo = l < A ? a.spec.act_lo[l] : 0.0, ahi = l < A ? a.spec.act_hi[l] : 0.0;
-    double ebase[K], ecoef[K];
-#pragma unroll
-    for (int q = 0; q < K; ++q) {
-        ebase[q] = a.spec.ebase[q];
-        ecoef[q] = a.spec.ecoef[q];
-    }
-    double s_o[NE], s0_o[NE], objacc[NE][K], ret[NE], objraw[NE][K];
-    int elapsed[NE], done[NE], badf[NE];
-#pragma unroll
-    for (int e = 0; e < NE; ++e) {
-        const int n = min(w + 4 * e, N - 1);
-        s_o[e] = a.st.s[((size_t)p * N + n) * O + lo];
-        s0_o[e] = a.st.s0[(size_t)n * O + lo];
-#pragma unroll
-        for (int q = 0; q < K; ++q) {
-            objacc[e][q] = a.st.obj_acc[((size_t)p * N + n) * K + q];
-            objraw[e][q] = 0.0;
-        }
-        ret[e] = a.st.ret[p * N + n];
-        elapsed[e] = a.st.elapsed[p * N + n];
-        done[e] = badf[e] = 0;
-    }
-    int obj_valid = a.st.obj_acc_valid[p];
-    // running statistics in LDS
-    for (int o = t; o < O; o += RT) {
-        S.ob_mean[o] = a.ns.ob_mean[(size_t)p * O + o];
-        S.ob_var[o] = a.ns.ob_var[(size_t)p * O + o];
-    }
-    if (t < K) {
-        S.obj_mean[t] = a.ns.obj_mean[p * K + t];
-        S.obj_var[t] = a.ns.obj_var[p * K + t];
-    }
-    if (t == 0) {
-        S.ob_count = a.ns.ob_count[p];
-        S.obj_count = a.ns.obj_count[p];
-        S.ret_mean = a.ns.ret_mean[p];
-        S.ret_var = a.ns.ret_var[p];
-        S.ret_count = a.ns.ret_count[p];
-    }
-    if (a.carry) {  // after_update(): slot T -> slot 0 (storage.py:71-75); each thread re-reads its own writes
-        for (int i = t; i < N * O; i += RT) obs[i] = obs[(size_t)T * N * O + i];
-        if (t < N) {
-            masks[t] = masks[(size_t)T * N + t];
-            bad[t] = bad[(size_t)T * N + t];
-        }
-    }
-    for (int i = t; i < N * O; i += RT) S.x[i / O][i % O] = obs[i];
-    __syncthreads();
-
-    // policy forward of env n on this wave: value[K], mean[A] (uniform across lanes)
-    auto forward = [&](int n, float (&v)[K], float (&mu)[A], bool heads_actor) {
-        float zc = b1c, za = b1a;
-#pragma unroll
-        for (int k = 0; k < opad<O>(); k += 4) {
-            const float4 x = *reinterpret_cast<const float4*>(&S.x[n][k]);
-            zc = fmaf(x.x, w1c[k], zc);
-            za = fmaf(x.x, w1a[k], za);
-            if (k + 1 < O) { zc = fmaf(x.y, w1c[k + 1], zc); za = fmaf(x.y, w1a[k + 1], za); }
-            if (k + 2 < O) { zc = fmaf(x.z, w1c[k + 2], zc); za = fmaf(x.z, w1a[k + 2], za); }
-            if (k + 3 < O) { zc = fmaf(x.w, w1c[k + 3], zc); za = fmaf(x.w, w1a[k + 3], za); }
-        }
-        S.h1[w][l] = tanh_f(zc);
-        S.h1[w][H + l] = tanh_f(za);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_wave_barrier();
-        float c0 = b2c, c1 = 0.f, c2 = 0.f, c3 = 0.f, a0 = b2a, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-#pragma unroll
-        for (int k = 0; k < H; k += 4) {
-            const float4 hc = *reinterpret_cast<const float4*>(&S.h1[w][k]);
-            const float4 ha = *reinterpret_cast<const float4*>(&S.h1[w][H + k]);
-            c0 = fmaf(hc.x, w2c[k], c0);
-            c1 = fmaf(hc.y, w2c[k + 1], c1);
-            c2 = fmaf(hc.z, w2c[k + 2], c2);
-            c3 = fmaf(hc.w, w2c[k + 3], c3);
-            a0 = fmaf(ha.x, w2a[k], a0);
-            a1 = fmaf(ha.y, w2a[k + 1], a1);
-            a2 = fmaf(ha.z, w2a[k + 2], a2);
-            a3 = fmaf(ha.w, w2a[k + 3], a3);
-        }
-        const float h2c = tanh_f((c0 + c1) + (c2 + c3));
-#pragma unroll
-        for (int q = 0; q < K; ++q) v[q] = wave_sum64(h2c * wv[q]) + bv[q];
-        if (heads_actor) {
-            const float h2a = tanh_f((a0 + a1) + (a2 + a3));
-#pragma unroll
-            for (int j = 0; j < A; ++j) mu[j] = wave_sum64(h2a * wm[j]) + bm[j];
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // h1 reads done before the next row's writes
-        __builtin_amdgcn_wave_barrier();
-    };
-
-    // lane j < A of each env wave keeps its noise one step ahead
-    float eps_next[NE];
-    auto fetch_eps = [&](int step) {
-#pragma unroll
-        for (int e = 0; e < NE; ++e) {
-            const int n = w + 4 * e;
-            const size_t idx = ((size_t)step * N + n) * A + l;
-            eps_next[e] = (n < N && l < A) ? (a.noise ? a.noise[idx] : counter_normal(a.seed, idx)) : 0.f;
-        }
-    };
-    fetch_eps(0);
-    PGM_STAMP_DECL
-    for (int step = 0; step < T; ++step) {
-        float eps[NE];
-#pragma unroll
-        for (int e = 0; e < NE; ++e) eps[e] = eps_next[e];
-        if (step + 1 < T) fetch_eps(step + 1);
-        PGM_STAMP(0);
-#pragma unroll
-        for (int e = 0; e < NE; ++e) {
-            const int n = w + 4 * e;
-            if (n >= N) break;
-            float v[K], mu[A];
-            forward(n, v, mu, true);
-            if (l < K) val[((size_t)step * N + n) * K + l] = sel_lane(v, l);
-            // Gaussian draw (torch.normal(mean, std) = eps * std + mean), log-prob, clipped env action
-            float lpj = 0.f;
-            double acj = 0.0;
-            if (l < A) {
-                const float muj = sel_lane(mu, l);
-                const float av = fmaf(eps[e], sd, muj);
-                const float dz = (av - muj) / sd;
-                lpj = -0.5f * dz * dz - ls - LOG_SQRT_2PI;
-                act[((size_t)step * N + n) * A + l] = av;
-                acj = clipd((double)av, alo, ahi);
-            }
-            const float lps = wave_sum64(lpj);
-            if (l == 0) logp[(size_t)step * N + n] = lps;
-            PGM_STAMP(1);
-            // dynamics (fp64): s' = tanh(d*s + U a_c + c), objectives, time limit, auto-reset
-            double ac[A], e2 = 0.0;
-#pragma unroll
-            for (int j = 0; j < A; ++j) {
-                ac[j] = readlane_d(acj, j);
-                e2 += ac[j] * ac[j];
-            }
-            double ua = 0.0;
-#pragma unroll
-            for (int j = 0; j < A; ++j) ua += Uo[j] * ac[j];
-            const double sn = tanh_d(d_o * s_o[e] + ua + c_o);
-#pragma unroll
-            for (int q = 0; q < K; ++q) objraw[e][q] = wave_sum64_d(fl ? Vo[q] * sn : 0.0) + ebase[q] - ecoef[q] * e2;
-            const int el = elapsed[e] + 1;
-            done[e] = el >= maxs;
-            badf[e] = done[e] && el == maxs;
-            elapsed[e] = done[e] ? 0 : el;
-            s_o[e] = done[e] ? s0_o[e] : sn;
-#pragma unroll
-            for (int q = 0; q < K; ++q)
-                objacc[e][q] = obj_valid ? objacc[e][q] * nc.gamma + objraw[e][q] : objraw[e][q];
-            ret[e] = ret[e] * nc.gamma + 0.0;
-            if (fl) S.snew[n][l] = s_o[e];
-            if (l < K) S.objacc[n][l] = sel_lane_d(objacc[e], l);
-            if (l == 0) S.ret[n] = ret[e];
-        }
-        obj_valid = 1;
-        PGM_STAMP(3);
-        lds_sync();
-        // ---- VecNormalize statistics (counts from before this step)
-        {
-            const double dn = (double)N;
-            const bool pow2 = (N & (N - 1)) == 0;
-            const double rn = 1.0 / dn;
-            auto divn = [&](double x) { return pow2 ? x * rn : x / dn; };
-            if (w == 0 && fl && nc.use_ob) {
-                double sum = 0.0;
-                for (int n = 0; n < N; ++n) sum += S.snew[n][l];
-                const double bmn = divn(sum);
-                double sq = 0.0;
-                for (int n = 0; n < N; ++n) {
-                    const double dd = S.snew[n][l] - bmn;
-                    sq += dd * dd;
-                }
-                double mean = S.ob_mean[l], var = S.ob_var[l];
-                chan_merge(mean, var, S.ob_count, bmn, divn(sq), dn);
-                S.ob_mean[l] = mean;
-                S.ob_var[l] = var;
-                S.ob_inv[l] = 1.0 / sqrt(var + nc.eps);
-            }
-            if (w == 1 && l < K && nc.use_obj) {
-                double sum = 0.0;
-                for (int n = 0; n < N; ++n) sum += S.objacc[n][l];
-                const double bmn = divn(sum);
-                double sq = 0.0;
-                for (int n = 0; n < N; ++n) {
-                    const double dd = S.objacc[n][l] - bmn;
-                    sq += dd * dd;
-                }
-                double mean = S.obj_mean[l], var = S.obj_var[l];
-                chan_merge(mean, var, S.obj_count, bmn, divn(sq), dn);
-                S.obj_mean[l] = mean;
-                S.obj_var[l] = var;
-                S.obj_inv[l] = 1.0 / sqrt(var + nc.eps);
-            }
-            if (w == 2 && l == 0) {  // ret_rms on the (always zero-reward) discounted return
-                double sum = 0.0;
-                for (int n = 0; n < N; ++n) sum += S.ret[n];
-                const double bmn = divn(sum);
-                double sq = 0.0;
-                for (int n = 0; n < N; ++n) sq += (S.ret[n] - bmn) * (S.ret[n] - bmn);
-                chan_merge(S.ret_mean, S.ret_var, S.ret_count, bmn, divn(sq), dn);
-                S.ret_count += dn;
-            }
-        }
-        lds_sync();
-        PGM_STAMP(4);
-        if (t == 0) {  // counts advance after every reader of this step
-            if (nc.use_ob) S.ob_count += (double)N;
-            if (nc.use_obj) S.obj_count += (double)N;
-        }
-        // ---- emit: normalised fp32 obs (next step's input), scaled objectives, masks
-#pragma unroll
-        for (int e = 0; e < NE; ++e) {
-            const int n = w + 4 * e;
-            if (n >= N) break;
-            if (fl) {
-                double v = s_o[e];
-                if (nc.use_ob) v = clipd((v - S.ob_mean[l]) * S.ob_inv[l], -nc.clipob, nc.clipob);
-                const float f = (float)v;  // VecPyTorch .float() (envs.py:192)
-                S.x[n][l] = f;
-                obs[((size_t)(step + 1) * N + n) * O + l] = f;
-            }
-            if (l < K) {
-                double r = sel_lane_d(objraw[e], l);
-                if (nc.use_obj) r = clipd(r * S.obj_inv[l], -nc.cliprew, nc.cliprew);
-                rew[((size_t)step * N + n) * K + l] = (float)r;
-            }
-            if (l == 0) {
-                masks[(size_t)(step + 1) * N + n] = done[e] ? 0.f : 1.f;
-                bad[(size_t)(step + 1) * N + n] = badf[e] ? 0.f : 1.f;
-            }
-            if (done[e]) {
-#pragma unroll
-                for (int q = 0; q < K; ++q) objacc[e][q] = 0.0;
-                ret[e] = 0.0;
-            }
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // x rows visible to this wave's lanes
-        __builtin_amdgcn_wave_barrier();
-        PGM_STAMP(5);
-    }
-    // bootstrap value (mopg.py:132-135) -> value_preds[T] (storage.py:85)
-#pragma unroll
-    for (int e = 0; e < NE; ++e) {
-        const int n = w + 4 * e;
-        if (n >= N) break;
-        float v[K], mu[A];
-        forward(n, v, mu, false);
-        if (l < K) val[((size_t)T * N + n) * K + l] = sel_lane(v, l);
-    }
-    // ---- env state and statistics back to HBM
-#pragma unroll
-    for (int e = 0; e < NE; ++e) {
-        const int n = w + 4 * e;
-        if (n >= N) break;
-        if (fl) a.st.s[((size_t)p * N + n) * O + l] = s_o[e];
-        if (l < K) a.st.obj_acc[((size_t)p * N + n) * K + l] = sel_lane_d(objacc[e], l);
-        if (l == 0) {
-            a.st.ret[p * N + n] = ret[e];
-            a.st.elapsed[p * N + n] = elapsed[e];
-        }
-    }
-    __syncthreads();
-    for (int o = t; o < O; o += RT) {
-        a.ns.ob_mean[(size_t)p * O + o] = S.ob_mean[o];
-        a.ns.ob_var[(size_t)p * O + o] = S.ob_var[o];
-    }
-    if (t < K) {
-        a.ns.obj_mean[p * K + t] = S.obj_mean[t];
-        a.ns.obj_var[p * K + t] = S.obj_var[t];
-    }
-    if (t == 0) {
-        a.ns.ob_count[p] = S.ob_count;
-        a.ns.obj_count[p] = S.obj_count;
-        a.ns.ret_mean[p] = S.ret_mean;
-        a.ns.ret_var[p] = S.ret_var;
-        a.ns.ret_count[p] = S.ret_count;
-        a.st.obj_acc_valid[p] = obj_valid;
-    }
-}
-
-struct EvalArgs {
-    int P;
-    Layout L;
-    const float* params;
-    pgm_env_spec spec;
-    const double *ob_mean, *ob_var, *s0_eval;
-    int eval_num, use_ob, raw;
-    double gamma;
-    double* objs;
-};
 
 template <int O, int A, int K>
 __global__ __launch_bounds__(RT) void eval_kernel(EvalArgs a) {
@@ -1184,14 +760,10 @@ int pgm_rollout(const pgm_dims* d, const float* params, const pgm_env_spec* spec
     }
     RolloutArgs a{d->P, d->N, d->T, make_layout(d->O, d->A, d->K, d->H), params, *spec, *st, *ns, *rb,
                   noise, seed, carry};
+    const char* sel = getenv("PGM_ROLLOUT_KERNEL");  // "block": the workgroup-per-step kernel (A/B, tests)
+    if (!(sel && sel[0] == 'b') && rollout_lanes_supported(d)) return launch_rollout_lanes(d, a, (hipStream_t)stream);
     return dispatch_dims(d->O, d->A, d->K, "pgm_rollout", [&](auto o, auto aa, auto k) {
         constexpr int O = decltype(o)::value, A = decltype(aa)::value, K = decltype(k)::value;
-        const char* sel = getenv("PGM_ROLLOUT_KERNEL");  // "block": the workgroup-per-step kernel (A/B)
-        if constexpr (O <= 32) {  // one wave per env (N <= 8)
-            if (!(sel && sel[0] == 'b'))
-                return launch_smem(rollout_wave_kernel<O, A, K>, d->P, sizeof(WaveSmem<O, A, K>),
-                                   (hipStream_t)stream, a, "pgm_rollout");
-        }
         return launch_smem(rollout_kernel<O, A, K>, d->P, sizeof(StepSmem<O, A, K>), (hipStream_t)stream, a,
                            "pgm_rollout");
     });
@@ -1207,6 +779,8 @@ int pgm_eval(const pgm_dims* d, const float* params, const pgm_env_spec* spec, c
     }
     EvalArgs a{d->P, make_layout(d->O, d->A, d->K, d->H), params, *spec, ob_mean, ob_var, s0_eval,
                eval_num, use_ob_rms, raw, gamma, objs_out};
+    const char* sel = getenv("PGM_EVAL_KERNEL");  // "block": the workgroup-per-step kernel (A/B, tests)
+    if (!(sel && sel[0] == 'b') && eval_waves_supported(d, eval_num)) return launch_eval_waves(d, a, (hipStream_t)stream);
     return dispatch_dims(d->O, d->A, d->K, "pgm_eval", [&](auto o, auto aa, auto k) {
         constexpr int O = decltype(o)::value, A = decltype(aa)::value, K = decltype(k)::value;
         return launch_smem(eval_kernel<O, A, K>, d->P, sizeof(StepSmem<O, A, K>), (hipStream_t)stream, a,

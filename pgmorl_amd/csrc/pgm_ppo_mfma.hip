@@ -744,6 +744,7 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
             a.stats[p * 3 + 2] = st_e / n;
         }
     }
+    PGM_STAMP_FLUSH;
 }
 
 static int device_cus() {

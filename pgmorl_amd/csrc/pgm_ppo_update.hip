@@ -501,6 +501,7 @@ __global__ __launch_bounds__(UT) void ppo_update_kernel(UpdArgs a) {
         a.stats[p * 3 + 1] = st_a / n;
         a.stats[p * 3 + 2] = st_e / n;
     }
+    PGM_STAMP_FLUSH;
 }
 
 }  // namespace pgm

@@ -1,0 +1,99 @@
+// Shared pieces of the rollout / evaluation kernels: argument blocks, fp64 VecNormalize helpers and the
+// launchers of the lane-parallel kernels (pgm_rollout_lanes.hip) used by the entry points in
+// pgm_policy_env.hip.
+#pragma once
+#include "pgm_common.hpp"
+
+namespace pgm {
+
+constexpr int NMAX = 8;  // envs per task handled by one workgroup
+constexpr int RT = 256;  // threads per workgroup of the block-per-task kernels
+
+template <int O>
+constexpr int opad() { return (O + 3) & ~3; }
+
+// LDS-only barrier: waits for this wave's LDS traffic, not for its outstanding HBM stores
+// (__syncthreads() would also drain vmcnt, i.e. wait for every rollout-storage store).
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+// this wave's LDS writes visible to its own lanes
+__device__ __forceinline__ void wave_lds_fence_r() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
+
+struct NormCfg {
+    double gamma, clipob, cliprew, eps;
+    int use_ob, use_obj;
+};
+__host__ __device__ inline NormCfg norm_cfg(const pgm_norm_state& ns) {
+    return NormCfg{ns.gamma, ns.clipob, ns.cliprew, ns.epsilon, ns.use_ob_rms, ns.use_obj_rms};
+}
+
+// Chan merge of a batch (bm, bv, n) into (mean, var, count) -- running_mean_std.py:20-31
+// (one fp64 division: the reference's three divisions by tot_count become a multiply by 1/tot)
+__device__ __forceinline__ void chan_merge(double& mean, double& var, double count, double bm, double bv, double n) {
+    const double delta = bm - mean;
+    const double inv_tot = 1.0 / (count + n);
+    const double new_mean = mean + delta * n * inv_tot;
+    const double m2 = var * count + bv * n + delta * delta * count * n * inv_tot;
+    mean = new_mean;
+    var = m2 * inv_tot;
+}
+
+__device__ __forceinline__ double clipd(double x, double lo, double hi) { return fmin(fmax(x, lo), hi); }
+
+// fp64 tanh as expm1(2y) / (expm1(2y) + 2): a few ulp (the env state's precision is fp64, the
+// observation leaves as fp32), half the instructions of the double-double libm tanh.  |y| is clamped at
+// 20, where tanh is 1 to fp64 precision.
+__device__ __forceinline__ double tanh_d(double y) {
+    const double e = expm1(2.0 * fmin(fmax(y, -20.0), 20.0));
+    return e / (e + 2.0);
+}
+
+template <int N_>
+__device__ __forceinline__ float sel_lane(const float (&v)[N_], int l) {
+    float r = 0.f;
+#pragma unroll
+    for (int q = 0; q < N_; ++q) r = l == q ? v[q] : r;
+    return r;
+}
+template <int N_>
+__device__ __forceinline__ double sel_lane_d(const double (&v)[N_], int l) {
+    double r = 0.0;
+#pragma unroll
+    for (int q = 0; q < N_; ++q) r = l == q ? v[q] : r;
+    return r;
+}
+
+struct RolloutArgs {
+    int P, N, T;
+    Layout L;
+    const float* params;
+    pgm_env_spec spec;
+    pgm_env_state st;
+    pgm_norm_state ns;
+    pgm_rollout_buf rb;
+    const float* noise;
+    uint64_t seed;
+    int carry;
+};
+
+struct EvalArgs {
+    int P;
+    Layout L;
+    const float* params;
+    pgm_env_spec spec;
+    const double *ob_mean, *ob_var, *s0_eval;
+    int eval_num, use_ob, raw;
+    double gamma;
+    double* objs;
+};
+
+// Lane-parallel kernels (pgm_rollout_lanes.hip).  Each returns PGM_E_UNSUPPORTED without launching when
+// the dims are outside its envelope (the caller then uses the block-per-task kernel).
+int launch_rollout_lanes(const pgm_dims* d, const RolloutArgs& a, hipStream_t stream);
+int launch_eval_waves(const pgm_dims* d, const EvalArgs& a, hipStream_t stream);
+bool rollout_lanes_supported(const pgm_dims* d);
+bool eval_waves_supported(const pgm_dims* d, int eval_num);
+
+}  // namespace pgm

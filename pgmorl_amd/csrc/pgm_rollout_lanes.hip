@@ -1,0 +1,652 @@
+// Lane-parallel rollout, critic-value and evaluation kernels (obs_dim <= 48, the default path for every
+// SynthMO env but Humanoid; Humanoid uses the block-per-task kernels of pgm_policy_env.hip).
+//
+// rollout_lane_kernel: one workgroup per task, env n on wave n % 4.  A wave's lanes hold unit l of the
+// ACTOR tower (the env step only needs the action) and feature l of its env's state.  The critic is not on
+// the T-step dependency chain at all: value_kernel evaluates it afterwards for all (T+1) x N stored
+// observations at once.  The one cross-env step of an iteration, the VecNormalize running statistics, is
+// computed REDUNDANTLY by every wave from a double-buffered LDS row per env (lane l < O: feature l of
+// ob_rms; lanes O..O+K-1: obj_rms; lane O+K: ret_rms), so a step costs one workgroup barrier and the
+// normalised observation never leaves the wave that needs it.  The action mean is wave-uniform (DPP sums
+// end in readlanes), so the Gaussian draw, the clipped action and the log-prob are computed uniformly in
+// every lane: no cross-lane traffic between the policy head and the dynamics.
+//
+// eval_wave_kernel: one wave per evaluation episode (morl/mopg.py:25-46), no workgroup barriers.
+//
+// Reference semantics (paths relative to the reference tree):
+//   Policy.act / get_value                 a2c_ppo_acktr/model.py:57-73, 237-246
+//   DiagGaussian sample + log_prob         a2c_ppo_acktr/distributions.py:29-40,71-90
+//   DummyVecEnv auto-reset                 baselines/common/vec_env/dummy_vec_env.py:45-56
+//   TimeLimitMask bad_transition           a2c_ppo_acktr/envs.py:122-131
+//   VecNormalize.step_wait                 baselines/common/vec_env/vec_normalize.py:29-61
+//   RunningMeanStd Chan merge              baselines/common/running_mean_std.py:3-31
+//   masks / bad_masks / obj_tensor         morl/mopg.py:110-130
+//   RolloutStorage.insert / after_update   a2c_ppo_acktr/storage.py:50-75
+//   bootstrap value (get_value on obs[T])  morl/mopg.py:132-135, storage.py:85
+//   evaluation()                           morl/mopg.py:25-46
+#include "pgm_dispatch.hpp"
+#include "pgm_rollout.hpp"
+
+PGM_STAMP_UNIT(lanes)
+
+namespace pgm {
+
+template <int O, int K>
+constexpr bool lanes_fit() { return O <= 48 && O + K + 1 <= 64; }
+
+// per-lane actor tower: unit l of both layers, every head row of unit l (weights constant in a launch)
+template <int O, int A>
+struct ActorLane {
+    float w1[O], w2[H], wm[A], bm[A], ls[A], sd[A], rsd[A];
+    float b1, b2;
+    __device__ void load(const float* __restrict__ prm, const Layout& L, int l) {
+#pragma unroll
+        for (int k = 0; k < O; ++k) w1[k] = prm[L.off[PGM_P_ACTOR_W1] + k * H + l];
+#pragma unroll
+        for (int k = 0; k < H; ++k) w2[k] = prm[L.off[PGM_P_ACTOR_W2] + k * H + l];
+#pragma unroll
+        for (int j = 0; j < A; ++j) {
+            wm[j] = prm[L.off[PGM_P_MEAN_W] + l * A + j];
+            bm[j] = prm[L.off[PGM_P_MEAN_B] + j];
+            ls[j] = prm[L.off[PGM_P_LOGSTD] + j];
+            sd[j] = expf(ls[j]);
+            rsd[j] = 1.0f / sd[j];
+        }
+        b1 = prm[L.off[PGM_P_ACTOR_B1] + l];
+        b2 = prm[L.off[PGM_P_ACTOR_B2] + l];
+    }
+    // action mean of the fp32 row x (LDS, read by every lane) -> mu[A], wave-uniform.  h1 is this wave's
+    // [H] LDS exchange row.  Ends with h1 free for reuse.
+    __device__ void forward(const float* x, float* h1, int l, float (&mu)[A]) const {
+        constexpr int OP = opad<O>();
+        float z0 = b1, z1 = 0.f;  // two chains over the inputs
+#pragma unroll
+        for (int k = 0; k < OP; k += 4) {
+            const float4 v = *reinterpret_cast<const float4*>(x + k);
+            z0 = fmaf(v.x, w1[k], z0);
+            if (k + 1 < O) z1 = fmaf(v.y, w1[k + 1], z1);
+            if (k + 2 < O) z0 = fmaf(v.z, w1[k + 2], z0);
+            if (k + 3 < O) z1 = fmaf(v.w, w1[k + 3], z1);
+        }
+        h1[l] = tanh_f(z0 + z1);
+        wave_lds_fence_r();
+        float a0 = b2, a1 = 0.f, a2 = 0.f, a3 = 0.f;  // four short chains instead of one of 64
+#pragma unroll
+        for (int k = 0; k < H; k += 4) {
+            const float4 h = *reinterpret_cast<const float4*>(h1 + k);
+            a0 = fmaf(h.x, w2[k], a0);
+            a1 = fmaf(h.y, w2[k + 1], a1);
+            a2 = fmaf(h.z, w2[k + 2], a2);
+            a3 = fmaf(h.w, w2[k + 3], a3);
+        }
+        const float h2 = tanh_f((a0 + a1) + (a2 + a3));
+        float pr[A];
+#pragma unroll
+        for (int j = 0; j < A; ++j) pr[j] = h2 * wm[j];
+        wave_sum64_multi<A>(pr, mu);
+#pragma unroll
+        for (int j = 0; j < A; ++j) mu[j] += bm[j];
+        wave_lds_fence_r();  // every lane's h1 reads done before the row is rewritten
+    }
+};
+
+// pairwise (tree) sum of a short register array: log2(M) dependent adds instead of M
+template <class V, int M>
+__device__ __forceinline__ V tree_sum(const V (&x)[M]) {
+    if constexpr (M == 1) {
+        return x[0];
+    } else {
+        constexpr int H0 = M / 2;
+        V lo[H0], hi[M - H0];
+#pragma unroll
+        for (int i = 0; i < H0; ++i) lo[i] = x[i];
+#pragma unroll
+        for (int i = 0; i < M - H0; ++i) hi[i] = x[H0 + i];
+        return tree_sum(lo) + tree_sum(hi);
+    }
+}
+
+// per-lane SynthMO constants of feature o = l (zeros beyond O) and the wave-uniform ones
+template <int O, int A, int K>
+struct EnvLane {
+    double U[A], V[K], d, c;
+    double lo[A], hi[A], ebase[K], ecoef[K];
+    __device__ void load(const pgm_env_spec& g, int l) {
+        const bool fl = l < O;
+        const int o = fl ? l : 0;
+#pragma unroll
+        for (int j = 0; j < A; ++j) {
+            U[j] = fl ? g.U[o * A + j] : 0.0;
+            lo[j] = g.act_lo[j];
+            hi[j] = g.act_hi[j];
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            V[k] = fl ? g.V[k * O + o] : 0.0;
+            ebase[k] = g.ebase[k];
+            ecoef[k] = g.ecoef[k];
+        }
+        d = fl ? g.d[o] : 0.0;
+        c = fl ? g.c[o] : 0.0;
+    }
+    // s' = tanh(d*s + U clip(a) + c) for this lane's feature; raw objectives (wave-uniform):
+    // obj_k = V_k . s' + ebase_k - ecoef_k * |clip(a)|^2   (the Walker form, environments/walker2d.py:23-25)
+    __device__ double step(double s, const double (&ac)[A], double e2, double (&objraw)[K]) const {
+        double pu[A];
+#pragma unroll
+        for (int j = 0; j < A; ++j) pu[j] = U[j] * ac[j];
+        const double sn = tanh_d(d * s + tree_sum(pu) + c);
+#pragma unroll
+        for (int k = 0; k < K; ++k) objraw[k] = wave_sum64_d(V[k] * sn) + ebase[k] - ecoef[k] * e2;
+        return sn;
+    }
+};
+
+// ------------------------------------------------------------------------------------------ rollout
+constexpr int NCH = 32;  // rollout steps per staged noise chunk
+
+template <int O, int A, int NN>
+struct LaneSmem {
+    alignas(16) float x[NN][opad<O>()];  // normalised fp32 obs row of env n (written / read by its wave)
+    alignas(16) float h1[4][H];          // per-wave layer-1 exchange row
+    double sr[2][NN][64];                // statistics rows, double-buffered by step parity
+    alignas(16) float eps[2][NN][NCH * A];  // action noise of env n for NCH steps, double-buffered
+};
+
+// 1 / sqrt(x) in fp64: hardware estimate + two Newton steps (~1 ulp; the IEEE sqrt + divide pair is a
+// ~25-instruction dependent chain on the per-step critical path)
+__device__ __forceinline__ double rsqrt_d(double x) {
+    double r = __builtin_amdgcn_rsq(x);
+    double e = fma(-x * r, r, 1.0);
+    r = fma(r * e, 0.5, r);
+    e = fma(-x * r, r, 1.0);
+    return fma(r * e, 0.5, r);
+}
+
+template <int O, int A, int K, int NN>
+__global__ __launch_bounds__(256) void rollout_lane_kernel(RolloutArgs a) {
+    static_assert(lanes_fit<O, K>(), "lane roles need O + K + 1 <= 64");
+    constexpr int NE = (NN + 3) / 4;  // env slots per wave
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    auto& S = *reinterpret_cast<LaneSmem<O, A, NN>*>(smem_raw);
+    const int p = blockIdx.x, l = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int T = a.T;
+    const NormCfg nc = norm_cfg(a.ns);
+    const Layout& L = a.L;
+    const float* prm = a.params + (size_t)p * L.total;
+    float* obs = a.rb.obs + (size_t)p * (T + 1) * NN * O;
+    float* act = a.rb.actions + (size_t)p * T * NN * A;
+    float* logp = a.rb.logp + (size_t)p * T * NN;
+    float* rew = a.rb.rewards + (size_t)p * T * NN * K;
+    float* masks = a.rb.masks + (size_t)p * (T + 1) * NN;
+    float* bad = a.rb.bad_masks + (size_t)p * (T + 1) * NN;
+    const int maxs = a.spec.max_episode_steps;
+
+    ActorLane<O, A> pol;
+    pol.load(prm, L, l);
+    EnvLane<O, A, K> env;
+    env.load(a.spec, l);
+
+    // ---- env state of this wave's envs (feature l), VecNormalize accumulators (wave-uniform)
+    const bool fl = l < O;
+    const int lo = fl ? l : 0;
+    double s_o[NE], s0_o[NE], objacc[NE][K], ret[NE], objraw[NE][K];
+    int elapsed[NE], done[NE], badf[NE];
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+        const int n = min(w + 4 * e, NN - 1);
+        s_o[e] = a.st.s[((size_t)p * NN + n) * O + lo];
+        s0_o[e] = a.st.s0[(size_t)n * O + lo];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            objacc[e][k] = a.st.obj_acc[((size_t)p * NN + n) * K + k];
+            objraw[e][k] = 0.0;
+        }
+        ret[e] = a.st.ret[p * NN + n];
+        elapsed[e] = a.st.elapsed[p * NN + n];
+        done[e] = badf[e] = 0;
+    }
+    int obj_valid = a.st.obj_acc_valid[p];
+
+    // ---- running statistics, one lane per statistic (role 0: ob feature l, 1: objective l - O, 2: ret),
+    // replicated in every wave
+    const int role = l < O ? 0 : l < O + K ? 1 : l == O + K ? 2 : 3;
+    const int ko = role == 1 ? l - O : 0;
+    double mean = 0.0, var = 1.0, cnt = 1.0;
+    if (role == 0) {
+        mean = a.ns.ob_mean[(size_t)p * O + l];
+        var = a.ns.ob_var[(size_t)p * O + l];
+        cnt = a.ns.ob_count[p];
+    } else if (role == 1) {
+        mean = a.ns.obj_mean[p * K + ko];
+        var = a.ns.obj_var[p * K + ko];
+        cnt = a.ns.obj_count[p];
+    } else if (role == 2) {
+        mean = a.ns.ret_mean[p];
+        var = a.ns.ret_var[p];
+        cnt = a.ns.ret_count[p];
+    }
+    const bool upd = role == 0 ? nc.use_ob != 0 : role == 1 ? nc.use_obj != 0 : role == 2;
+    double itot = 1.0;  // 1 / (count + batch) of this step's merge, computed at the top of the step
+    double inv = 1.0;
+
+    // ---- slot 0: after_update() carry (storage.py:71-75) and the first policy input
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+        const int n = w + 4 * e;
+        if (n >= NN) break;
+        if (fl) {
+            float v = obs[(size_t)(a.carry ? T : 0) * NN * O + n * O + l];
+            if (a.carry) obs[n * O + l] = v;
+            S.x[n][l] = v;
+        }
+        if (a.carry && l == 0) {
+            masks[n] = masks[(size_t)T * NN + n];
+            bad[n] = bad[(size_t)T * NN + n];
+        }
+    }
+    // action noise, staged per wave in LDS chunks of NCH steps: the next chunk is loaded into registers a
+    // whole chunk ahead and written to LDS at the chunk boundary, so its vmcnt wait (which also drains the
+    // wave's rollout-storage stores) is paid once per NCH steps.  (LDS-DMA would make the compiler wait on
+    // vmcnt before every read of the buffer.)  NULL noise: the perf-mode counter stream, drawn by the lanes.
+    constexpr int CA = NCH * A, CR = (CA + 63) / 64;
+    float nreg[NE][CR];
+    auto load_eps = [&](int c) {
+        size_t idx[NE][CR];
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+            const int n = min(w + 4 * e, NN - 1);
+#pragma unroll
+            for (int r = 0; r < CR; ++r) {
+                const int i = min(64 * r + l, CA - 1);
+                const int st = min(c * NCH + i / A, T - 1), j = i % A;
+                idx[e][r] = ((size_t)st * NN + n) * A + j;
+            }
+        }
+        if (a.noise) {  // uniform branch: plain loads, consumed a chunk later
+#pragma unroll
+            for (int e = 0; e < NE; ++e)
+#pragma unroll
+                for (int r = 0; r < CR; ++r) nreg[e][r] = a.noise[idx[e][r]];
+        } else {
+#pragma unroll
+            for (int e = 0; e < NE; ++e)
+#pragma unroll
+                for (int r = 0; r < CR; ++r) nreg[e][r] = counter_normal(a.seed, idx[e][r]);
+        }
+    };
+    auto store_eps = [&](int cb) {
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+            const int n = w + 4 * e;
+            if (n >= NN) break;
+#pragma unroll
+            for (int r = 0; r < CR; ++r)
+                if (64 * r + l < CA) S.eps[cb][n][64 * r + l] = nreg[e][r];
+        }
+    };
+    load_eps(0);
+    store_eps(0);
+    // every preamble load (weights, constants, state) retired here with a wait the compiler's scoreboard
+    // sees: otherwise their first uses inside the step loop get vmcnt waits that, from the second step on,
+    // drain the previous step's rollout-storage stores
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    if (NCH < T) load_eps(1);
+    wave_lds_fence_r();
+    PGM_STAMP_DECL
+
+    for (int step = 0; step < T; ++step) {
+        const int buf = step & 1;
+        const int cs = step % NCH, cb = (step / NCH) & 1;
+        if (cs == 0 && step > 0) {  // chunk step / NCH (loaded a chunk ago) into LDS; load the next one
+            store_eps(cb);
+            if (step + NCH < T) load_eps(step / NCH + 1);
+            wave_lds_fence_r();
+        }
+        itot = 1.0 / (cnt + (double)NN);
+        PGM_STAMP(0);
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+            const int n = w + 4 * e;
+            if (n >= NN) break;
+            float mu[A];
+            pol.forward(S.x[n], S.h1[w], l, mu);
+            PGM_STAMP(1);
+            // Gaussian draw (torch.normal(mean, std) = eps * std + mean), log-prob and clipped action, all
+            // wave-uniform: lane j's noise is broadcast by readlane
+            float lpt[A], avl = 0.f;
+            double ac[A], sq[A];
+#pragma unroll
+            for (int j = 0; j < A; ++j) {
+                const float ej = S.eps[cb][n][cs * A + j];
+                const float av = fmaf(ej, pol.sd[j], mu[j]);
+                const float dz = (av - mu[j]) * pol.rsd[j];
+                lpt[j] = -0.5f * dz * dz - pol.ls[j] - LOG_SQRT_2PI;
+                avl = l == j ? av : avl;
+                ac[j] = clipd((double)av, env.lo[j], env.hi[j]);
+                sq[j] = ac[j] * ac[j];
+            }
+            const float lp = tree_sum(lpt);
+            const double e2 = tree_sum(sq);
+            if (l < A) act[((size_t)step * NN + n) * A + l] = avl;
+            if (l == 0) logp[(size_t)step * NN + n] = lp;
+            PGM_STAMP(6);
+            // dynamics (fp64), time limit, auto-reset, VecNormalize accumulators
+            const double sn = env.step(s_o[e], ac, e2, objraw[e]);
+            PGM_STAMP(7);
+            const int el = elapsed[e] + 1;
+            done[e] = el >= maxs;
+            badf[e] = done[e] && el == maxs;
+            elapsed[e] = done[e] ? 0 : el;
+            s_o[e] = done[e] ? s0_o[e] : sn;
+#pragma unroll
+            for (int k = 0; k < K; ++k) objacc[e][k] = obj_valid ? objacc[e][k] * nc.gamma + objraw[e][k] : objraw[e][k];
+            ret[e] = ret[e] * nc.gamma + 0.0;  // SynthMO's scalar reward is 0 (vec_normalize.py:32)
+            const double rv = role == 0 ? s_o[e] : role == 1 ? sel_lane_d(objacc[e], ko) : role == 2 ? ret[e] : 0.0;
+            S.sr[buf][n][l] = rv;
+            PGM_STAMP(2);
+        }
+        obj_valid = 1;
+        lds_sync();
+        PGM_STAMP(3);
+        // ---- VecNormalize statistics, every wave (counts from before this step; numpy's mean / var
+        // divide by N, exact for N a power of two)
+        {
+            double v[NN], sum = 0.0;
+#pragma unroll
+            for (int n = 0; n < NN; ++n) {
+                v[n] = S.sr[buf][n][l];
+                sum += v[n];
+            }
+            constexpr double rn = 1.0 / NN;
+            const double bm = sum * rn;
+            double sq = 0.0;
+#pragma unroll
+            for (int n = 0; n < NN; ++n) sq = fma(v[n] - bm, v[n] - bm, sq);
+            if (upd) {
+                const double delta = bm - mean;
+                mean = mean + delta * (double)NN * itot;
+                var = (var * cnt + (sq * rn) * (double)NN + delta * delta * cnt * (double)NN * itot) * itot;
+                cnt += (double)NN;
+                inv = rsqrt_d(var + nc.eps);
+            }
+        }
+        PGM_STAMP(4);
+        // ---- emit: normalised fp32 obs (next input), scaled objectives, masks
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+            const int n = w + 4 * e;
+            if (n >= NN) break;
+            if (role == 0) {
+                double v = s_o[e];
+                if (nc.use_ob) v = clipd((v - mean) * inv, -nc.clipob, nc.clipob);
+                const float f = (float)v;  // VecPyTorch .float() (envs.py:192)
+                S.x[n][l] = f;
+                obs[((size_t)(step + 1) * NN + n) * O + l] = f;
+            } else if (role == 1) {
+                double r = sel_lane_d(objraw[e], ko);
+                if (nc.use_obj) r = clipd(r * inv, -nc.cliprew, nc.cliprew);
+                rew[((size_t)step * NN + n) * K + ko] = (float)r;
+            }
+            if (l == 0) {
+                masks[(size_t)(step + 1) * NN + n] = done[e] ? 0.f : 1.f;
+                bad[(size_t)(step + 1) * NN + n] = badf[e] ? 0.f : 1.f;
+            }
+            if (done[e]) {
+#pragma unroll
+                for (int k = 0; k < K; ++k) objacc[e][k] = 0.0;
+                ret[e] = 0.0;
+            }
+        }
+        wave_lds_fence_r();
+        PGM_STAMP(5);
+    }
+
+    // ---- env state and statistics back to HBM
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+        const int n = w + 4 * e;
+        if (n >= NN) break;
+        if (fl) a.st.s[((size_t)p * NN + n) * O + l] = s_o[e];
+        if (l < K) a.st.obj_acc[((size_t)p * NN + n) * K + l] = sel_lane_d(objacc[e], l);
+        if (l == 0) {
+            a.st.ret[p * NN + n] = ret[e];
+            a.st.elapsed[p * NN + n] = elapsed[e];
+        }
+    }
+    if (w == 0) {
+        if (role == 0) {
+            a.ns.ob_mean[(size_t)p * O + l] = mean;
+            a.ns.ob_var[(size_t)p * O + l] = var;
+            if (l == 0) a.ns.ob_count[p] = cnt;
+        } else if (role == 1) {
+            a.ns.obj_mean[p * K + ko] = mean;
+            a.ns.obj_var[p * K + ko] = var;
+            if (ko == 0) a.ns.obj_count[p] = cnt;
+        } else if (role == 2) {
+            a.ns.ret_mean[p] = mean;
+            a.ns.ret_var[p] = var;
+            a.ns.ret_count[p] = cnt;
+            a.st.obj_acc_valid[p] = obj_valid;
+        }
+    }
+    PGM_STAMP_FLUSH;
+}
+
+// ------------------------------------------------------------------------------------------ critic values
+// values[p][i][:] = critic(obs[p][i]) for all (T+1) x N stored rows of a task (get_value on every step's
+// obs, model.py:71-73, and the bootstrap value on obs[T]).  One thread per row, critic tower in LDS
+// (read as wave-wide broadcasts), activations in registers.
+struct ValueArgs {
+    int R;  // rows per task
+    Layout L;
+    const float* params;
+    const float* obs;  // [P][R][O]
+    float* values;     // [P][R][K]
+};
+
+template <int O, int K>
+struct CriticSmem {
+    alignas(16) float W1t[O][H];
+    alignas(16) float W2t[H][H];
+    alignas(16) float Wv[K][H];
+    alignas(16) float b1[H];
+    alignas(16) float b2[H];
+    float bv[K];
+};
+
+template <int O, int K>
+__global__ __launch_bounds__(256) void value_kernel(ValueArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    auto& S = *reinterpret_cast<CriticSmem<O, K>*>(smem_raw);
+    const int p = blockIdx.y, t = threadIdx.x;
+    const Layout& L = a.L;
+    const float* prm = a.params + (size_t)p * L.total;
+    for (int i = t; i < O * H; i += 256) (&S.W1t[0][0])[i] = prm[L.off[PGM_P_CRITIC_W1] + i];
+    for (int i = t; i < H * H; i += 256) (&S.W2t[0][0])[i] = prm[L.off[PGM_P_CRITIC_W2] + i];
+    for (int i = t; i < K * H; i += 256) S.Wv[i / H][i % H] = prm[L.off[PGM_P_VALUE_W] + (i % H) * K + i / H];
+    if (t < H) {
+        S.b1[t] = prm[L.off[PGM_P_CRITIC_B1] + t];
+        S.b2[t] = prm[L.off[PGM_P_CRITIC_B2] + t];
+    }
+    if (t < K) S.bv[t] = prm[L.off[PGM_P_VALUE_B] + t];
+    __syncthreads();
+    const int r = blockIdx.x * 256 + t;
+    if (r >= a.R) return;
+    const float* x = a.obs + ((size_t)p * a.R + r) * O;
+    float h1[H];
+#pragma unroll
+    for (int j = 0; j < H; ++j) h1[j] = S.b1[j];
+    for (int k = 0; k < O; ++k) {  // z1 = b1 + sum_k x_k W1t[k][:]
+        const float xk = x[k];
+#pragma unroll
+        for (int j = 0; j < H; j += 4) {
+            const float4 wv = *reinterpret_cast<const float4*>(&S.W1t[k][j]);
+            h1[j] = fmaf(xk, wv.x, h1[j]);
+            h1[j + 1] = fmaf(xk, wv.y, h1[j + 1]);
+            h1[j + 2] = fmaf(xk, wv.z, h1[j + 2]);
+            h1[j + 3] = fmaf(xk, wv.w, h1[j + 3]);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < H; ++j) h1[j] = tanh_f(h1[j]);
+    float v[K];
+#pragma unroll
+    for (int q = 0; q < K; ++q) v[q] = S.bv[q];
+    for (int j = 0; j < H; j += 4) {  // four output units per pass over h1
+        float4 z = *reinterpret_cast<const float4*>(&S.b2[j]);
+#pragma unroll
+        for (int i = 0; i < H; ++i) {
+            const float4 wv = *reinterpret_cast<const float4*>(&S.W2t[i][j]);
+            z.x = fmaf(h1[i], wv.x, z.x);
+            z.y = fmaf(h1[i], wv.y, z.y);
+            z.z = fmaf(h1[i], wv.z, z.z);
+            z.w = fmaf(h1[i], wv.w, z.w);
+        }
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+            const float4 wq = *reinterpret_cast<const float4*>(&S.Wv[q][j]);
+            v[q] = fmaf(tanh_f(z.x), wq.x, v[q]);
+            v[q] = fmaf(tanh_f(z.y), wq.y, v[q]);
+            v[q] = fmaf(tanh_f(z.z), wq.z, v[q]);
+            v[q] = fmaf(tanh_f(z.w), wq.w, v[q]);
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < K; ++q) a.values[((size_t)p * a.R + r) * K + q] = v[q];
+}
+
+// ------------------------------------------------------------------------------------------ evaluation
+template <int O>
+struct EvalSmem {
+    alignas(16) float x[8][opad<O>()];
+    alignas(16) float h1[8][H];
+    double epi[64][4];  // per-episode objective sums
+};
+constexpr int EVAL_MAX_WAVES = 8, EVAL_MAX_EPISODES = 64;
+
+template <int O, int A, int K>
+__global__ __launch_bounds__(64 * EVAL_MAX_WAVES) void eval_wave_kernel(EvalArgs a) {
+    static_assert(K <= 4, "epi rows hold 4 objectives");
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    auto& S = *reinterpret_cast<EvalSmem<O>*>(smem_raw);
+    const int p = blockIdx.x, l = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nw = blockDim.x >> 6;
+    const float* prm = a.params + (size_t)p * a.L.total;
+    ActorLane<O, A> pol;
+    pol.load(prm, a.L, l);
+    EnvLane<O, A, K> env;
+    env.load(a.spec, l);
+    const bool fl = l < O;
+    const int lo = fl ? l : 0;
+    // mopg.py:37-38: fp64 normalisation with the snapshot ob_rms, fixed eps 1e-8 / clip 10, no fp32 round
+    const double mean = a.use_ob ? a.ob_mean[(size_t)p * O + lo] : 0.0;
+    const double inv = a.use_ob ? 1.0 / sqrt(a.ob_var[(size_t)p * O + lo] + 1e-8) : 1.0;
+    const int maxs = a.spec.max_episode_steps;
+    for (int ep = w; ep < a.eval_num; ep += nw) {
+        double s = a.s0_eval[(size_t)ep * O + lo];
+        double acc[K], g = 1.0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc[k] = 0.0;
+        for (int st = 0; st < maxs; ++st) {  // SynthMO episodes end at the time limit
+            if (fl) {
+                double v = s;
+                if (a.use_ob) v = clipd((v - mean) * inv, -10.0, 10.0);
+                S.x[w][l] = (float)v;
+            }
+            wave_lds_fence_r();
+            float mu[A];
+            pol.forward(S.x[w], S.h1[w], l, mu);
+            double ac[A], sq[A];
+#pragma unroll
+            for (int j = 0; j < A; ++j) {  // deterministic action = mean, clipped by the env
+                ac[j] = clipd((double)mu[j], env.lo[j], env.hi[j]);
+                sq[j] = ac[j] * ac[j];
+            }
+            const double e2 = tree_sum(sq);
+            double objraw[K];
+            s = env.step(s, ac, e2, objraw);
+#pragma unroll
+            for (int k = 0; k < K; ++k) acc[k] += g * objraw[k];
+            if (!a.raw) g *= a.gamma;
+        }
+        if (l < K) S.epi[ep][l] = sel_lane_d(acc, l);
+    }
+    __syncthreads();
+    if (threadIdx.x < K) {  // objs /= eval_num, episodes summed in order
+        double sum = 0.0;
+        for (int ep = 0; ep < a.eval_num; ++ep) sum += S.epi[ep][threadIdx.x];
+        a.objs[(size_t)p * K + threadIdx.x] = sum / (double)a.eval_num;
+    }
+}
+
+// ------------------------------------------------------------------------------------------ launchers
+template <class Kern, class Args>
+static int launch_k(Kern k, dim3 grid, dim3 block, size_t smem, hipStream_t s, const Args& args, const char* what) {
+    if (smem > 160 * 1024) {
+        set_error("%s: LDS image %zu bytes exceeds 160 KiB", what, smem);
+        return PGM_E_UNSUPPORTED;
+    }
+    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    if (e != hipSuccess) return hip_fail(e, what);
+    hipLaunchKernelGGL(k, grid, block, smem, s, args);
+    return launch_status(what);
+}
+
+static bool lanes_dims(int O, int K) { return O <= 48 && O + K + 1 <= 64; }
+
+bool rollout_lanes_supported(const pgm_dims* d) {
+    return lanes_dims(d->O, d->K) && (d->N == 1 || d->N == 2 || d->N == 4 || d->N == 8);
+}
+
+bool eval_waves_supported(const pgm_dims* d, int eval_num) {
+    return lanes_dims(d->O, d->K) && d->K <= 4 && eval_num <= EVAL_MAX_EPISODES;
+}
+
+template <int O, int A, int K, int NN>
+static int launch_rollout_n(const pgm_dims* d, const RolloutArgs& a, hipStream_t s) {
+    if (int rc = launch_k(rollout_lane_kernel<O, A, K, NN>, dim3(d->P), dim3(64 * (NN < 4 ? NN : 4)),
+                          sizeof(LaneSmem<O, A, NN>), s, a, "pgm_rollout"))
+        return rc;
+    const int R = (d->T + 1) * d->N;
+    ValueArgs va{R, a.L, a.params, a.rb.obs, a.rb.values};
+    return launch_k(value_kernel<O, K>, dim3((R + 255) / 256, d->P), dim3(256), sizeof(CriticSmem<O, K>), s, va,
+                    "pgm_rollout (critic values)");
+}
+
+int launch_rollout_lanes(const pgm_dims* d, const RolloutArgs& a, hipStream_t stream) {
+    return dispatch_dims(d->O, d->A, d->K, "pgm_rollout", [&](auto o, auto aa, auto k) -> int {
+        constexpr int O = decltype(o)::value, A = decltype(aa)::value, K = decltype(k)::value;
+        if constexpr (!lanes_fit<O, K>()) {
+            set_error("pgm_rollout: obs_dim %d outside the lane kernel", O);
+            return PGM_E_UNSUPPORTED;
+        } else {
+            switch (d->N) {
+                case 1: return launch_rollout_n<O, A, K, 1>(d, a, stream);
+                case 2: return launch_rollout_n<O, A, K, 2>(d, a, stream);
+                case 4: return launch_rollout_n<O, A, K, 4>(d, a, stream);
+                case 8: return launch_rollout_n<O, A, K, 8>(d, a, stream);
+            }
+            set_error("pgm_rollout: N=%d outside the lane kernel (1, 2, 4, 8)", d->N);
+            return PGM_E_UNSUPPORTED;
+        }
+    });
+}
+
+int launch_eval_waves(const pgm_dims* d, const EvalArgs& a, hipStream_t stream) {
+    return dispatch_dims(d->O, d->A, d->K, "pgm_eval", [&](auto o, auto aa, auto k) -> int {
+        constexpr int O = decltype(o)::value, A = decltype(aa)::value, K = decltype(k)::value;
+        if constexpr (!lanes_fit<O, K>() || K > 4) {
+            set_error("pgm_eval: dims outside the wave kernel");
+            return PGM_E_UNSUPPORTED;
+        } else {
+            const int nw = a.eval_num < EVAL_MAX_WAVES ? a.eval_num : EVAL_MAX_WAVES;
+            return launch_k(eval_wave_kernel<O, A, K>, dim3(d->P), dim3(64 * nw), sizeof(EvalSmem<O>), stream, a,
+                            "pgm_eval");
+        }
+    });
+}
+
+}  // namespace pgm

@@ -20,7 +20,7 @@ tb.env_reset()
 L = _lib.lib()
 buf = (C.c_ulonglong * 64)()
 SB = int(os.environ.get('STAMP_BLOCK', 0))  # workgroup sampled (update SPLIT: 2p = critic, 2p+1 = actor)
-for name in ('rollout', 'update', 'mfma'):
+for name in ('rollout', 'update', 'mfma', 'lanes'):
     getattr(L, f'pgm_debug_stamps_{name}')(buf, 1)
     getattr(L, f'pgm_debug_stamp_block_{name}')(SB)
 tb.iteration(0, 3e-4)
@@ -29,9 +29,13 @@ names = {0: "loop/top", 1: 'policy fwd', 2: 'store val + sample', 3: 'logp + dyn
          5: 'vecnorm emit', 10: 'policy L2 (in fwd)'}
 mnames = {0: 'stage rows', 1: 'pass end sync', 2: 'grad image rounds', 3: 'Adam', 8: 'sumsq', 9: 'norm exchange',
           4: 'tile: L1 + L2 fwd', 5: 'tile: heads + loss', 6: 'tile: gWh, dH2, gW2', 7: 'tile: dH1, gW1'}
-for name, steps in (('rollout', T), ('update', 320), ('mfma', 320)):
+lnames = {0: 'loop/top', 1: 'actor fwd', 6: 'sample', 7: 'dynamics', 2: 'accumulators + row', 3: 'barrier',
+          4: 'stats', 5: 'emit'}
+for name, steps in (('rollout', T), ('update', 320), ('mfma', 320), ('lanes', T)):
     if name == 'mfma':
         names = mnames
+    if name == 'lanes':
+        names = lnames
     getattr(L, f'pgm_debug_stamps_{name}')(buf, 1)
     v = np.array(list(buf), dtype=np.float64)
     tot = v.sum()

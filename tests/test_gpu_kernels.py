@@ -237,10 +237,12 @@ def _oracle_rollout(pol, envs, ro, noise):
         ro.value_preds[-1] = pol.get_value(ro.obs[-1])
 
 
-@pytest.mark.parametrize('kernel', ['wave', 'block'])
-@pytest.mark.parametrize('env,N,T', [('MO-Hopper-v2', 4, 48), ('MO-Walker2d-v2', 2, 520), ('MO-Hopper-v3', 6, 40)])
+@pytest.mark.parametrize('kernel', ['lanes', 'block'])
+@pytest.mark.parametrize('env,N,T', [('MO-Hopper-v2', 4, 48), ('MO-Walker2d-v2', 2, 520), ('MO-Hopper-v3', 6, 40),
+                                     ('MO-Hopper-v3', 8, 40), ('MO-Walker2d-v2', 1, 33), ('MO-Ant-v2', 4, 24)])
 def test_rollout(gpu, env, N, T, kernel, monkeypatch):
-    monkeypatch.setenv('PGM_ROLLOUT_KERNEL', kernel)  # wave: one wave per env (default); block: workgroup step
+    # lanes: one wave per env + batched critic values (default for N in 1/2/4/8); block: workgroup per step
+    monkeypatch.setenv('PGM_ROLLOUT_KERNEL', kernel)
     P = 2
     spec, tb, pols = _batch_with_policies(env, P, N, T, seed=3, scale=0.05)
     s0 = envspec.reset_table(spec['obs_dim'], 0, N)
@@ -283,8 +285,11 @@ def test_rollout_perf_rng_equals_explicit_noise(gpu):
     assert torch.equal(a_rng, tb.actions)
 
 
-@pytest.mark.parametrize('env,eval_num,raw', [('MO-Walker2d-v2', 1, True), ('MO-Hopper-v3', 2, False)])
-def test_eval(gpu, env, eval_num, raw):
+@pytest.mark.parametrize('kernel', ['waves', 'block'])
+@pytest.mark.parametrize('env,eval_num,raw', [('MO-Walker2d-v2', 1, True), ('MO-Hopper-v3', 2, False),
+                                              ('MO-Hopper-v2', 11, True)])
+def test_eval(gpu, env, eval_num, raw, kernel, monkeypatch):
+    monkeypatch.setenv('PGM_EVAL_KERNEL', kernel)  # waves: one wave per episode (default); block: workgroup step
     P = 3
     spec, tb, pols = _batch_with_policies(env, P, 4, 8, seed=5, scale=0.1, eval_num=eval_num, raw=raw)
     args = small_args(env, eval_num=eval_num, raw=raw)

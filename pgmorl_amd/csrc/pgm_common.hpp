@@ -21,15 +21,26 @@ struct Layout {
     int32_t total;
 };
 Layout make_layout(int O, int A, int K, int Hd);
-// pgm_ppo_update workspace: [2P] tagged 8-byte granules + 1 flag word (padded to 256 bytes), then the
-// packed sample table [P][T*N][RS] fp32 (obs | action | old logp | adv | old value | return, RS a power of 2)
+// pgm_ppo_update workspace: [4P + 1] tagged 8-byte granules (tower-norm hand-offs; word 2P = timeout flag),
+// padded to 256 bytes; the gradient exchange of the half-split update, [P][2 towers][2 halves][2 parities]
+// slots of (tower image + 1) granules; then the packed sample table [P][T*N][RS] fp32 (obs | action |
+// old logp | adv | old value | return, RS a power of 2)
 inline int ppo_row_stride(int O, int A, int K) {
     const int n = O + A + 2 + 2 * K;
     return n <= 16 ? 16 : n <= 32 ? 32 : n <= 64 ? 64 : 128;
 }
-inline size_t ppo_flag_bytes(int P) { return ((size_t)(2 * P + 1) * 8 + 255) / 256 * 256; }
+constexpr int ppo_img_floats(int O, int A, int K) {  // TowerImg<O, A, K> of pgm_ppo_mfma.hip
+    const int Q = A > K ? A : K;
+    return O * H + H * (H + 1) + Q * H + 2 * H + Q + A;
+}
+inline size_t ppo_flag_bytes(int P) { return ((size_t)(4 * P + 1) * 8 + 255) / 256 * 256; }
+inline int ppo_xslot(int O, int A, int K) { return (ppo_img_floats(O, A, K) + 1 + 31) / 32 * 32; }  // granules
+inline size_t ppo_xbuf_bytes(const pgm_dims* d) {
+    return d->O <= 32 ? (size_t)d->P * 8 * ppo_xslot(d->O, d->A, d->K) * 8 : 0;
+}
 inline size_t ppo_workspace_bytes(const pgm_dims* d) {
-    return ppo_flag_bytes(d->P) + (size_t)d->P * d->T * d->N * ppo_row_stride(d->O, d->A, d->K) * sizeof(float);
+    return ppo_flag_bytes(d->P) + ppo_xbuf_bytes(d) +
+           (size_t)d->P * d->T * d->N * ppo_row_stride(d->O, d->A, d->K) * sizeof(float);
 }
 
 // ---------------------------------------------------------------- device helpers

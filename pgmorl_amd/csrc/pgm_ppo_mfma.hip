@@ -35,6 +35,7 @@ PGM_STAMP_UNIT(mfma)
 namespace pgm {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void lds_void_t;
 
 constexpr int MT = 256;     // threads: 4 waves
@@ -178,15 +179,23 @@ struct MArgs {
     const int32_t* perms;
     const float* rows;       // packed sample table [P][T*N][RS]
     float* stats;
-    unsigned long long* ws;  // SPLIT: [2P] tagged granules + [1] timeout flag, zeroed before the launch
+    unsigned long long* ws;  // SPLIT: tagged norm granules + timeout flag (word 2P), zeroed before the launch
+    unsigned long long* xb;  // MODE 2: gradient-image exchange slots, zeroed before the launch
+    int xslot;               // 8-byte words per exchange slot (image payload, flag granule in the last word)
+    int xbytes;              // bytes of the exchange buffer
     int P;
 };
 
 __device__ __forceinline__ float wmin2(float a, float b) { return a < b ? 1.f : (a == b ? 0.5f : 0.f); }
 __device__ __forceinline__ float wmax2(float a, float b) { return a > b ? 1.f : (a == b ? 0.5f : 0.f); }
 
-template <int O, int A, int K, bool SPLIT>
+// MODE 0: one workgroup per task (joint towers).  MODE 1 (SPLIT): one workgroup per tower.  MODE 2: each tower
+// on TWO workgroups that take one half of every minibatch's rows each and add their gradient images through
+// tagged granules (both compute half0 + half1 in that order, so their Adam steps stay bitwise identical).
+template <int O, int A, int K, int MODE>
 __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
+    constexpr bool SPLIT = MODE >= 1;
+    constexpr int NS = MODE == 2 ? 2 : 1;  // workgroups per tower
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     using Sm = MSmem<O, A, K, SPLIT>;
     auto& S = *reinterpret_cast<Sm*>(smem_raw);
@@ -201,14 +210,21 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
     constexpr int oW2 = O * H, oWh = oW2 + H * SCR, oB1 = oWh + Q * H, oB2 = oB1 + H, oBh = oB2 + H, oLs = oBh + Q;
     constexpr int NWT = SPLIT ? 4 : 2;  // waves per tower
     const int t = threadIdx.x, w = t >> 6, l = t & 63, h = l >> 5, c = l & 31;
-    const int p = SPLIT ? (int)(blockIdx.x >> 1) : (int)blockIdx.x;
-    const int m = SPLIT ? (int)(blockIdx.x & 1) : (w & 1);  // tower of this wave
+    // MODE 2 block map: in each group of 16 blocks, block r holds half r >> 3 of tower (r & 7) & 1 of task
+    // 4g + ((r & 7) >> 1): the two halves of a tower are blocks b and b + 8 (one XCD under round-robin
+    // placement -- speed only, the hand-off is correct anywhere)
+    const int bx = (int)blockIdx.x;
+    const int p = MODE == 2 ? 4 * (bx >> 4) + ((bx & 7) >> 1) : SPLIT ? (bx >> 1) : bx;
+    const int hs = MODE == 2 ? (bx >> 3) & 1 : 0;  // half of the minibatch rows
+    if (p >= a.P) return;
+    const int m = MODE == 2 ? (bx & 1) : SPLIT ? (bx & 1) : (w & 1);  // tower of this wave
     const int sh = SPLIT ? w : (w >> 1);                      // wave index within the tower
     const int NQ = m == 0 ? K : A;
     const int N = a.N, T = a.T, B = T * N;
     const int E = a.hp.ppo_epoch, M = a.hp.num_mini_batch;
     const int mb = B / M, nb = B / mb;
-    const int npm = (mb + SBk - 1) / SBk;  // passes per minibatch
+    const int r0 = hs * mb / NS, mbs = (hs + 1) * mb / NS - r0;  // this workgroup's rows of each minibatch
+    const int npm = (mbs + SBk - 1) / SBk;  // passes per minibatch
     const int npass = E * nb * npm;
     const float clip = a.hp.clip_param;
     const Layout& L = a.L;
@@ -225,8 +241,8 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
     // re-reads the row's first chunk.
     auto issue_idx = [&](int g, int buf) {
         const int e = g / (nb * npm), rem = g - e * nb * npm, bb = rem / npm, j = rem - bb * npm;
-        const int ns = min(SBk, mb - j * SBk);
-        const int32_t* src = a.perms + (size_t)e * B + bb * mb + j * SBk;
+        const int ns = min(SBk, mbs - j * SBk);
+        const int32_t* src = a.perms + (size_t)e * B + bb * mb + r0 + j * SBk;
         for (int r0 = w * 64; r0 < SBk; r0 += 256)  // rows beyond ns re-read the last valid index
             __builtin_amdgcn_global_load_lds((const void*)(src + min(r0 + l, ns - 1)),
                                              (lds_void_t*)&S.IB[buf][r0], 4, 0, 0);
@@ -302,8 +318,8 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
             for (int q = 0; q < A; ++q) gLs[q] = 0.f;
             float lsum = 0.f;
 
-            for (int s0 = 0; s0 < mb; s0 += SBk, ++gp) {
-                const int ns = min(SBk, mb - s0);
+            for (int s0 = 0; s0 < mbs; s0 += SBk, ++gp) {
+                const int ns = min(SBk, mbs - s0);
                 const int cur = NBUF == 2 ? (gp & 1) : 0;
                 if constexpr (NBUF == 2) {  // stage the next pass while this one computes
                     if (gp + 1 < npass) issue_rows(cur ^ 1, (gp + 1) & 1);
@@ -612,11 +628,84 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                 lds_sync_m();
             }
             PGM_STAMP(2);
+            if constexpr (NS == 2) {
+                // ---- add the other half's gradient image.  Publish: 16-B sc1 (write-through) buffer stores,
+                // every wave drains them, barrier, ONE lane stores the tagged flag granule {step, loss sum}.
+                // Consume: ONE lane polls the partner's flag, barrier, 16-B sc1 loads of its image (no acquire
+                // fence needed: every load of the handed-off bytes is sc1; cdna_hip_programming.md G16 R1).
+                // Slots are double-buffered by step parity: a half can only rewrite a slot after the partner
+                // has published the next step, i.e. after it finished reading this one.
+                const unsigned tag = (unsigned)(nstep + 1);
+                const int par = nstep & 1;
+                const int slot_mine = ((p * 2 + m) * 2 + hs) * 2 + par;
+                const int slot_other = ((p * 2 + m) * 2 + (1 - hs)) * 2 + par;
+                const int off_mine = slot_mine * a.xslot * 8, off_other = slot_other * a.xslot * 8;
+                const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(a.xb, 0, a.xbytes, 0x00020000);
+                constexpr int NV4 = IMG / 4, TAIL = IMG - 4 * NV4;
+                constexpr int SC1 = 16;  // cache-policy aux bit of the buffer builtins: sc1
+                float* G0 = S.big.GA[0];
+                const float* G1 = S.big.GA[1];
+                const float lsum_wg = (S.red[8] + S.red[9]) + (S.red[10] + S.red[11]);
+                for (int i = t; i < NV4; i += MT) {
+                    u32x4 v;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const float g = G0[4 * i + q] + G1[4 * i + q];
+                        G0[4 * i + q] = g;
+                        v[q] = __float_as_uint(g);
+                    }
+                    __builtin_amdgcn_raw_buffer_store_b128(v, xr, off_mine + 16 * i, 0, SC1);
+                }
+                if (t < TAIL) {
+                    const float g = G0[4 * NV4 + t] + G1[4 * NV4 + t];
+                    G0[4 * NV4 + t] = g;
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(g), xr, off_mine + 16 * NV4 + 4 * t, 0, SC1);
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
+                lds_sync_m();
+                PGM_STAMP(10);
+                if (t == 0) {
+                    unsigned long long* flag_mine = a.xb + (size_t)slot_mine * a.xslot + a.xslot - 1;
+                    const unsigned long long* flag_other = a.xb + (size_t)slot_other * a.xslot + a.xslot - 1;
+                    __hip_atomic_store(flag_mine, ((unsigned long long)tag << 32) | __float_as_uint(lsum_wg),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    unsigned long long x = 0;
+                    for (unsigned spins = 0;; ++spins) {
+                        x = __hip_atomic_load(flag_other, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if ((unsigned)(x >> 32) == tag) break;
+                        if (spins > (1u << 26)) {  // partner never arrived: flag the launch as failed
+                            __hip_atomic_store(a.ws + 2 * a.P, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            x = 0;
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                    const float lo = __uint_as_float((unsigned)x);
+                    S.red[12] = hs == 0 ? lsum_wg + lo : lo + lsum_wg;
+                }
+                lds_sync_m();  // the polling lane matched: every wave may load the partner's image
+                for (int i = t; i < NV4; i += MT) {
+                    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(xr, off_other + 16 * i, 0, SC1);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const float ov = __uint_as_float(v[q]);
+                        G0[4 * i + q] = hs == 0 ? G0[4 * i + q] + ov : ov + G0[4 * i + q];
+                    }
+                }
+                if (t < TAIL) {
+                    const float ov = __uint_as_float(
+                        __builtin_amdgcn_raw_buffer_load_b32(xr, off_other + 16 * NV4 + 4 * t, 0, SC1));
+                    G0[4 * NV4 + t] = hs == 0 ? G0[4 * NV4 + t] + ov : ov + G0[4 * NV4 + t];
+                }
+                PGM_STAMP(11);
+                lds_sync_m();
+            }
             // ---- clip_grad_norm_ over every parameter (padding slots hold zeros)
             constexpr int NG = SPLIT ? IMG : 2 * IMG;
             const float* GA0 = S.big.GA[0];
             const float* GA1 = S.big.GA[1];
-            auto gval = [&](int i) { return SPLIT ? GA0[i] + GA1[i] : GA0[i]; };  // joint: GA[0..1] contiguous
+            // SPLIT: g = GA[0] + GA[1] (MODE 2: already summed into GA[0]); joint: GA[0..1] contiguous
+            auto gval = [&](int i) { return SPLIT && NS == 1 ? GA0[i] + GA1[i] : GA0[i]; };
             float sq = 0.f;
             for (int i = t; i < NG; i += MT) {
                 const float g = gval(i);
@@ -630,7 +719,7 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
             if constexpr (SPLIT) {  // tagged 8-byte granule hand-off with the other tower's workgroup
                 if (t == 0) {
                     const unsigned tag = (unsigned)(nstep + 1);
-                    unsigned long long* ws = a.ws + 2 * p;
+                    unsigned long long* ws = a.ws + (hs == 0 ? 2 * p : 2 * a.P + 1 + 2 * p);
                     __hip_atomic_store(ws + m, ((unsigned long long)tag << 32) | __float_as_uint(total),
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     unsigned long long x = 0;
@@ -655,7 +744,7 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
             const float coef = fminf(a.hp.max_grad_norm / (sqrtf(total) + 1e-6f), 1.f);
             if (t == 0) {
                 if constexpr (SPLIT) {
-                    const float ls = (S.red[8] + S.red[9]) + (S.red[10] + S.red[11]);
+                    const float ls = NS == 2 ? S.red[12] : (S.red[8] + S.red[9]) + (S.red[10] + S.red[11]);
                     if (m == 0) st_v += 0.5f * ls / (float)(mb * K);
                     else st_a += ls / (float)mb;
                 } else {
@@ -725,7 +814,11 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
             PGM_STAMP(3);
         }  // minibatches
     }      // epochs
-    // ---- write back (parameters; SPLIT also the moments)
+    // ---- write back (parameters; SPLIT also the moments); MODE 2: the halves hold identical copies
+    if (hs != 0) {
+        PGM_STAMP_FLUSH;
+        return;
+    }
     for (int i = t; i < NT * IMG; i += MT) {
         const int mi = i / IMG, f = img_to_flat<O, A, K>(i - mi * IMG, img_tower(mi), L);
         if (f < 0) continue;
@@ -758,21 +851,23 @@ static int device_cus() {
     return cus;
 }
 
-template <int O, int A, int K, bool SPLIT>
+template <int O, int A, int K, int MODE>
 int launch_mode(const pgm_dims* d, const MArgs& a, hipStream_t stream) {
+    constexpr bool SPLIT = MODE >= 1;
     const size_t smem = sizeof(MSmem<O, A, K, SPLIT>);
     if (smem > 160 * 1024) {
         set_error("pgm_ppo_update: LDS image %zu bytes exceeds 160 KiB", smem);
         return PGM_E_UNSUPPORTED;
     }
-    auto kern = ppo_update_mfma_kernel<O, A, K, SPLIT>;
+    auto kern = ppo_update_mfma_kernel<O, A, K, MODE>;
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update");
-    if (SPLIT) {
-        e = hipMemsetAsync(a.ws, 0, ppo_flag_bytes(d->P), stream);
+    if (SPLIT) {  // norm granules, timeout flag (and MODE 2: the exchange slots) start at tag 0
+        e = hipMemsetAsync(a.ws, 0, ppo_flag_bytes(d->P) + (MODE == 2 ? ppo_xbuf_bytes(d) : 0), stream);
         if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update (workspace reset)");
     }
-    hipLaunchKernelGGL(kern, dim3(SPLIT ? 2 * d->P : d->P), dim3(MT), smem, stream, a);
+    const int grid = MODE == 2 ? 16 * ((d->P + 3) / 4) : SPLIT ? 2 * d->P : d->P;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(MT), smem, stream, a);
     return launch_status("pgm_ppo_update");
 }
 
@@ -780,18 +875,23 @@ template <int O, int A, int K>
 int launch_ppo_update_mfma(const pgm_dims* d, const MArgs& a, const pgm_rollout_buf* rb, hipStream_t stream) {
     // packed sample table, then the update
     constexpr int RS = row_stride<O, A, K>();
+    static_assert(img_floats<O, A, K>() == ppo_img_floats(O, A, K), "host exchange-slot size out of sync");
     PackArgs pa{d->P, d->N, d->T, rb->obs, rb->actions, rb->logp, rb->adv, rb->values, rb->returns,
                 const_cast<float*>(a.rows)};
     const long long n4 = (long long)d->P * d->T * d->N * (RS / 4);
     auto pack = pack_rows_kernel<O, A, K>;
     hipLaunchKernelGGL(pack, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, stream, pa);
     if (int rc = launch_status("pgm_ppo_update (pack rows)")) return rc;
-    // the split needs both workgroups of a task resident at once: one workgroup per CU (LDS > 80 KiB,
-    // 512 registers per lane), so 2P must not exceed the CU count; otherwise one workgroup per task
+    // every workgroup of a split launch must be resident at once: one per CU (LDS > 80 KiB, 512 registers
+    // per lane), so the grid must fit the CU count.  MODE 2 (4 CUs per task) while 16 * ceil(P / 4) <= CUs,
+    // MODE 1 (2 per task) while 2P <= CUs, else one workgroup per task.  PGM_UPDATE_SPLIT=0/1/2 caps it.
     static_assert(sizeof(MSmem<O, A, K, true>) > 80 * 1024, "split residency argument needs > 80 KiB LDS");
     const char* sel = getenv("PGM_UPDATE_SPLIT");
-    const bool split = 2 * d->P <= device_cus() && !(sel && sel[0] == '0');
-    return split ? launch_mode<O, A, K, true>(d, a, stream) : launch_mode<O, A, K, false>(d, a, stream);
+    const int cap = sel && sel[0] >= '0' && sel[0] <= '2' ? sel[0] - '0' : 2;
+    const int cus = device_cus();
+    if (cap >= 2 && 16 * ((d->P + 3) / 4) <= cus) return launch_mode<O, A, K, 2>(d, a, stream);
+    if (cap >= 1 && 2 * d->P <= cus) return launch_mode<O, A, K, 1>(d, a, stream);
+    return launch_mode<O, A, K, 0>(d, a, stream);
 }
 
 int ppo_update_mfma(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params, float* adam_m, float* adam_v,
@@ -803,7 +903,9 @@ int ppo_update_mfma(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params,
     }
     char* ws = (char*)workspace;
     MArgs a{d->N, d->T, make_layout(d->O, d->A, d->K, d->H), *hp, params, adam_m, adam_v, adam_step, lr, perms,
-            (const float*)(ws + ppo_flag_bytes(d->P)), stats, (unsigned long long*)ws, d->P};
+            (const float*)(ws + ppo_flag_bytes(d->P) + ppo_xbuf_bytes(d)), stats, (unsigned long long*)ws,
+            (unsigned long long*)(ws + ppo_flag_bytes(d->P)), ppo_xslot(d->O, d->A, d->K), (int)ppo_xbuf_bytes(d),
+            d->P};
     return dispatch_dims(d->O, d->A, d->K, "pgm_ppo_update", [&](auto o, auto aa, auto k) -> int {
         constexpr int O = decltype(o)::value, A = decltype(aa)::value, K = decltype(k)::value;
         if constexpr (O > 32) {

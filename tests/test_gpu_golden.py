@@ -67,10 +67,10 @@ def test_golden_adv(gpu, obj_rms):
     _close(tb.adv, g['adv/adv' if obj_rms else 'adv/adv_noobjrms'], 1e-5, 1e-5, 'advantages')
 
 
-@pytest.mark.parametrize('kernel', ['mfma', 'mfma-joint', 'valu'])
+@pytest.mark.parametrize('kernel', ['mfma', 'mfma-tower', 'mfma-joint', 'valu'])
 def test_golden_ppo_update(gpu, kernel, monkeypatch):
     monkeypatch.setenv('PGM_UPDATE_KERNEL', kernel.split('-')[0])
-    monkeypatch.setenv('PGM_UPDATE_SPLIT', '0' if kernel == 'mfma-joint' else '1')
+    monkeypatch.setenv('PGM_UPDATE_SPLIT', {'mfma': '2', 'mfma-tower': '1', 'mfma-joint': '0'}.get(kernel, '2'))
     g = load('kernels')
     E = g['ppo/perms'].shape[0]
     tb = _kernels_batch(g, ppo_epoch=E, num_mini_batch=4)

@@ -347,7 +347,7 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                         const float bias = W.b1[hb * TS + c];
 #pragma unroll
                         for (int r = 0; r < 16; ++r) {
-                            H1[hb][r] = tanh_f(z[hb][r] + bias);
+                            H1[hb][r] = tanh_fast(z[hb][r] + bias);
                             scr[rowof(r, h) * SCR + hb * TS + c] = H1[hb][r];
                         }
                     }
@@ -366,7 +366,7 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                     for (int ob = 0; ob < 2; ++ob) {
                         const float bias = W.b2[ob * TS + c];
 #pragma unroll
-                        for (int r = 0; r < 16; ++r) H2[ob][r] = tanh_f(z[ob][r] + bias);
+                        for (int r = 0; r < 16; ++r) H2[ob][r] = tanh_fast(z[ob][r] + bias);
                     }
                     PGM_STAMP(4);
                     wave_lds_fence();  // every lane finished reading the H1 tile

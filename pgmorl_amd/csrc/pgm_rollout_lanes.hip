@@ -68,7 +68,7 @@ struct ActorLane {
             if (k + 2 < O) z0 = fmaf(v.z, w1[k + 2], z0);
             if (k + 3 < O) z1 = fmaf(v.w, w1[k + 3], z1);
         }
-        h1[l] = tanh_f(z0 + z1);
+        h1[l] = tanh_fast(z0 + z1);
         wave_lds_fence_r();
         float a0 = b2, a1 = 0.f, a2 = 0.f, a3 = 0.f;  // four short chains instead of one of 64
 #pragma unroll
@@ -79,7 +79,7 @@ struct ActorLane {
             a2 = fmaf(h.z, w2[k + 2], a2);
             a3 = fmaf(h.w, w2[k + 3], a3);
         }
-        const float h2 = tanh_f((a0 + a1) + (a2 + a3));
+        const float h2 = tanh_fast((a0 + a1) + (a2 + a3));
         float pr[A];
 #pragma unroll
         for (int j = 0; j < A; ++j) pr[j] = h2 * wm[j];
@@ -490,7 +490,7 @@ __global__ __launch_bounds__(256) void value_kernel(ValueArgs a) {
         }
     }
 #pragma unroll
-    for (int j = 0; j < H; ++j) h1[j] = tanh_f(h1[j]);
+    for (int j = 0; j < H; ++j) h1[j] = tanh_fast(h1[j]);
     float v[K];
 #pragma unroll
     for (int q = 0; q < K; ++q) v[q] = S.bv[q];
@@ -507,10 +507,10 @@ __global__ __launch_bounds__(256) void value_kernel(ValueArgs a) {
 #pragma unroll
         for (int q = 0; q < K; ++q) {
             const float4 wq = *reinterpret_cast<const float4*>(&S.Wv[q][j]);
-            v[q] = fmaf(tanh_f(z.x), wq.x, v[q]);
-            v[q] = fmaf(tanh_f(z.y), wq.y, v[q]);
-            v[q] = fmaf(tanh_f(z.z), wq.z, v[q]);
-            v[q] = fmaf(tanh_f(z.w), wq.w, v[q]);
+            v[q] = fmaf(tanh_fast(z.x), wq.x, v[q]);
+            v[q] = fmaf(tanh_fast(z.y), wq.y, v[q]);
+            v[q] = fmaf(tanh_fast(z.z), wq.z, v[q]);
+            v[q] = fmaf(tanh_fast(z.w), wq.w, v[q]);
         }
     }
 #pragma unroll

@@ -41,7 +41,7 @@ def parse():
     ap.add_argument('--num-steps', type=int, default=2048)
     ap.add_argument('--ppo-epoch', type=int, default=10)
     ap.add_argument('--num-mini-batch', type=int, default=32)
-    ap.add_argument('--cpu-iters', type=int, default=3, help='oracle iterations timed for cpu_baseline')
+    ap.add_argument('--cpu-iters', type=int, default=10, help='oracle iterations timed for cpu_baseline')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--traffic-file', default=os.path.join(ROOT, 'profiles', 'r01_ppo_update_pmc.json'))
     return ap.parse_args()

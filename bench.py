@@ -169,12 +169,12 @@ def main():
     out = {
         'metric': METRIC, 'value': value, 'unit': 'env steps/sec', 'n_gpus': world, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': dt / args.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak',
-        'vs_baseline': None, 'dtype': 'fp32', 'data': 'synthetic (SynthMO-Walker2d env, reference-order random init)',
+        'vs_baseline': None, 'dtype': 'fp32', 'data': f"synthetic (SynthMO-{args.env_name.split('-')[1]} env, reference-order random init)",
         'config': {'workload': f'{args.env_name} (SynthMO) pop={P}/GPU, N={N}, T={T}, ppo_epoch={E}, '
                                f'num_mini_batch={M}, eval_num=1, perf-mode device RNG',
                    'env': args.env_name, 'tasks_per_gpu': P, 'global_tasks': P * world, 'num_processes': N,
                    'num_steps': T, 'ppo_epoch': E, 'num_mini_batch': M, 'parallelism': f'task-sharded x{world}'},
-        'roofline': {'bound': 'mfma', 'kernel': 'ppo_update_mfma_kernel', 'achieved': achieved,
+        'roofline': {'bound': 'mfma', 'kernel': 'ppo_update_mfma_kernel' if spec['obs_dim'] <= 32 else 'ppo_update_wide_kernel', 'achieved': achieved,
                      'peak': PEAK_FP32_TFLOPS, 'unit': 'TFLOP/s', 'frac': achieved / PEAK_FP32_TFLOPS,
                      'traffic': traffic, 'avg_launch_ms': upd_ms, 'flop_per_launch': upd_flop,
                      'algorithmic_bytes_per_launch': P * T * N * E * 4 * (spec['obs_dim'] + spec['act_dim'] +

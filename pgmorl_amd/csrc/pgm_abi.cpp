@@ -26,6 +26,17 @@ int launch_status(const char* what) {
     return PGM_OK;
 }
 
+int device_cu_count() {
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 1;
+    }
+    return cus;
+}
+
 static inline int32_t round_up(int32_t x, int32_t m) { return (x + m - 1) / m * m; }
 
 Layout make_layout(int O, int A, int K, int Hd) {

@@ -38,10 +38,12 @@ inline int ppo_xslot(int O, int A, int K) { return (ppo_img_floats(O, A, K) + 1 
 inline size_t ppo_xbuf_bytes(const pgm_dims* d) {
     return d->O <= 32 ? (size_t)d->P * 8 * ppo_xslot(d->O, d->A, d->K) * 8 : 0;
 }
-inline size_t ppo_workspace_bytes(const pgm_dims* d) {
+inline size_t ppo_workspace_bytes(const pgm_dims* d) {  // obs_dim > 32 (wide kernel): flags + dW1 running sums
+    if (d->O > 32) return ppo_flag_bytes(d->P) + (size_t)d->P * 2 * ((d->O + 31) / 32 * 32) * H * sizeof(float);
     return ppo_flag_bytes(d->P) + ppo_xbuf_bytes(d) +
            (size_t)d->P * d->T * d->N * ppo_row_stride(d->O, d->A, d->K) * sizeof(float);
 }
+int device_cu_count();  // CUs of the current device (cached)
 
 // ---------------------------------------------------------------- device helpers
 // Branch-free fp32 tanh (~14 VALU ops, rel. error ~3e-7): odd Taylor series through x^9 for |x| < 0.25

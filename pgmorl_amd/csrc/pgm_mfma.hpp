@@ -1,0 +1,50 @@
+// Shared pieces of the f32-MFMA PPO update kernels (pgm_ppo_mfma.hip: obs_dim <= 32, pgm_ppo_wide.hip:
+// wider observations).  Tiles of 32 samples; samples on accumulator ROWS, features on COLUMNS:
+//     lane l, register r  <->  (sample rowof(r, l>>5), feature l & 31),  rowof(r,h) = (r&3)+8(r>>2)+4h.
+#pragma once
+#include "pgm_common.hpp"
+
+namespace pgm {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+constexpr int MT = 256;     // threads: 4 waves
+constexpr int TS = 32;      // samples per MFMA tile
+constexpr int SCR = H + 1;  // per-wave transpose tile row stride (conflict-free column reads)
+
+template <int A, int K>
+constexpr int qmax() { return A > K ? A : K; }
+template <int O, int A, int K>
+constexpr int row_stride() {
+    constexpr int n = O + A + 2 + 2 * K;
+    return n <= 16 ? 16 : n <= 32 ? 32 : n <= 64 ? 64 : 128;
+}
+
+__device__ __forceinline__ int rowof(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+__device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ void wave_lds_fence() {  // this wave's LDS writes are visible to its own lanes
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
+// workgroup barrier that leaves in-flight LDS-DMA (vmcnt) alone
+__device__ __forceinline__ void lds_sync_m() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+// retire this wave's LDS-DMA / loads, then the barrier
+__device__ __forceinline__ void dma_sync_m() {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+// v[l] + v[l ^ 32] in every lane: one v_permlane32_swap (VALU, no LDS round trip); the sum is
+// commutative, so both halves get bit-identical results
+__device__ __forceinline__ float half_sum(float v) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// torch.min(a,b) / torch.max(a,b) backward weights for the first argument (ties split the gradient in half)
+__device__ __forceinline__ float wmin2(float a, float b) { return a < b ? 1.f : (a == b ? 0.5f : 0.f); }
+__device__ __forceinline__ float wmax2(float a, float b) { return a > b ? 1.f : (a == b ? 0.5f : 0.f); }
+
+}  // namespace pgm

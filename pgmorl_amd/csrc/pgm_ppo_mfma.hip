@@ -29,47 +29,11 @@
 #include <stdlib.h>
 
 #include "pgm_dispatch.hpp"
+#include "pgm_mfma.hpp"
 
 PGM_STAMP_UNIT(mfma)
 
 namespace pgm {
-
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) void lds_void_t;
-
-constexpr int MT = 256;     // threads: 4 waves
-constexpr int TS = 32;      // samples per MFMA tile
-constexpr int SCR = H + 1;  // per-wave transpose tile row stride (conflict-free column reads)
-
-template <int A, int K>
-constexpr int qmax() { return A > K ? A : K; }
-template <int O, int A, int K>
-constexpr int row_stride() {
-    constexpr int n = O + A + 2 + 2 * K;
-    return n <= 16 ? 16 : n <= 32 ? 32 : n <= 64 ? 64 : 128;
-}
-
-__device__ __forceinline__ int rowof(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
-__device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
-    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
-}
-__device__ __forceinline__ void wave_lds_fence() {  // this wave's LDS writes are visible to its own lanes
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-}
-// workgroup barrier that leaves in-flight LDS-DMA (vmcnt) alone
-__device__ __forceinline__ void lds_sync_m() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-// retire this wave's LDS-DMA / loads, then the barrier
-__device__ __forceinline__ void dma_sync_m() {
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
-// v[l] + v[l ^ 32] in every lane: one v_permlane32_swap (VALU, no LDS round trip); the sum is
-// commutative, so both halves get bit-identical results
-__device__ __forceinline__ float half_sum(float v) {
-    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
 
 // ---------------------------------------------------------------- packed sample table
 struct PackArgs {
@@ -186,8 +150,6 @@ struct MArgs {
     int P;
 };
 
-__device__ __forceinline__ float wmin2(float a, float b) { return a < b ? 1.f : (a == b ? 0.5f : 0.f); }
-__device__ __forceinline__ float wmax2(float a, float b) { return a > b ? 1.f : (a == b ? 0.5f : 0.f); }
 
 // MODE 0: one workgroup per task (joint towers).  MODE 1 (SPLIT): one workgroup per tower.  MODE 2: each tower
 // on TWO workgroups that take one half of every minibatch's rows each and add their gradient images through
@@ -840,16 +802,7 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
     PGM_STAMP_FLUSH;
 }
 
-static int device_cus() {
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            cus = 1;
-    }
-    return cus;
-}
+static int device_cus() { return device_cu_count(); }
 
 template <int O, int A, int K, int MODE>
 int launch_mode(const pgm_dims* d, const MArgs& a, hipStream_t stream) {

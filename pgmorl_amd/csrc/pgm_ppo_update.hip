@@ -510,6 +510,9 @@ namespace pgm {
 int ppo_update_mfma(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params, float* adam_m, float* adam_v,
                     int32_t* adam_step, const float* lr, const int32_t* perms, const pgm_rollout_buf* rb, float* stats,
                     void* workspace, hipStream_t stream);
+int ppo_update_wide(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params, float* adam_m, float* adam_v,
+                    int32_t* adam_step, const float* lr, const int32_t* perms, const pgm_rollout_buf* rb, float* stats,
+                    void* workspace, hipStream_t stream);
 }
 
 using namespace pgm;
@@ -530,12 +533,16 @@ extern "C" int pgm_ppo_update(const pgm_dims* d, const pgm_ppo_hparams* hp, floa
         set_error("pgm_ppo_update: need T*N (%d) >= num_mini_batch (%d) > 0 and ppo_epoch > 0", B, hp->num_mini_batch);
         return PGM_E_SHAPE;
     }
-    // f32-MFMA kernel for obs_dim <= 32 (Walker, Cheetah, Hopper, Ant, Swimmer); the VALU kernel is kept
-    // for A/B measurements (PGM_UPDATE_KERNEL=valu) and covers obs_dim <= 64
+    // f32-MFMA kernels: obs_dim <= 32 (Walker, Cheetah, Hopper, Ant, Swimmer) with LDS-resident towers, wider
+    // observations (Humanoid) with layer 1 in L2; the VALU kernel is kept for A/B measurements
+    // (PGM_UPDATE_KERNEL=valu) and covers obs_dim <= 64
     const char* sel = getenv("PGM_UPDATE_KERNEL");
     const bool valu = sel && sel[0] == 'v';
     if (!valu && d->O <= 32)
         return ppo_update_mfma(d, hp, params, adam_m, adam_v, adam_step, lr, perms, rb, stats, workspace,
+                               (hipStream_t)stream);
+    if (!valu && d->O > 64)
+        return ppo_update_wide(d, hp, params, adam_m, adam_v, adam_step, lr, perms, rb, stats, workspace,
                                (hipStream_t)stream);
     if (d->O > 64) {
         set_error("pgm_ppo_update: obs_dim %d > 64 not supported by the update kernels", d->O);

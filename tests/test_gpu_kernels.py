@@ -207,6 +207,14 @@ def test_ppo_update(gpu, env, T, N, E, M, kernel, monkeypatch):
         _close(tb.stats[p].cpu(), stats, 1e-5, 1e-4, 'loss stats')
 
 
+@pytest.mark.parametrize('env,T,N,E,M', [('MO-Humanoid-v2', 64, 8, 2, 4), ('MO-Humanoid-v2', 50, 3, 1, 3),
+                                         ('MO-Humanoid-v2', 128, 8, 1, 2), ('MO-Humanoid-v2', 256, 8, 1, 32)])
+def test_ppo_update_wide(gpu, env, T, N, E, M, monkeypatch):
+    # obs_dim 376: layer 1 from L2, dW1 running sums in the workspace (pgm_ppo_wide.hip); ragged (mb = 50),
+    # one-pass (mb = 128) and multi-pass (mb = 512) minibatches
+    test_ppo_update(gpu, env, T, N, E, M, 'mfma', monkeypatch)
+
+
 def test_randperm_and_noise_streams(gpu):
     tb = TaskBatch('MO-Walker2d-v2', 1, num_processes=4, num_steps=2048)
     tb.make_perms(5)

@@ -87,6 +87,23 @@ def cpu_baseline(args, spec):
                       f' ({os.cpu_count()} logical CPUs visible)'}
 
 
+def hypervolume(args, history, budget):
+    """HV of the EP over every offspring objective vector this run produced (morl/ep.py:23-31,
+    morl/hypervolume.py), plus the committed device-vs-oracle comparison at an equal budget
+    (scripts/hv_budget.py -> profiles/r01_hv_budget.json), when one exists for this env."""
+    from pgmorl_amd import pareto
+    objs = torch.cat(history).cpu().numpy()
+    idx = pareto.get_ep_indices(objs)
+    hv = {'hv': pareto.compute_hypervolume(objs[idx]) if len(idx) else 0.0, 'ep_size': len(idx),
+          'budget_env_steps': budget, 'rng': 'perf-mode device streams', 'ref_point': 0}
+    path = os.path.join(ROOT, 'profiles', 'r01_hv_budget.json')
+    if os.path.exists(path):
+        rows = [r for r in json.load(open(path)).get('runs', []) if r.get('env') == args.env_name]
+        if rows:
+            hv['vs_oracle_equal_budget'] = {'source': 'profiles/r01_hv_budget.json', 'runs': rows}
+    return hv
+
+
 def main():
     args = parse()
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -115,12 +132,15 @@ def main():
     gathered = torch.zeros(world * P, spec['obj_num'], dtype=torch.float64, device=dev)
     total_updates = 5_000_000 // T // N
 
+    history = []  # every iteration's gathered objective vectors (the offspring the EP is built from)
+
     def step(j):
         tb.iteration(j, 3e-4 * (1 - j / total_updates), carry=True)
         if world > 1:
             dist.all_gather_into_tensor(gathered, tb.objs)
         else:
             gathered.copy_(tb.objs)
+        history.append(gathered.clone())
 
     j = 0
     for _ in range(args.warmup):
@@ -187,6 +207,7 @@ def main():
                           'hbm_frac': value * bytes_per_env_step(spec['obs_dim'], spec['act_dim'], spec['obj_num'],
                                                                  E) / (world * PEAK_HBM_GBS * 1e9)},
     }
+    out['hypervolume'] = hypervolume(args, history, world * P * N * T * len(history))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out['cpu_baseline'] = cb = cpu_baseline(args, spec)
         out['vs_96vcpu_extrapolated'] = value / cb['extrapolated_96vcpu']

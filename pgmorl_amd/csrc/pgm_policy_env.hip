@@ -762,6 +762,7 @@ int pgm_rollout(const pgm_dims* d, const float* params, const pgm_env_spec* spec
                   noise, seed, carry};
     const char* sel = getenv("PGM_ROLLOUT_KERNEL");  // "block": the workgroup-per-step kernel (A/B, tests)
     if (!(sel && sel[0] == 'b') && rollout_lanes_supported(d)) return launch_rollout_lanes(d, a, (hipStream_t)stream);
+    if (!(sel && sel[0] == 'b') && rollout_wide_supported(d)) return launch_rollout_wide(d, a, (hipStream_t)stream);
     return dispatch_dims(d->O, d->A, d->K, "pgm_rollout", [&](auto o, auto aa, auto k) {
         constexpr int O = decltype(o)::value, A = decltype(aa)::value, K = decltype(k)::value;
         return launch_smem(rollout_kernel<O, A, K>, d->P, sizeof(StepSmem<O, A, K>), (hipStream_t)stream, a,

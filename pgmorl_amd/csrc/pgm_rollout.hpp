@@ -50,6 +50,32 @@ __device__ __forceinline__ double tanh_d(double y) {
     return e / (e + 2.0);
 }
 
+// pairwise (tree) sum of a short register array: log2(M) dependent adds instead of M
+template <class V, int M>
+__device__ __forceinline__ V tree_sum(const V (&x)[M]) {
+    if constexpr (M == 1) {
+        return x[0];
+    } else {
+        constexpr int H0 = M / 2;
+        V lo[H0], hi[M - H0];
+#pragma unroll
+        for (int i = 0; i < H0; ++i) lo[i] = x[i];
+#pragma unroll
+        for (int i = 0; i < M - H0; ++i) hi[i] = x[H0 + i];
+        return tree_sum(lo) + tree_sum(hi);
+    }
+}
+
+// 1 / sqrt(x) in fp64: hardware estimate + two Newton steps (~1 ulp; the IEEE sqrt + divide pair is a
+// ~25-instruction dependent chain on the per-step critical path)
+__device__ __forceinline__ double rsqrt_d(double x) {
+    double r = __builtin_amdgcn_rsq(x);
+    double e = fma(-x * r, r, 1.0);
+    r = fma(r * e, 0.5, r);
+    e = fma(-x * r, r, 1.0);
+    return fma(r * e, 0.5, r);
+}
+
 template <int N_>
 __device__ __forceinline__ float sel_lane(const float (&v)[N_], int l) {
     float r = 0.f;
@@ -95,5 +121,10 @@ int launch_rollout_lanes(const pgm_dims* d, const RolloutArgs& a, hipStream_t st
 int launch_eval_waves(const pgm_dims* d, const EvalArgs& a, hipStream_t stream);
 bool rollout_lanes_supported(const pgm_dims* d);
 bool eval_waves_supported(const pgm_dims* d, int eval_num);
+// critic values of every stored observation (value_kernel, after an actor-only rollout)
+int launch_critic_values(const pgm_dims* d, const RolloutArgs& a, hipStream_t stream);
+// wide-observation rollout (pgm_rollout_wide.hip): 48 < obs_dim <= 448, N in {1, 2, 4, 8}, N*K <= 16
+bool rollout_wide_supported(const pgm_dims* d);
+int launch_rollout_wide(const pgm_dims* d, const RolloutArgs& a, hipStream_t stream);
 
 }  // namespace pgm

@@ -90,22 +90,6 @@ struct ActorLane {
     }
 };
 
-// pairwise (tree) sum of a short register array: log2(M) dependent adds instead of M
-template <class V, int M>
-__device__ __forceinline__ V tree_sum(const V (&x)[M]) {
-    if constexpr (M == 1) {
-        return x[0];
-    } else {
-        constexpr int H0 = M / 2;
-        V lo[H0], hi[M - H0];
-#pragma unroll
-        for (int i = 0; i < H0; ++i) lo[i] = x[i];
-#pragma unroll
-        for (int i = 0; i < M - H0; ++i) hi[i] = x[H0 + i];
-        return tree_sum(lo) + tree_sum(hi);
-    }
-}
-
 // per-lane SynthMO constants of feature o = l (zeros beyond O) and the wave-uniform ones
 template <int O, int A, int K>
 struct EnvLane {
@@ -152,16 +136,6 @@ struct LaneSmem {
     double sr[2][NN][64];                // statistics rows, double-buffered by step parity
     alignas(16) float eps[2][NN][NCH * A];  // action noise of env n for NCH steps, double-buffered
 };
-
-// 1 / sqrt(x) in fp64: hardware estimate + two Newton steps (~1 ulp; the IEEE sqrt + divide pair is a
-// ~25-instruction dependent chain on the per-step critical path)
-__device__ __forceinline__ double rsqrt_d(double x) {
-    double r = __builtin_amdgcn_rsq(x);
-    double e = fma(-x * r, r, 1.0);
-    r = fma(r * e, 0.5, r);
-    e = fma(-x * r, r, 1.0);
-    return fma(r * e, 0.5, r);
-}
 
 template <int O, int A, int K, int NN>
 __global__ __launch_bounds__(256) void rollout_lane_kernel(RolloutArgs a) {
@@ -610,10 +584,17 @@ static int launch_rollout_n(const pgm_dims* d, const RolloutArgs& a, hipStream_t
     if (int rc = launch_k(rollout_lane_kernel<O, A, K, NN>, dim3(d->P), dim3(64 * (NN < 4 ? NN : 4)),
                           sizeof(LaneSmem<O, A, NN>), s, a, "pgm_rollout"))
         return rc;
-    const int R = (d->T + 1) * d->N;
-    ValueArgs va{R, a.L, a.params, a.rb.obs, a.rb.values};
-    return launch_k(value_kernel<O, K>, dim3((R + 255) / 256, d->P), dim3(256), sizeof(CriticSmem<O, K>), s, va,
-                    "pgm_rollout (critic values)");
+    return launch_critic_values(d, a, s);
+}
+
+int launch_critic_values(const pgm_dims* d, const RolloutArgs& a, hipStream_t s) {
+    return dispatch_dims(d->O, d->A, d->K, "pgm_rollout (critic values)", [&](auto o, auto, auto k) -> int {
+        constexpr int O = decltype(o)::value, K = decltype(k)::value;
+        const int R = (d->T + 1) * d->N;
+        ValueArgs va{R, a.L, a.params, a.rb.obs, a.rb.values};
+        return launch_k(value_kernel<O, K>, dim3((R + 255) / 256, d->P), dim3(256), sizeof(CriticSmem<O, K>), s, va,
+                        "pgm_rollout (critic values)");
+    });
 }
 
 int launch_rollout_lanes(const pgm_dims* d, const RolloutArgs& a, hipStream_t stream) {

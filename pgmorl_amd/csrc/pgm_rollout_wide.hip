@@ -1,0 +1,543 @@
+// Rollout for WIDE observations (48 < obs_dim <= 512: Humanoid's 376) -- one 256-thread workgroup per task
+// (one wave per SIMD, 512 registers per lane), every one of the T steps on one CU with three workgroup
+// barriers.  Same semantics as the lane kernel of
+// pgm_rollout_lanes.hip (reference sites listed there: Policy.act, DiagGaussian, DummyVecEnv auto-reset,
+// TimeLimitMask, VecNormalize.step_wait, RunningMeanStd, RolloutStorage.insert / after_update); the critic is
+// off the step chain here too (value_kernel afterwards).
+//
+// Work split of one step (NN envs, 4 waves, lane l):
+//   1. layer 1 (O x 64 per env, the dominant MACs): wave w owns the k-slice [w*KW, w*KW + KW) of the inputs,
+//      its W1 rows live in registers (lane = hidden unit), every env's input row is an LDS broadcast, the
+//      products are packed fp32 FMAs (two k per instruction); per-wave partial sums go to LDS.   barrier A
+//   2. env n on wave n % 4: sums the 4 partials (fixed order) + bias, tanh -> h1 row (wave-local), layer 2
+//      with its W2 column in registers, the mean head as transposing DPP sums, then the Gaussian draw,
+//      log-prob and clipped action with lane a = action a; clipped actions (fp64) to LDS.          barrier C
+//   3. feature slots (thread t: features t and t + 256, every env in registers): fp64 SynthMO dynamics, time limit /
+//      auto-reset, per-wave transposing fp64 sums of V_k . s'[n] for the objectives, ob_rms Chan merge of the
+//      feature (all envs are in the thread: no cross-thread reduction), normalised fp32 obs -> LDS + HBM.
+//      The last wave (fewest features) then finishes the PREVIOUS step's objectives: objective sums,
+//      VecNormalize.obj accumulators, obj_rms / ret_rms merges and the scaled rewards.             barrier D
+#include "pgm_dispatch.hpp"
+#include "pgm_rollout.hpp"
+
+namespace pgm {
+
+namespace {
+
+constexpr int WW = 4;          // waves per workgroup (one per SIMD: 512 registers per lane)
+constexpr int WTH = 64 * WW;   // threads
+constexpr int WNCH = 32;       // rollout steps per staged noise chunk
+
+template <int O>
+constexpr int wkw() { return ((O + WW - 1) / WW + 3) & ~3; }  // inputs per wave slice (multiple of 4)
+template <int O>
+constexpr int wrow() { return WW * wkw<O>(); }               // padded LDS input row
+template <int O, int K, int NN>
+constexpr bool wide_fit() { return O > 48 && O <= 2 * WTH && NN * K <= 16 && (K & (K - 1)) == 0; }
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+template <int O, int A, int K, int NN>
+struct WideSmem {
+    alignas(16) float x[NN][wrow<O>()];  // normalised fp32 obs rows (zero padding beyond O)
+    alignas(16) float zp[WW][NN][H];     // layer-1 partial sums, one k-slice per wave
+    alignas(16) float h1[NN][H];         // per-env layer-1 row (written / read by wave n)
+    float mu[NN][32];                    // per-env action means (lane-distribution staging)
+    double ac[NN][A];                    // clipped actions of this step
+    double e2[2][NN];                    // |clip(a)|^2, by step parity (read one step later)
+    double objp[2][WW][16];              // per-wave sums of V_k . s'[n] (index n*K + k), by step parity
+    alignas(16) float eps[2][NN][WNCH * A];
+    double U[A][2 * WTH];                // SynthMO U^T, feature-contiguous (conflict-free per-thread reads)
+};
+
+// fp64 lane-half / row folds of the transposing multi-value sum (pgm_common.hpp has the fp32 forms)
+__device__ __forceinline__ double pl32_fold_d(double a, double b) {
+    const auto lo = __builtin_amdgcn_permlane32_swap(__double2loint(a), __double2loint(b), false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap(__double2hiint(a), __double2hiint(b), false, false);
+    return __hiloint2double(hi[0], lo[0]) + __hiloint2double(hi[1], lo[1]);
+}
+__device__ __forceinline__ double pl16_fold_d(double a, double b) {
+    const auto lo = __builtin_amdgcn_permlane16_swap(__double2loint(a), __double2loint(b), false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap(__double2hiint(a), __double2hiint(b), false, false);
+    return __hiloint2double(hi[0], lo[0]) + __hiloint2double(hi[1], lo[1]);
+}
+__device__ __forceinline__ double row_sum16_d(double v) {
+    v += dpp_d<0x128>(v);
+    v += dpp_d<0x124>(v);
+    v += dpp_d<0x122>(v);
+    v += dpp_d<0x121>(v);
+    return v;
+}
+// 16 simultaneous fp64 64-lane sums: after the folds, row R of y[j] holds value j + 4R; lane 16R writes it
+__device__ __forceinline__ void wave_sum16_d(const double (&v)[16], double* out) {
+    double x[8], y[4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x[i] = pl32_fold_d(v[i], v[i + 8]);  // rows 0,1: v_i   rows 2,3: v_{i+8}
+#pragma unroll
+    for (int j = 0; j < 4; ++j) y[j] = row_sum16_d(pl16_fold_d(x[j], x[j + 4]));  // rows: j, j+4, j+8, j+12
+    const int l = threadIdx.x & 63;
+    if ((l & 15) == 0) {
+        const int R = l >> 4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) out[j + 4 * R] = y[j];
+    }
+}
+
+template <int N_>
+__device__ __forceinline__ int sel_lane_i(const int (&v)[N_], int i) {
+    int r = 0;
+#pragma unroll
+    for (int q = 0; q < N_; ++q) r = i == q ? v[q] : r;
+    return r;
+}
+
+// fp64 tanh for the SynthMO dynamics: 1 - 2 / (exp(2|y|) + 1) with the sign restored; exp through
+// 2^(j/64) table-free range reduction is ocml's, the division is rcp + two Newton steps (~1 ulp).  Absolute
+// error ~1e-16 (relative error grows as |y| -> 0, where the state's absolute precision is what matters).
+__device__ __forceinline__ double tanh_d2(double y) {
+    const double ay = fmin(fabs(y), 20.0);
+    const double e = exp(2.0 * ay) + 1.0;
+    double r = __builtin_amdgcn_rcp(e);
+    r = fma(r, fma(-e, r, 1.0), r);
+    r = fma(r, fma(-e, r, 1.0), r);
+    return copysign(fma(-2.0, r, 1.0), y);
+}
+
+// 17-wide (or any A <= 24) action-mean sums: groups of 8 through wave_sum64_multi
+template <int A>
+__device__ __forceinline__ void head_sums(const float (&pr)[A], float (&mu)[A]) {
+#pragma unroll
+    for (int g = 0; g < A; g += 8) {
+        constexpr int G = 8;
+        float in[G], out[G];
+#pragma unroll
+        for (int i = 0; i < G; ++i) in[i] = g + i < A ? pr[g + i] : 0.f;
+        wave_sum64_multi<G>(in, out);
+#pragma unroll
+        for (int i = 0; i < G; ++i)
+            if (g + i < A) mu[g + i] = out[i];
+    }
+}
+
+template <int O, int A, int K, int NN>
+__global__ __launch_bounds__(WTH) void rollout_wide_kernel(RolloutArgs a) {
+    static_assert(wide_fit<O, K, NN>(), "wide rollout envelope");
+    static_assert(A <= 32, "action lanes");
+    constexpr int KW = wkw<O>(), OR = wrow<O>();
+    constexpr int FPL = (O + WTH - 1) / WTH;  // features per lane (thread t: t, t + WTH)
+    constexpr int EPW = (NN + WW - 1) / WW;   // env slots per wave (env n on wave n % WW, slot n / WW)
+    constexpr int SW = WW - 1;                // statistics wave (fewest features)
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    auto& S = *reinterpret_cast<WideSmem<O, A, K, NN>*>(smem_raw);
+    const int p = blockIdx.x, t = threadIdx.x, l = t & 63;
+    const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int T = a.T;
+    const NormCfg nc = norm_cfg(a.ns);
+    const Layout& L = a.L;
+    const float* prm = a.params + (size_t)p * L.total;
+    float* obs = a.rb.obs + (size_t)p * (T + 1) * NN * O;
+    float* act = a.rb.actions + (size_t)p * T * NN * A;
+    float* logp = a.rb.logp + (size_t)p * T * NN;
+    float* rew = a.rb.rewards + (size_t)p * T * NN * K;
+    float* masks = a.rb.masks + (size_t)p * (T + 1) * NN;
+    float* bad = a.rb.bad_masks + (size_t)p * (T + 1) * NN;
+    const int maxs = a.spec.max_episode_steps;
+
+    // ---- policy registers: W1 rows of this wave's k-slice (lane = unit), W2 column and head row of unit l
+    f2 w1[KW / 2];
+#pragma unroll
+    for (int i = 0; i < KW / 2; ++i) {
+        const int k0 = min(w * KW + 2 * i, O - 2);  // rows >= O: weight 0 (their inputs are 0 as well)
+        const float2 v = make_float2(prm[L.off[PGM_P_ACTOR_W1] + k0 * H + l], prm[L.off[PGM_P_ACTOR_W1] + (k0 + 1) * H + l]);
+        const bool in0 = w * KW + 2 * i < O, in1 = w * KW + 2 * i + 1 < O;
+        w1[i] = f2{in0 ? v.x : 0.f, in1 ? v.y : 0.f};
+    }
+    float w2[H], wm[A];
+#pragma unroll
+    for (int k = 0; k < H; ++k) w2[k] = prm[L.off[PGM_P_ACTOR_W2] + k * H + l];
+#pragma unroll
+    for (int j = 0; j < A; ++j) wm[j] = prm[L.off[PGM_P_MEAN_W] + l * A + j];
+    const float b1 = prm[L.off[PGM_P_ACTOR_B1] + l], b2 = prm[L.off[PGM_P_ACTOR_B2] + l];
+    const int la = l < A ? l : 0;  // action lane a = l < A
+    const float bm_l = prm[L.off[PGM_P_MEAN_B] + la], ls_l = prm[L.off[PGM_P_LOGSTD] + la];
+    const float sd_l = expf(ls_l), rsd_l = 1.0f / sd_l;
+    const double lo_l = a.spec.act_lo[la], hi_l = a.spec.act_hi[la];
+
+    // ---- feature slots j: feature o = t + WTH*j (< O): env constants, every env's state, ob_rms of o
+    bool fv[FPL];
+    int fo[FPL];
+    double V[FPL][K], dd[FPL], cc[FPL], s[FPL][NN], mean[FPL], var[FPL], inv[FPL];
+#pragma unroll
+    for (int j = 0; j < FPL; ++j) {
+        fv[j] = t + WTH * j < O;
+        fo[j] = fv[j] ? t + WTH * j : 0;
+        const int o = fo[j];
+#pragma unroll
+        for (int k = 0; k < K; ++k) V[j][k] = fv[j] ? a.spec.V[k * O + o] : 0.0;
+        dd[j] = fv[j] ? a.spec.d[o] : 0.0;
+        cc[j] = fv[j] ? a.spec.c[o] : 0.0;
+#pragma unroll
+        for (int n = 0; n < NN; ++n) s[j][n] = fv[j] ? a.st.s[((size_t)p * NN + n) * O + o] : 0.0;
+        mean[j] = fv[j] ? a.ns.ob_mean[(size_t)p * O + o] : 0.0;
+        var[j] = fv[j] ? a.ns.ob_var[(size_t)p * O + o] : 1.0;
+        inv[j] = 1.0;
+    }
+    for (int i = t; i < A * O; i += WTH) {
+        const int q = i / O, f = i - q * O;
+        S.U[q][f] = a.spec.U[f * A + q];
+    }
+    double cnt = a.ns.ob_count[p];
+    int elapsed[NN];
+#pragma unroll
+    for (int n = 0; n < NN; ++n) elapsed[n] = a.st.elapsed[p * NN + n];
+
+    // ---- statistics wave: lane i = n*K + k < NN*K (objective accumulator + obj_rms of objective k),
+    // lane 32 + n < 32 + NN (ret of env n + ret_rms)
+    const bool olane = w == SW && l < NN * K, rlane = w == SW && l >= 32 && l < 32 + NN;
+    const int on = olane ? l / K : 0, ok = olane ? l % K : 0, rn = rlane ? l - 32 : 0;
+    double objacc = olane ? a.st.obj_acc[((size_t)p * NN + on) * K + ok] : 0.0;
+    double retv = rlane ? a.st.ret[p * NN + rn] : 0.0;
+    double smean = 0.0, svar = 1.0, scnt = 1.0, sinv = 1.0;
+    if (olane) {
+        smean = a.ns.obj_mean[p * K + ok];
+        svar = a.ns.obj_var[p * K + ok];
+        scnt = a.ns.obj_count[p];
+    } else if (rlane) {
+        smean = a.ns.ret_mean[p];
+        svar = a.ns.ret_var[p];
+        scnt = a.ns.ret_count[p];
+    }
+    int obj_valid = a.st.obj_acc_valid[p];
+    const double ebase = a.spec.ebase[ok], ecoef = a.spec.ecoef[ok];
+
+    // ---- slot 0: after_update() carry (storage.py:71-75) and the first policy input
+    for (int i = t; i < NN * OR; i += WTH) {
+        const int n = i / OR, k = i - n * OR;
+        float v = 0.f;
+        if (k < O) {
+            v = obs[(size_t)(a.carry ? T : 0) * NN * O + n * O + k];
+            if (a.carry) obs[n * O + k] = v;
+        }
+        S.x[n][k] = v;
+    }
+    if (a.carry && t < NN) {
+        masks[t] = masks[(size_t)T * NN + t];
+        bad[t] = bad[(size_t)T * NN + t];
+    }
+    // action noise of this wave's envs in LDS chunks of WNCH steps (as the lane kernel), a chunk ahead in
+    // registers
+    constexpr int CA = WNCH * A, CR = (CA + 63) / 64;
+    float nreg[EPW][CR];
+    auto load_eps = [&](int c) {
+#pragma unroll
+        for (int e = 0; e < EPW; ++e) {
+            const int n = min(w + WW * e, NN - 1);
+            size_t idx[CR];
+#pragma unroll
+            for (int r = 0; r < CR; ++r) {
+                const int i = min(64 * r + l, CA - 1);
+                const int st = min(c * WNCH + i / A, T - 1), j = i % A;
+                idx[r] = ((size_t)st * NN + n) * A + j;
+            }
+            if (a.noise) {
+#pragma unroll
+                for (int r = 0; r < CR; ++r) nreg[e][r] = a.noise[idx[r]];
+            } else {
+#pragma unroll
+                for (int r = 0; r < CR; ++r) nreg[e][r] = counter_normal(a.seed, idx[r]);
+            }
+        }
+    };
+    auto store_eps = [&](int cb) {
+#pragma unroll
+        for (int e = 0; e < EPW; ++e) {
+            const int n = w + WW * e;
+            if (n >= NN) break;
+#pragma unroll
+            for (int r = 0; r < CR; ++r)
+                if (64 * r + l < CA) S.eps[cb][n][64 * r + l] = nreg[e][r];
+        }
+    };
+    load_eps(0);
+    store_eps(0);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): preamble loads retired before the step loop
+    if (WNCH < T) load_eps(1);
+    __syncthreads();
+
+    int done_prev[NN];  // done flags of the previous step (the statistics wave runs one step behind)
+#pragma unroll
+    for (int n = 0; n < NN; ++n) done_prev[n] = 0;
+
+    // statistics of step st (objective sums in objp[par], e2[par]) -> rewards, accumulators, obj/ret_rms
+    auto finish_step = [&](int st, int par) {
+        if (olane) {
+            double sum = 0.0;
+#pragma unroll
+            for (int ww = 0; ww < WW; ++ww) sum += S.objp[par][ww][l];
+            const double raw = sum + ebase - ecoef * S.e2[par][on];
+            objacc = obj_valid ? objacc * nc.gamma + raw : raw;
+            double r = raw;
+            if (nc.use_obj) {  // batch moments over the envs of objective k (lanes l ^ K*m)
+                double bsum = objacc;
+#pragma unroll
+                for (int m = K; m < NN * K; m <<= 1) bsum += __shfl_xor(bsum, m, 64);
+                const double bmean = bsum * (1.0 / NN);
+                double bsq = (objacc - bmean) * (objacc - bmean);
+#pragma unroll
+                for (int m = K; m < NN * K; m <<= 1) bsq += __shfl_xor(bsq, m, 64);
+                chan_merge(smean, svar, scnt, bmean, bsq * (1.0 / NN), (double)NN);
+                scnt += (double)NN;
+                sinv = rsqrt_d(svar + nc.eps);
+                r = clipd(r * sinv, -nc.cliprew, nc.cliprew);
+            }
+            rew[(size_t)st * NN * K + l] = (float)r;
+            if (sel_lane_i(done_prev, on)) objacc = 0.0;
+        }
+        if (rlane) {  // ret = ret * gamma + 0 (SynthMO's scalar reward), ret_rms over the envs
+            retv = retv * nc.gamma + 0.0;
+            double bsum = retv;
+#pragma unroll
+            for (int m = 1; m < NN; m <<= 1) bsum += __shfl_xor(bsum, m, 64);
+            const double bmean = bsum * (1.0 / NN);
+            double bsq = (retv - bmean) * (retv - bmean);
+#pragma unroll
+            for (int m = 1; m < NN; m <<= 1) bsq += __shfl_xor(bsq, m, 64);
+            chan_merge(smean, svar, scnt, bmean, bsq * (1.0 / NN), (double)NN);
+            scnt += (double)NN;
+            if (sel_lane_i(done_prev, rn)) retv = 0.0;
+        }
+        obj_valid = 1;
+    };
+
+    for (int step = 0; step < T; ++step) {
+        const int par = step & 1;
+        const int cs = step % WNCH, cb = (step / WNCH) & 1;
+        if (cs == 0 && step > 0) {
+            store_eps(cb);
+            if (step + WNCH < T) load_eps(step / WNCH + 1);
+        }
+        // ---- 1. layer-1 partial sums of this wave's k-slice, every env (packed fp32 FMAs over k pairs)
+        {
+            f2 acc[NN];
+#pragma unroll
+            for (int n = 0; n < NN; ++n) acc[n] = f2{0.f, 0.f};
+#pragma unroll
+            for (int i = 0; i < KW; i += 4) {
+#pragma unroll
+                for (int n = 0; n < NN; ++n) {
+                    const float4 xv = *reinterpret_cast<const float4*>(&S.x[n][w * KW + i]);
+                    acc[n] = __builtin_elementwise_fma(f2{xv.x, xv.y}, w1[i / 2], acc[n]);
+                    acc[n] = __builtin_elementwise_fma(f2{xv.z, xv.w}, w1[i / 2 + 1], acc[n]);
+                }
+                if ((i & 15) == 12) __builtin_amdgcn_sched_barrier(0);  // bound the hoisted input reads
+            }
+#pragma unroll
+            for (int n = 0; n < NN; ++n) S.zp[w][n][l] = acc[n].x + acc[n].y;
+        }
+        lds_sync();  // A
+        // ---- 2. this wave's envs: layer-1 sum + tanh, layer 2, mean head, Gaussian draw, clipped action
+#pragma unroll
+        for (int e = 0; e < EPW; ++e) {
+            const int n = w + WW * e;
+            if (n >= NN) break;
+            float z = b1;
+#pragma unroll
+            for (int ww = 0; ww < WW; ++ww) z += S.zp[ww][n][l];
+            S.h1[n][l] = tanh_fast(z);
+        }
+        wave_lds_fence_r();
+#pragma unroll
+        for (int e = 0; e < EPW; ++e) {
+            const int n = w + WW * e;
+            if (n >= NN) break;
+            float a0 = b2, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+#pragma unroll
+            for (int k = 0; k < H; k += 4) {
+                const float4 hv = *reinterpret_cast<const float4*>(&S.h1[n][k]);
+                a0 = fmaf(hv.x, w2[k], a0);
+                a1 = fmaf(hv.y, w2[k + 1], a1);
+                a2 = fmaf(hv.z, w2[k + 2], a2);
+                a3 = fmaf(hv.w, w2[k + 3], a3);
+            }
+            const float h2 = tanh_fast((a0 + a1) + (a2 + a3));
+            float pr[A], mu[A];
+#pragma unroll
+            for (int j = 0; j < A; ++j) pr[j] = h2 * wm[j];
+            head_sums<A>(pr, mu);
+            if (l == 0) {
+#pragma unroll
+                for (int j = 0; j < A; ++j) S.mu[n][j] = mu[j];
+            }
+        }
+        wave_lds_fence_r();
+#pragma unroll
+        for (int e = 0; e < EPW; ++e) {
+            const int n = w + WW * e;
+            if (n >= NN) break;
+            const bool al = l < A;
+            const float m = S.mu[n][la] + bm_l;
+            const float ej = S.eps[cb][n][cs * A + la];
+            const float av = fmaf(ej, sd_l, m);
+            const float dz = (av - m) * rsd_l;
+            const float lpt = al ? -0.5f * dz * dz - ls_l - LOG_SQRT_2PI : 0.f;
+            const double acd = clipd((double)av, lo_l, hi_l);
+            const float lp = wave_sum64(lpt);
+            const double e2 = wave_sum64_d(al ? acd * acd : 0.0);
+            if (al) {
+                S.ac[n][l] = acd;
+                act[((size_t)step * NN + n) * A + l] = av;
+            }
+            if (l == 0) {
+                S.e2[par][n] = e2;
+                logp[(size_t)step * NN + n] = lp;
+            }
+        }
+        lds_sync();  // C
+        // ---- 3. time limit, fp64 dynamics, objective partial sums, auto-reset, ob_rms, normalised obs
+        int done[NN];
+#pragma unroll
+        for (int n = 0; n < NN; ++n) {
+            const int el = elapsed[n] + 1;
+            done[n] = el >= maxs;
+            if (t == 0) {
+                masks[(size_t)(step + 1) * NN + n] = done[n] ? 0.f : 1.f;
+                bad[(size_t)(step + 1) * NN + n] = (done[n] && el == maxs) ? 0.f : 1.f;
+            }
+            elapsed[n] = done[n] ? 0 : el;
+        }
+        {
+            double vk[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) vk[i] = 0.0;
+#pragma unroll
+            for (int j = 0; j < FPL; ++j) {
+                if (j > 0 && !fv[j]) continue;
+                double u[A];  // U row of the feature, once per step; clipped actions are LDS broadcasts
+#pragma unroll
+                for (int q = 0; q < A; ++q) u[q] = S.U[q][fo[j]];
+#pragma unroll
+                for (int n = 0; n < NN; ++n) {
+                    asm volatile("" ::: "memory");  // re-read the action row per (feature, env): no hoisting
+                    double pu[A];
+#pragma unroll
+                    for (int q = 0; q < A; ++q) pu[q] = u[q] * S.ac[n][q];
+                    const double sn = tanh_d2(dd[j] * s[j][n] + tree_sum(pu) + cc[j]);
+#pragma unroll
+                    for (int k = 0; k < K; ++k) vk[n * K + k] = fma(V[j][k], sn, vk[n * K + k]);
+                    s[j][n] = sn;
+                }
+            }
+            wave_sum16_d(vk, &S.objp[par][w][0]);
+        }
+#pragma unroll
+        for (int j = 0; j < FPL; ++j) {
+            if (j > 0 && !fv[j]) continue;
+#pragma unroll
+            for (int n = 0; n < NN; ++n)
+                if (done[n]) s[j][n] = a.st.s0[(size_t)n * O + fo[j]];  // auto-reset (dummy_vec_env.py:45-56)
+            if (nc.use_ob) {  // ob_rms.update over the envs of this feature (numpy: divide by N)
+                double sum = 0.0;
+#pragma unroll
+                for (int n = 0; n < NN; ++n) sum += s[j][n];
+                const double bmean = sum * (1.0 / NN);
+                double sq = 0.0;
+#pragma unroll
+                for (int n = 0; n < NN; ++n) sq = fma(s[j][n] - bmean, s[j][n] - bmean, sq);
+                chan_merge(mean[j], var[j], cnt, bmean, sq * (1.0 / NN), (double)NN);
+                inv[j] = rsqrt_d(var[j] + nc.eps);
+            }
+            if (fv[j]) {
+#pragma unroll
+                for (int n = 0; n < NN; ++n) {
+                    double v = s[j][n];
+                    if (nc.use_ob) v = clipd((v - mean[j]) * inv[j], -nc.clipob, nc.clipob);
+                    const float f = (float)v;  // VecPyTorch .float() (envs.py:192)
+                    S.x[n][fo[j]] = f;
+                    obs[((size_t)(step + 1) * NN + n) * O + fo[j]] = f;
+                }
+            }
+        }
+        if (nc.use_ob) cnt += (double)NN;
+        if (w == SW && step > 0) finish_step(step - 1, par ^ 1);
+#pragma unroll
+        for (int n = 0; n < NN; ++n) done_prev[n] = done[n];
+        lds_sync();  // D
+    }
+    if (w == SW) finish_step(T - 1, (T - 1) & 1);
+
+    // ---- env state and statistics back to HBM
+#pragma unroll
+    for (int j = 0; j < FPL; ++j) {
+        if (!fv[j]) continue;
+#pragma unroll
+        for (int n = 0; n < NN; ++n) a.st.s[((size_t)p * NN + n) * O + fo[j]] = s[j][n];
+        a.ns.ob_mean[(size_t)p * O + fo[j]] = mean[j];
+        a.ns.ob_var[(size_t)p * O + fo[j]] = var[j];
+    }
+    if (t == 0) a.ns.ob_count[p] = cnt;
+#pragma unroll
+    for (int n = 0; n < NN; ++n)
+        if (t == n) a.st.elapsed[p * NN + n] = elapsed[n];
+    if (olane) {
+        a.st.obj_acc[((size_t)p * NN + on) * K + ok] = objacc;
+        if (on == 0) {
+            a.ns.obj_mean[p * K + ok] = smean;
+            a.ns.obj_var[p * K + ok] = svar;
+            if (ok == 0) a.ns.obj_count[p] = scnt;
+        }
+    }
+    if (rlane) {
+        a.st.ret[p * NN + rn] = retv;
+        if (rn == 0) {
+            a.ns.ret_mean[p] = smean;
+            a.ns.ret_var[p] = svar;
+            a.ns.ret_count[p] = scnt;
+            a.st.obj_acc_valid[p] = obj_valid;
+        }
+    }
+}
+
+}  // namespace
+
+bool rollout_wide_supported(const pgm_dims* d) {
+    return d->O > 48 && d->O <= 2 * WTH && (d->N == 1 || d->N == 2 || d->N == 4 || d->N == 8) &&
+           d->N * d->K <= 16 && (d->K & (d->K - 1)) == 0;
+}
+
+template <int O, int A, int K, int NN>
+static int launch_wide_n(const pgm_dims* d, const RolloutArgs& a, hipStream_t s) {
+    auto kern = rollout_wide_kernel<O, A, K, NN>;
+    const size_t smem = sizeof(WideSmem<O, A, K, NN>);
+    if (smem > 160 * 1024) {
+        set_error("pgm_rollout: LDS image %zu bytes exceeds 160 KiB", smem);
+        return PGM_E_UNSUPPORTED;
+    }
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    if (e != hipSuccess) return hip_fail(e, "pgm_rollout");
+    hipLaunchKernelGGL(kern, dim3(d->P), dim3(WTH), smem, s, a);
+    if (int rc = launch_status("pgm_rollout")) return rc;
+    return launch_critic_values(d, a, s);
+}
+
+int launch_rollout_wide(const pgm_dims* d, const RolloutArgs& a, hipStream_t stream) {
+    return dispatch_dims(d->O, d->A, d->K, "pgm_rollout", [&](auto o, auto aa, auto k) -> int {
+        constexpr int O = decltype(o)::value, A = decltype(aa)::value, K = decltype(k)::value;
+        if constexpr (O <= 48 || O > 2 * WTH || (K & (K - 1)) != 0 || A > 32) {
+            set_error("pgm_rollout: obs_dim %d outside the wide rollout kernel", O);
+            return PGM_E_UNSUPPORTED;
+        } else {
+            switch (d->N) {
+                case 1: return launch_wide_n<O, A, K, 1>(d, a, stream);
+                case 2: return launch_wide_n<O, A, K, 2>(d, a, stream);
+                case 4: return launch_wide_n<O, A, K, 4>(d, a, stream);
+                case 8:
+                    if constexpr (8 * K <= 16) return launch_wide_n<O, A, K, 8>(d, a, stream);
+                    break;
+            }
+            set_error("pgm_rollout: N=%d outside the wide rollout kernel (1, 2, 4, 8 with N*K <= 16)", d->N);
+            return PGM_E_UNSUPPORTED;
+        }
+    });
+}
+
+}  // namespace pgm

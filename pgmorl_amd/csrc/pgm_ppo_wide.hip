@@ -2,26 +2,33 @@
 // cores.  Same semantics as pgm_ppo_mfma.hip (a2c_ppo_acktr/algo/ppo.py:58-115, storage.py:118-154,
 // model.py:75-82, distributions.py:29-40; torch min/max/clamp tie rules), different data placement:
 //
-//   * one 256-thread workgroup per tower (critic / actor), the two exchanging the squared gradient norm
-//     through one tagged granule per Adam step, as in the narrow kernel's MODE 1;
-//   * layer 1 (O x 64 = 96 KB for Humanoid) does not fit LDS next to the rest, so it stays in HBM / L2:
-//     the forward reads W1 with sc1 (L1-bypassing) buffer loads, double-buffered in registers 4 k-steps
-//     ahead; the minibatch rows are read straight from the rollout buffers (no packed table);
-//   * dW1 never goes through LDS: wave w owns the 32-feature tiles kt = w, w + 4, w + 8 of dW1 and keeps
-//     their running sums in a per-tower workspace slice that only the owning lane reads and writes; every
-//     wave's dZ1 tile is shared through its LDS transpose tile, so each wave contracts its feature tiles
-//     over ALL samples of the pass.  Clip and Adam read those sums back (moments in HBM); W1's sum of
-//     squares is a register reduction over them;
+//   * each tower (critic / actor) on NS workgroups (NS = 2 while the grid fits the CUs): each takes 1/NS of
+//     every minibatch's rows, in passes of 128 rows (one 32-row MFMA tile per wave); the NS gradient images
+//     are added through a 16-B sc1 publish + tagged flag hand-off (cdna_hip_programming.md G16 R1), both
+//     halves add them in the same order, so their Adam steps stay bitwise identical; the two towers exchange
+//     the squared gradient norm through one tagged granule per step (the narrow kernel's MODE 2 protocol);
+//   * layer 1 (O x 64 = 96 KB) does not fit LDS next to the rest: the forward streams W1 from L2 (sc1 buffer
+//     loads) and the observation rows straight from the rollout buffer (float4 per lane), both two 4-k-step
+//     groups ahead of the MFMAs.  Layer-1 k-steps pair features (h*KH + ks) of the two lane halves: any
+//     bijection between the MFMA's two k-slots and the features works as long as the A (X) and B (W1)
+//     operands use the same one;
+//   * dW1 stays in REGISTERS: wave w owns the 32-feature tiles kt = w, w + 4, w + 8 of dW1 (96 accumulator
+//     registers) for the whole minibatch; every wave's dZ1 tile is shared through its LDS transpose tile, so
+//     each wave contracts its feature tiles over ALL samples of a pass, the observation values gathered from
+//     HBM one (tile, feature-tile) ahead.  Clip and Adam read those registers directly (moments in HBM);
 //   * everything but layer 1 (W2, heads, biases, logstd) is an LDS "small image" with LDS-resident Adam
-//     moments, reduced / clipped / updated exactly like the narrow kernel's tower images.
-// Layer-1 k-steps pair features (h*KH + ks) of the two lane halves: any bijection between the MFMA's two
-// k-slots and the features works as long as the A (X) and B (W1) operands use the same one.
+//     moments, reduced / clipped / updated like the narrow kernel's tower images; the head-weight gradient
+//     is an MFMA with the per-sample head gradients transposed through LDS.
+// Half 1 of a tower updates a private copy of its task's parameters / moments (workspace), so neither half
+// ever reads layer-1 weights the other is rewriting; half 0 works on the caller's arrays.
 #include <stdlib.h>
 
 #include "pgm_dispatch.hpp"
 #include "pgm_mfma.hpp"
 
 namespace pgm {
+
+namespace {
 
 template <int A, int K>
 struct SmallImg {
@@ -64,27 +71,52 @@ struct WSmem {
     float aiv[A];          // actor 1 / std^2
     float red[16];
     int32_t rowid[4][TS];  // rollout rows of every wave's tile of the current pass
+    float act2[4][TS][SCR];  // per-wave tile B: H2, then dZ2
     union Big {            // per-wave transpose tiles (dZ1 shared at the pass end), gradient images after
         float scr[4][TS][SCR];
         float GA[2][IMG];
     } big;
 };
 
+constexpr int WSPLIT = 16;  // cache-policy aux bit of the buffer builtins: sc1
+
+// A per-lane base value the optimiser cannot see through: addresses derived from it stay base + constant
+// (one VGPR) instead of being hoisted out of the step loop as one precomputed VGPR per element.
+__device__ __forceinline__ int opaque(int v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+
 struct WArgs {
     int N, T, P;
     Layout L;
     pgm_ppo_hparams hp;
-    float *params, *m, *v;
+    float *params, *m, *v;  // caller's arrays (half 0)
+    float* copies;          // NS = 2: half 1's private [P][3][L] params | exp_avg | exp_avg_sq
     int32_t* step;
     const float* lr;
     const int32_t* perms;
     const float *obs, *actions, *logp, *adv, *values, *returns;
     float* stats;
-    unsigned long long* ws;  // [2P] tagged norm granules + timeout flag (word 2P), zeroed before the launch
-    float* dw1;              // [P][2][ceil(O/32)*32][H] layer-1 gradient running sums (workspace)
+    unsigned long long* ws;  // tagged norm granules + timeout flag (word 2P), zeroed before the launch
+    unsigned long long* xb;  // NS = 2: gradient exchange slots [P][2 towers][2 halves][2 parities][xslot]
+    int xslot;               // 8-byte words per exchange slot (image | dW1 | flag granule)
+    int xbytes;
 };
 
-template <int O, int A, int K>
+}  // namespace
+
+// exchange-slot geometry shared with the host-side workspace size (pgm_common.hpp declares it)
+int wide_xslot_words(int O, int A, int K) {
+    const int Q = A > K ? A : K;
+    const int img = H * (H + 1) + Q * H + 2 * H + Q + A;
+    const int nkt = (O + 31) / 32;
+    return ((img + nkt * 32 * H + 2) / 2 + 31) / 32 * 32;  // floats -> 8-byte words, 256-B aligned slots
+}
+
+namespace {
+
+template <int O, int A, int K, int NS>
 __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
     static_assert(O > 32 && O % 8 == 0, "wide kernel: obs_dim > 32, multiple of 8 (float4 halves)");
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -92,38 +124,43 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
     auto& S = *reinterpret_cast<Sm*>(smem_raw);
     constexpr int Q = qmax<A, K>();
     constexpr int IMG = Sm::IMG;
-    constexpr int KH = O / 2;                  // layer-1 k-steps: lane half h covers features [h*KH, h*KH + KH)
-    constexpr int KG = 4;                      // k-steps per register group (one float4 of X per lane)
+    constexpr int KH = O / 2;              // layer-1 k-steps: lane half h covers features [h*KH, h*KH + KH)
+    constexpr int KG = 4;                  // k-steps per group (one float4 of X per lane)
     constexpr int NG = KH / KG;
     static_assert(NG * KG == KH, "KH multiple of 4");
-    constexpr int NKT = (O + TS - 1) / TS;     // 32-feature tiles of dW1
-    constexpr int NKW = (NKT + 3) / 4;         // tiles owned per wave: kt = w + 4j
+    constexpr int NKT = (O + TS - 1) / TS;  // 32-feature tiles of dW1
+    constexpr int NKW = (NKT + 3) / 4;      // tiles owned per wave: kt = w + 4j
     constexpr int oWh = H * SCR, oB1 = oWh + Q * H, oB2 = oB1 + H, oBh = oB2 + H, oLs = oBh + Q;
     const int t = threadIdx.x, w = t >> 6, l = t & 63, h = l >> 5, c = l & 31;
-    const int p = (int)(blockIdx.x >> 1), m = (int)(blockIdx.x & 1);
+    // block map (NS = 2): in each group of 16 blocks, block r holds half r >> 3 of tower r & 1 of task
+    // 4g + ((r & 7) >> 1): the two halves of a tower are blocks b and b + 8 (speed only)
+    const int bx = (int)blockIdx.x;
+    const int p = NS == 2 ? 4 * (bx >> 4) + ((bx & 7) >> 1) : (bx >> 1);
+    const int hs = NS == 2 ? (bx >> 3) & 1 : 0;
+    if (p >= a.P) return;
+    const int m = bx & 1;
     const int NQ = m == 0 ? K : A;
     const int N = a.N, T = a.T, B = T * N;
     const int E = a.hp.ppo_epoch, M = a.hp.num_mini_batch;
     const int mb = B / M, nb = B / mb;
-    const int npass = (mb + 4 * TS - 1) / (4 * TS);
+    const int r0 = hs * mb / NS, mbs = (hs + 1) * mb / NS - r0;  // this workgroup's rows of each minibatch
+    const int npass = (mbs + 4 * TS - 1) / (4 * TS);
     const float clip = a.hp.clip_param;
     const Layout& L = a.L;
-    float* __restrict__ P = a.params + (size_t)p * L.total;
-    float* __restrict__ Mo = a.m + (size_t)p * L.total;
-    float* __restrict__ Vo = a.v + (size_t)p * L.total;
+    float* __restrict__ P = hs == 0 ? a.params + (size_t)p * L.total : a.copies + ((size_t)p * 3 + 0) * L.total;
+    float* __restrict__ Mo = hs == 0 ? a.m + (size_t)p * L.total : a.copies + ((size_t)p * 3 + 1) * L.total;
+    float* __restrict__ Vo = hs == 0 ? a.v + (size_t)p * L.total : a.copies + ((size_t)p * 3 + 2) * L.total;
     const int offW1 = L.off[m ? PGM_P_ACTOR_W1 : PGM_P_CRITIC_W1];
-    float* __restrict__ dw1 = a.dw1 + (size_t)(p * 2 + m) * NKT * TS * H;  // this tower's dW1 running sums
     const float* obs = a.obs + (size_t)p * (T + 1) * N * O;
     const float* acts = a.actions + (size_t)p * B * A;
     const float* oldlp = a.logp + (size_t)p * B;
     const float* advs = a.adv + (size_t)p * B;
     const float* vals = a.values + (size_t)p * (T + 1) * N * K;
     const float* rets = a.returns + (size_t)p * (T + 1) * N * K;
-    // this task's parameters as a buffer: layer-1 weights are re-read every tile with sc1 (L2) loads
+    // this workgroup's parameters as a buffer: layer-1 weights are re-read every tile with sc1 (L2) loads
     const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(P, 0, L.total * 4, 0x00020000);
-    constexpr int SC1 = 16;
-    auto w1 = [&](int k, int col) {  // W1^T[k][col] from L2
-        return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(prs, (offW1 + k * H + col) * 4, 0, SC1));
+    auto w1 = [&](int k, int col) {  // W1^T[k][col]
+        return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(prs, (offW1 + k * H + col) * 4, 0, WSPLIT));
     };
 
     // ---- small image + its Adam moments
@@ -147,21 +184,23 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
     float st_v = 0.f, st_a = 0.f, st_e = 0.f;
     int nstep = 0;
     double b1p = pow((double)b1c, (double)step0), b2p = pow((double)b2c, (double)step0);
-    float* scr = &S.big.scr[w][0][0];
+    float* scr = &S.big.scr[w][0][0];  // tile A: H1, then dZ1
+    float* scr2 = &S.act2[w][0][0];     // tile B: H2, then dZ2
 
     for (int e = 0; e < E; ++e) {
         for (int bb = 0; bb < nb; ++bb) {
-            const int32_t* perm = a.perms + (size_t)e * B + bb * mb;
-            f32x16 gW2[2][2];
-            float gWh[2][Q], gB1[2], gB2[2], gBh[Q], gLs[A];
+            const int32_t* perm = a.perms + (size_t)e * B + bb * mb + r0;
+            f32x16 gW2[2][2], gWh[2], dW1[NKW][2];
+            float gB1[2], gB2[2], gBh[Q], gLs[A];
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
 #pragma unroll
                 for (int j = 0; j < 2; ++j) gW2[i][j] = f32x16{0};
+                gWh[i] = f32x16{0};
                 gB1[i] = gB2[i] = 0.f;
-#pragma unroll
-                for (int q = 0; q < Q; ++q) gWh[i][q] = 0.f;
             }
+#pragma unroll
+            for (int j = 0; j < NKW; ++j) dW1[j][0] = dW1[j][1] = f32x16{0};
 #pragma unroll
             for (int q = 0; q < Q; ++q) gBh[q] = 0.f;
 #pragma unroll
@@ -171,58 +210,53 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
             for (int ps = 0; ps < npass; ++ps) {
                 const int i0 = (ps * 4 + w) * TS;  // this wave's tile of the pass
                 const int si = i0 + c;
-                const bool ok = si < mb;
-                const int row = perm[min(si, mb - 1)];
+                const bool ok = si < mbs;
+                const int row = perm[min(si, mbs - 1)];
                 if (h == 0) S.rowid[w][c] = row;
-                if (i0 < mb) {  // wave-uniform
-                    // ---- layer 1 from L2: Z1[s][u] = sum_k X[s][k] W1t[k][u], X row of sample c, features
-                    // h*KH + ks; register groups of KG k-steps loaded one group ahead
+                if (i0 < mbs) {  // wave-uniform
+                    // ---- layer 1: Z1[s][u] = sum_k X[s][k] W1t[k][u]; X row of sample c, features h*KH + ks;
+                    // groups of KG k-steps, two groups in flight ahead of the MFMAs (static ping-pong)
                     const float4* xr = reinterpret_cast<const float4*>(obs + (size_t)row * O + h * KH);
                     f32x16 z[2] = {f32x16{0}, f32x16{0}};
-                    float4 xa = xr[0];
-                    float wa[KG][2];
+                    float4 xa, xb;
+                    float wa[KG][2], wb[KG][2];
+                    auto load_group = [&](int g, float4& x, float (&wv)[KG][2]) {
+                        x = xr[g];
 #pragma unroll
-                    for (int q = 0; q < KG; ++q) {
-                        wa[q][0] = w1(h * KH + q, c);
-                        wa[q][1] = w1(h * KH + q, TS + c);
-                    }
+                        for (int q = 0; q < KG; ++q) {
+                            wv[q][0] = w1(h * KH + g * KG + q, c);
+                            wv[q][1] = w1(h * KH + g * KG + q, TS + c);
+                        }
+                    };
+                    auto mfma_group = [&](const float4& x, const float (&wv)[KG][2]) {
+                        const float xv[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+                        for (int q = 0; q < KG; ++q) {
+                            z[0] = mfma(xv[q], wv[q][0], z[0]);
+                            z[1] = mfma(xv[q], wv[q][1], z[1]);
+                        }
+                    };
+                    load_group(0, xa, wa);
+                    if (NG > 1) load_group(1, xb, wb);
 #pragma unroll 1
-                    for (int g = 0; g < NG; ++g) {
-                        float4 xn = xa;
-                        float wn[KG][2];
+                    for (int g = 0; g < NG; g += 2) {
+                        mfma_group(xa, wa);
+                        if (g + 2 < NG) load_group(g + 2, xa, wa);
                         if (g + 1 < NG) {
-                            xn = xr[g + 1];
-#pragma unroll
-                            for (int q = 0; q < KG; ++q) {
-                                wn[q][0] = w1(h * KH + (g + 1) * KG + q, c);
-                                wn[q][1] = w1(h * KH + (g + 1) * KG + q, TS + c);
-                            }
-                        }
-                        const float xv[4] = {xa.x, xa.y, xa.z, xa.w};
-#pragma unroll
-                        for (int q = 0; q < KG; ++q) {
-                            z[0] = mfma(xv[q], wa[q][0], z[0]);
-                            z[1] = mfma(xv[q], wa[q][1], z[1]);
-                        }
-                        xa = xn;
-#pragma unroll
-                        for (int q = 0; q < KG; ++q) {
-                            wa[q][0] = wn[q][0];
-                            wa[q][1] = wn[q][1];
+                            mfma_group(xb, wb);
+                            if (g + 3 < NG) load_group(g + 3, xb, wb);
                         }
                     }
-                    f32x16 H1[2];
+                    // activations live in two per-wave LDS tiles, not registers (the 230 accumulator registers
+                    // leave no room): tile A = H1 (later dZ1), tile B = H2 (later dZ2)
 #pragma unroll
                     for (int hb = 0; hb < 2; ++hb) {
                         const float bias = W.b1[hb * TS + c];
 #pragma unroll
-                        for (int r = 0; r < 16; ++r) {
-                            H1[hb][r] = tanh_fast(z[hb][r] + bias);
-                            scr[rowof(r, h) * SCR + hb * TS + c] = H1[hb][r];
-                        }
+                        for (int r = 0; r < 16; ++r) scr[rowof(r, h) * SCR + hb * TS + c] = tanh_fast(z[hb][r] + bias);
                     }
                     wave_lds_fence();
-                    // ---- layer 2 (A from the transpose tile)
+                    // ---- layer 2 (A from tile A, transposed)
                     z[0] = z[1] = f32x16{0};
 #pragma unroll 8
                     for (int ks = 0; ks < H / 2; ++ks) {
@@ -231,18 +265,12 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
 #pragma unroll
                         for (int ob = 0; ob < 2; ++ob) z[ob] = mfma(av, W.W2t[k][ob * TS + c], z[ob]);
                     }
-                    f32x16 H2[2];
 #pragma unroll
                     for (int ob = 0; ob < 2; ++ob) {
                         const float bias = W.b2[ob * TS + c];
 #pragma unroll
-                        for (int r = 0; r < 16; ++r) H2[ob][r] = tanh_fast(z[ob][r] + bias);
+                        for (int r = 0; r < 16; ++r) scr2[rowof(r, h) * SCR + ob * TS + c] = tanh_fast(z[ob][r] + bias);
                     }
-                    wave_lds_fence();
-#pragma unroll
-                    for (int ob = 0; ob < 2; ++ob)
-#pragma unroll
-                        for (int r = 0; r < 16; ++r) scr[rowof(r, h) * SCR + ob * TS + c] = H2[ob][r];
                     wave_lds_fence();
                     // ---- heads (VALU): lane = sample c, half h sums units [32h, 32h+32)
                     float outv[Q];
@@ -250,7 +278,7 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
                     for (int q = 0; q < Q; ++q) outv[q] = 0.f;
 #pragma unroll 4
                     for (int u = 0; u < TS; ++u) {
-                        const float hv = scr[c * SCR + h * TS + u];
+                        const float hv = scr2[c * SCR + h * TS + u];
 #pragma unroll
                         for (int q = 0; q < Q; ++q) outv[q] = fmaf(hv, W.Wh[q][h * TS + u], outv[q]);
                     }
@@ -281,14 +309,11 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
                         }
                         if (ok && h == 0) lsum += ls;
                     } else {  // clipped surrogate
-                        float act[A];
-#pragma unroll
-                        for (int q = 0; q < A; ++q) act[q] = acts[(size_t)row * A + q];
                         const float lpo = oldlp[row], ad = advs[row];
                         float lp = 0.f;
 #pragma unroll
                         for (int q = 0; q < A; ++q) {
-                            const float diff = act[q] - outv[q];
+                            const float diff = acts[(size_t)row * A + q] - outv[q];
                             lp += -0.5f * diff * diff * S.aiv[q] - lstd[q] - LOG_SQRT_2PI;
                         }
                         const float ratio = expf(lp - lpo);
@@ -300,7 +325,7 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
                         if (ok && h == 0) lsum += -fminf(s1, s2);
 #pragma unroll
                         for (int q = 0; q < A; ++q) {
-                            const float diff = act[q] - outv[q];
+                            const float diff = acts[(size_t)row * A + q] - outv[q];
                             const float iv = S.aiv[q];
                             dO[q] = dlp * diff * iv;
                             if (h == 0) gLs[q] += dlp * (diff * diff * iv - 1.f);
@@ -314,21 +339,15 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
                         }
                     }
                     wave_lds_fence();
-                    // ---- head-weight grads (VALU, C layout); one dO row per register, scheduling fences keep the
-                    // Q-wide row loads from being hoisted (Q = 17 would not fit the register file)
+                    // ---- head-weight grads on the MFMA: gWh^T[u][q] += sum_s H2[s][u] dO[s][q]
+                    // (A = H2 in the C layout from tile B: lane u, samples rowof(r, 0/1); B = dO, lane q)
 #pragma unroll
                     for (int r = 0; r < 16; ++r) {
-                        const int s = rowof(r, h);
-                        float dv[Q];
+                        const float bq = c < Q ? S.dout[w][rowof(r, h)][c < Q ? c : 0] : 0.f;
 #pragma unroll
-                        for (int q = 0; q < Q; ++q) dv[q] = S.dout[w][s][q];
-#pragma unroll
-                        for (int ob = 0; ob < 2; ++ob)
-#pragma unroll
-                            for (int q = 0; q < Q; ++q) gWh[ob][q] = fmaf(H2[ob][r], dv[q], gWh[ob][q]);
-                        __builtin_amdgcn_sched_barrier(0);
+                        for (int ob = 0; ob < 2; ++ob) gWh[ob] = mfma(scr2[rowof(r, h) * SCR + ob * TS + c], bq, gWh[ob]);
                     }
-                    // ---- dH2 = dO . Wh (MFMA) -> dZ2; dW2^T += H1^T dZ2
+                    // ---- dH2 = dO . Wh (MFMA) -> dZ2 (H2 from tile B); dW2^T += H1^T dZ2 (H1 from tile A)
                     z[0] = z[1] = f32x16{0};
 #pragma unroll
                     for (int ks = 0; ks < (Q + 1) / 2; ++ks) {
@@ -342,27 +361,30 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
                     for (int ob = 0; ob < 2; ++ob)
 #pragma unroll
                         for (int r = 0; r < 16; ++r) {
-                            dZ2[ob][r] = z[ob][r] * (1.f - H2[ob][r] * H2[ob][r]);
+                            const float h2 = scr2[rowof(r, h) * SCR + ob * TS + c];
+                            dZ2[ob][r] = z[ob][r] * (1.f - h2 * h2);
                             gB2[ob] += dZ2[ob][r];
                         }
 #pragma unroll
                     for (int r = 0; r < 16; ++r)
 #pragma unroll
-                        for (int ib = 0; ib < 2; ++ib)
+                        for (int ib = 0; ib < 2; ++ib) {
+                            const float h1 = scr[rowof(r, h) * SCR + ib * TS + c];
 #pragma unroll
-                            for (int ob = 0; ob < 2; ++ob) gW2[ib][ob] = mfma(H1[ib][r], dZ2[ob][r], gW2[ib][ob]);
-                    // ---- dH1 = dZ2 W2 -> dZ1
-                    wave_lds_fence();
+                            for (int ob = 0; ob < 2; ++ob) gW2[ib][ob] = mfma(h1, dZ2[ob][r], gW2[ib][ob]);
+                        }
+                    // ---- dH1 = dZ2 W2 -> dZ1 (dZ2 through tile B, transposed)
+                    wave_lds_fence();  // every H2 read of tile B returned before the overwrite
 #pragma unroll
                     for (int ob = 0; ob < 2; ++ob)
 #pragma unroll
-                        for (int r = 0; r < 16; ++r) scr[rowof(r, h) * SCR + ob * TS + c] = dZ2[ob][r];
+                        for (int r = 0; r < 16; ++r) scr2[rowof(r, h) * SCR + ob * TS + c] = dZ2[ob][r];
                     wave_lds_fence();
                     z[0] = z[1] = f32x16{0};
 #pragma unroll 8
                     for (int ks = 0; ks < H / 2; ++ks) {
                         const int k = 2 * ks + h;
-                        const float av = scr[c * SCR + k];
+                        const float av = scr2[c * SCR + k];
 #pragma unroll
                         for (int ib = 0; ib < 2; ++ib) z[ib] = mfma(av, W.W2t[ib * TS + c][k], z[ib]);
                     }
@@ -371,10 +393,11 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
                     for (int ib = 0; ib < 2; ++ib)
 #pragma unroll
                         for (int r = 0; r < 16; ++r) {
-                            dZ1[ib][r] = z[ib][r] * (1.f - H1[ib][r] * H1[ib][r]);
+                            const float h1 = scr[rowof(r, h) * SCR + ib * TS + c];
+                            dZ1[ib][r] = z[ib][r] * (1.f - h1 * h1);
                             gB1[ib] += dZ1[ib][r];
                         }
-                    // ---- dZ1 to this wave's transpose tile: every wave contracts it with its dW1 tiles
+                    // ---- dZ1 to tile A: every wave contracts it with its dW1 tiles
                     wave_lds_fence();
 #pragma unroll
                     for (int ib = 0; ib < 2; ++ib)
@@ -382,44 +405,37 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
                         for (int r = 0; r < 16; ++r) scr[rowof(r, h) * SCR + ib * TS + c] = dZ1[ib][r];
                 }
                 lds_sync_m();  // every tile's dZ1 and rows visible
-                // ---- dW1^T[k][u] += X^T dZ1 over the pass's tiles, for this wave's feature tiles.  The running
-                // sums live in the workspace (each element read and written only by its owning lane), one
-                // 32-feature tile in registers at a time
+                // ---- dW1^T[k][u] += X^T dZ1 over the pass's tiles for this wave's feature tiles; the X values
+                // of (tile u, feature tile kt) are gathered from HBM one round ahead (rows of the tile)
                 {
-                    int rw[4][16];
+                    const int nu = min(4, (mbs - ps * 4 * TS + TS - 1) / TS);  // tiles of this pass
+                    constexpr int NR = NKW * 4;                                // rounds (j, u)
+                    auto gather = [&](int rd, float (&xv)[16]) {
+                        const int j = rd >> 2, u = rd & 3, kf = (w + 4 * j) * TS + c;
+                        const bool live = u < nu && kf < O;
 #pragma unroll
-                    for (int u = 0; u < 4; ++u)
+                        for (int r = 0; r < 16; ++r) {
+                            const int rr = S.rowid[u][rowof(r, h)];
+                            xv[r] = live ? obs[(size_t)rr * O + kf] : 0.f;
+                        }
+                    };
+                    float xa[16], xb[16];
+                    gather(0, xa);
 #pragma unroll
-                        for (int r = 0; r < 16; ++r) rw[u][r] = S.rowid[u][rowof(r, h)];
-                    const int nu = min(4, (mb - ps * 4 * TS + TS - 1) / TS);  // tiles of this pass
-#pragma unroll 1
-                    for (int j = 0; j < NKW; ++j) {
-                        const int kt = w + 4 * j;
-                        if (kt >= NKT) break;
-                        const int kf = kt * TS + c;
-                        float* gp = dw1 + (size_t)(kt * TS) * H + c;
-                        f32x16 acc[2];
-#pragma unroll
-                        for (int ib = 0; ib < 2; ++ib)
-#pragma unroll
-                            for (int r = 0; r < 16; ++r) acc[ib][r] = ps == 0 ? 0.f : gp[rowof(r, h) * H + ib * TS];
-#pragma unroll 1
-                        for (int u = 0; u < nu; ++u) {
+                    for (int rd = 0; rd < NR; ++rd) {
+                        float(&cur)[16] = (rd & 1) ? xb : xa;
+                        float(&nxt)[16] = (rd & 1) ? xa : xb;
+                        if (rd + 1 < NR) gather(rd + 1, nxt);
+                        const int j = rd >> 2, u = rd & 3;
+                        if (u < nu && w + 4 * j < NKT) {
                             const float* dz = &S.big.scr[u][0][0];
-                            float xv[16];
-#pragma unroll
-                            for (int r = 0; r < 16; ++r) xv[r] = kf < O ? obs[(size_t)rw[u][r] * O + kf] : 0.f;
 #pragma unroll
                             for (int r = 0; r < 16; ++r) {
                                 const int s = rowof(r, h);
 #pragma unroll
-                                for (int ib = 0; ib < 2; ++ib) acc[ib] = mfma(xv[r], dz[s * SCR + ib * TS + c], acc[ib]);
+                                for (int ib = 0; ib < 2; ++ib) dW1[j][ib] = mfma(cur[r], dz[s * SCR + ib * TS + c], dW1[j][ib]);
                             }
                         }
-#pragma unroll
-                        for (int ib = 0; ib < 2; ++ib)
-#pragma unroll
-                            for (int r = 0; r < 16; ++r) gp[rowof(r, h) * H + ib * TS] = acc[ib][r];
                     }
                 }
                 lds_sync_m();  // transpose tiles / row ids reused by the next pass
@@ -430,8 +446,6 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
             for (int i = 0; i < 2; ++i) {
                 gB1[i] = half_sum(gB1[i]);
                 gB2[i] = half_sum(gB2[i]);
-#pragma unroll
-                for (int q = 0; q < Q; ++q) gWh[i][q] = half_sum(gWh[i][q]);
             }
 #pragma unroll
             for (int q = 0; q < Q; ++q) gBh[q] = wave_sum64(gBh[q]);
@@ -465,13 +479,17 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
 #pragma unroll
                         for (int ob = 0; ob < 2; ++ob)
                             acc16([&](int r) { return (ib * TS + rowof(r, h)) * SCR + ob * TS + c; }, gW2[ib][ob]);
+                    // head weights: gWh[ob] row rowof(r,h) = unit ob*32 + rowof, column c = output q (c < Q)
+                    if (c < Q) {
+#pragma unroll
+                        for (int ob = 0; ob < 2; ++ob)
+                            acc16([&](int r) { return oWh + c * H + ob * TS + rowof(r, h); }, gWh[ob]);
+                    }
                     if (h == 0) {
 #pragma unroll
                         for (int i = 0; i < 2; ++i) {
                             acc(oB1 + i * TS + c, gB1[i]);
                             acc(oB2 + i * TS + c, gB2[i]);
-#pragma unroll
-                            for (int q = 0; q < Q; ++q) acc(oWh + q * H + i * TS + c, q < NQ ? gWh[i][q] : 0.f);
                         }
                     }
                     if (l == 0) {
@@ -493,33 +511,125 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
                 }
                 lds_sync_m();
             }
-            // ---- clip_grad_norm_: small image + this wave's dW1 registers
-            const float* GA0 = S.big.GA[0];
-            const float* GA1 = S.big.GA[1];
-            float sq = 0.f;
-            for (int i = t; i < IMG; i += MT) {
-                const float g = GA0[i] + GA1[i];
-                sq = fmaf(g, g, sq);
+            // head rows q >= NQ (critic: 2..16) are exactly zero: dO[q] = 0 for them
+            float* G0 = S.big.GA[0];
+            const float* G1 = S.big.GA[1];
+            const float lsum_wg = (S.red[8] + S.red[9]) + (S.red[10] + S.red[11]);
+            float lsum_task = lsum_wg;
+            if constexpr (NS == 2) {
+                // ---- add the other half's gradients (small image + this wave's dW1 registers): 16-B sc1 stores
+                // of G0 + G1 and 4-B sc1 stores of the dW1 registers, every wave drains, barrier, one lane stores
+                // the tagged flag granule {step, loss sum}; then one lane polls the partner's flag, barrier, sc1
+                // loads.  Both halves add half0 + half1 in that order (bitwise identical Adam steps).  Slots are
+                // double-buffered by step parity.
+                const unsigned tag = (unsigned)(nstep + 1);
+                const int par = nstep & 1;
+                const int slot_mine = ((p * 2 + m) * 2 + hs) * 2 + par;
+                const int slot_other = ((p * 2 + m) * 2 + (1 - hs)) * 2 + par;
+                const int off_mine = slot_mine * a.xslot * 8, off_other = slot_other * a.xslot * 8;
+                const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(a.xb, 0, a.xbytes, 0x00020000);
+                constexpr int NV4 = IMG / 4, TAIL = IMG - 4 * NV4;
+                constexpr int DW = IMG * 4;  // byte offset of the dW1 block inside a slot
+                for (int i = t; i < NV4; i += MT) {
+                    u32x4 v;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const float g = G0[4 * i + q] + G1[4 * i + q];
+                        G0[4 * i + q] = g;
+                        v[q] = __float_as_uint(g);
+                    }
+                    __builtin_amdgcn_raw_buffer_store_b128(v, xr, off_mine + 16 * i, 0, WSPLIT);
+                }
+                if (t < TAIL) {
+                    const float g = G0[4 * NV4 + t] + G1[4 * NV4 + t];
+                    G0[4 * NV4 + t] = g;
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(g), xr, off_mine + 16 * NV4 + 4 * t, 0, WSPLIT);
+                }
+                const int dwb = opaque(4 * ((w * TS + 4 * h) * H + c));  // lane base of its dW1 elements
+#pragma unroll
+                for (int j = 0; j < NKW; ++j)
+#pragma unroll
+                    for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) {
+                            const int cidx = (4 * j * TS + (r & 3) + 8 * (r >> 2)) * H + ib * TS;
+                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dW1[j][ib][r]), xr, dwb,
+                                                                  off_mine + DW + 4 * cidx, WSPLIT);
+                        }
+                __builtin_amdgcn_sched_barrier(0);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                lds_sync_m();
+                if (t == 0) {
+                    unsigned long long* flag_mine = a.xb + (size_t)slot_mine * a.xslot + a.xslot - 1;
+                    const unsigned long long* flag_other = a.xb + (size_t)slot_other * a.xslot + a.xslot - 1;
+                    __hip_atomic_store(flag_mine, ((unsigned long long)tag << 32) | __float_as_uint(lsum_wg),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    unsigned long long x = 0;
+                    for (unsigned spins = 0;; ++spins) {
+                        x = __hip_atomic_load(flag_other, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if ((unsigned)(x >> 32) == tag) break;
+                        if (spins > (1u << 26)) {  // partner never arrived: flag the launch as failed
+                            __hip_atomic_store(a.ws + 2 * a.P, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            x = 0;
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                    const float lo = __uint_as_float((unsigned)x);
+                    S.red[12] = hs == 0 ? lsum_wg + lo : lo + lsum_wg;
+                }
+                lds_sync_m();  // the polling lane matched: every wave may load the partner's gradients
+                for (int i = t; i < NV4; i += MT) {
+                    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(xr, off_other + 16 * i, 0, WSPLIT);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const float ov = __uint_as_float(v[q]);
+                        G0[4 * i + q] = hs == 0 ? G0[4 * i + q] + ov : ov + G0[4 * i + q];
+                    }
+                }
+                if (t < TAIL) {
+                    const float ov = __uint_as_float(
+                        __builtin_amdgcn_raw_buffer_load_b32(xr, off_other + 16 * NV4 + 4 * t, 0, WSPLIT));
+                    G0[4 * NV4 + t] = hs == 0 ? G0[4 * NV4 + t] + ov : ov + G0[4 * NV4 + t];
+                }
+                const int dwo = opaque(4 * ((w * TS + 4 * h) * H + c));
+#pragma unroll
+                for (int j = 0; j < NKW; ++j)
+#pragma unroll
+                    for (int ib = 0; ib < 2; ++ib) {
+                        float ov[16];
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) {
+                            const int cidx = (4 * j * TS + (r & 3) + 8 * (r >> 2)) * H + ib * TS;
+                            ov[r] = __uint_as_float(
+                                __builtin_amdgcn_raw_buffer_load_b32(xr, dwo, off_other + DW + 4 * cidx, WSPLIT));
+                        }
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) dW1[j][ib][r] = hs == 0 ? dW1[j][ib][r] + ov[r] : ov[r] + dW1[j][ib][r];
+                        __builtin_amdgcn_sched_barrier(0);  // one 16-load block in flight at a time
+                    }
+                lds_sync_m();
+                lsum_task = S.red[12];
+            } else {
+                for (int i = t; i < IMG; i += MT) G0[i] = G0[i] + G1[i];
+                lds_sync_m();
             }
-            for (int j = 0; j < NKW; ++j) {  // this wave's dW1 tiles (rows k >= O hold zeros)
-                const int kt = w + 4 * j;
-                if (kt >= NKT) break;
-                const float* gp = dw1 + (size_t)(kt * TS) * H + c;
+            // ---- clip_grad_norm_: small image + this wave's dW1 registers (rows k >= O hold zeros)
+            float sq = 0.f;
+            for (int i = t; i < IMG; i += MT) sq = fmaf(G0[i], G0[i], sq);
+#pragma unroll
+            for (int j = 0; j < NKW; ++j)
 #pragma unroll
                 for (int ib = 0; ib < 2; ++ib)
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const float g = gp[rowof(r, h) * H + ib * TS];
-                        sq = fmaf(g, g, sq);
-                    }
-            }
+                    for (int r = 0; r < 16; ++r) sq = fmaf(dW1[j][ib][r], dW1[j][ib][r], sq);
             sq = wave_sum64(sq);
             if (l == 0) S.red[w] = sq;
             lds_sync_m();
             float total = (S.red[0] + S.red[1]) + (S.red[2] + S.red[3]);
-            if (t == 0) {  // tagged 8-byte granule hand-off with the other tower's workgroup
+            if (t == 0) {  // tagged 8-byte granule hand-off with the other tower's workgroup (same half)
                 const unsigned tag = (unsigned)(nstep + 1);
-                unsigned long long* ws = a.ws + 2 * p;
+                unsigned long long* ws = a.ws + (hs == 0 ? 2 * p : 2 * a.P + 1 + 2 * p);
                 __hip_atomic_store(ws + m, ((unsigned long long)tag << 32) | __float_as_uint(total), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
                 unsigned long long x = 0;
@@ -541,9 +651,8 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
             total = S.red[4];
             const float coef = fminf(a.hp.max_grad_norm / (sqrtf(total) + 1e-6f), 1.f);
             if (t == 0) {
-                const float ls = (S.red[8] + S.red[9]) + (S.red[10] + S.red[11]);
-                if (m == 0) st_v += 0.5f * ls / (float)(mb * K);
-                else st_a += ls / (float)mb;
+                if (m == 0) st_v += 0.5f * lsum_task / (float)(mb * K);
+                else st_a += lsum_task / (float)mb;
                 st_e += ent;
             }
             // ---- Adam: the small image in LDS, layer 1 from the owning wave's registers (moments in HBM)
@@ -561,46 +670,49 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
             };
             for (int i = t; i < IMG; i += MT) {
                 float mm = S.MV[i], vv = S.MV[IMG + i], pp = Pf[i];
-                adam(GA0[i] + GA1[i], mm, vv, pp);
+                adam(G0[i], mm, vv, pp);
                 S.MV[i] = mm;
                 S.MV[IMG + i] = vv;
                 Pf[i] = pp;
                 if (m == 1 && i >= oLs && i < oLs + A) S.aiv[i - oLs] = expf(-2.f * pp);
             }
+            {
+                // layer 1 rows k = (w + 4j)*32 + rowof(r, h) of this lane (column ib*32 + c): lane base + constant
+                const int kb = opaque(w * TS + 4 * h);
+                const int fb = opaque(offW1 + kb * H + c);
 #pragma unroll
-            for (int j = 0; j < NKW; ++j) {
-                const int kt = w + 4 * j;
-                if (kt >= NKT) break;
-                const float* gp = dw1 + (size_t)(kt * TS) * H + c;
+                for (int j = 0; j < NKW; ++j) {
+                    if (w + 4 * j >= NKT) break;
 #pragma unroll
-                for (int ib = 0; ib < 2; ++ib) {
-                    float mm[16], vv[16], pp[16], gg[16];
+                    for (int ib = 0; ib < 2; ++ib) {
+                        float mm[16], vv[16], pp[16];
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const int k = min(kt * TS + rowof(r, h), O - 1);
-                        const int f = offW1 + k * H + ib * TS + c;
-                        mm[r] = Mo[f];
-                        vv[r] = Vo[f];
-                        pp[r] = P[f];
-                        gg[r] = gp[rowof(r, h) * H + ib * TS];
+                        for (int r = 0; r < 16; ++r) {
+                            const int kr = 4 * j * TS + (r & 3) + 8 * (r >> 2);  // k - kb
+                            const int f = kb + kr < O ? fb + kr * H + ib * TS : offW1;
+                            mm[r] = Mo[f];
+                            vv[r] = Vo[f];
+                            pp[r] = P[f];
+                        }
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) {
+                            const int kr = 4 * j * TS + (r & 3) + 8 * (r >> 2);
+                            if (kb + kr >= O) continue;
+                            const int f = fb + kr * H + ib * TS;
+                            adam(dW1[j][ib][r], mm[r], vv[r], pp[r]);
+                            Mo[f] = mm[r];
+                            Vo[f] = vv[r];
+                            P[f] = pp[r];
+                        }
+                        __builtin_amdgcn_sched_barrier(0);  // one 48-load block in flight at a time
                     }
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const int k = kt * TS + rowof(r, h);
-                        if (k >= O) continue;
-                        const int f = offW1 + k * H + ib * TS + c;
-                        adam(gg[r], mm[r], vv[r], pp[r]);
-                        Mo[f] = mm[r];
-                        Vo[f] = vv[r];
-                        P[f] = pp[r];
-                    }
-                    __builtin_amdgcn_sched_barrier(0);  // one 16-element block of loads in flight at a time
                 }
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // layer-1 stores land in L2 before any re-read
             lds_sync_m();
         }  // minibatches
     }      // epochs
+    if (hs != 0) return;  // half 1 worked on copies
     // ---- write back the small image (layer 1 was updated in place)
     for (int i = t; i < IMG; i += MT) {
         const int f = simg_to_flat<A, K>(i, m, L);
@@ -620,6 +732,8 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
     }
 }
 
+}  // namespace
+
 int ppo_update_wide(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params, float* adam_m, float* adam_v,
                     int32_t* adam_step, const float* lr, const int32_t* perms, const pgm_rollout_buf* rb, float* stats,
                     void* workspace, hipStream_t stream) {
@@ -627,13 +741,35 @@ int ppo_update_wide(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params,
         set_error("pgm_ppo_update: the wide update needs the workspace (pgm_ppo_update_workspace_bytes)");
         return PGM_E_INVALID_ARG;
     }
-    if (2 * d->P > device_cu_count()) {
+    // NS = 2 (each tower on two CUs) while the 16-block groups fit the CU count; PGM_UPDATE_SPLIT=1 caps it
+    const char* sel = getenv("PGM_UPDATE_SPLIT");
+    const int cap = sel && sel[0] >= '0' && sel[0] <= '2' ? sel[0] - '0' : 2;
+    const int cus = device_cu_count();
+    const int ns = cap >= 2 && 16 * ((d->P + 3) / 4) <= cus ? 2 : 1;
+    if (ns == 1 && 2 * d->P > cus) {
         set_error("pgm_ppo_update: the wide update needs 2P <= CUs (P=%d); shard the tasks over more GPUs", d->P);
         return PGM_E_UNSUPPORTED;
     }
-    WArgs a{d->N, d->T, d->P, make_layout(d->O, d->A, d->K, d->H), *hp, params, adam_m, adam_v, adam_step, lr, perms,
-            rb->obs, rb->actions, rb->logp, rb->adv, rb->values, rb->returns, stats, (unsigned long long*)workspace,
-            (float*)((char*)workspace + ppo_flag_bytes(d->P))};
+    const Layout L = make_layout(d->O, d->A, d->K, d->H);
+    char* ws = (char*)workspace;
+    const size_t flags = ppo_flag_bytes(d->P);
+    const int xslot = wide_xslot_words(d->O, d->A, d->K);
+    const size_t xbytes = (size_t)d->P * 8 * xslot * 8;
+    float* copies = (float*)(ws + flags + xbytes);
+    WArgs a{d->N, d->T, d->P, L, *hp, params, adam_m, adam_v, copies, adam_step, lr, perms,
+            rb->obs, rb->actions, rb->logp, rb->adv, rb->values, rb->returns, stats, (unsigned long long*)ws,
+            (unsigned long long*)(ws + flags), xslot, (int)xbytes};
+    hipError_t e = hipMemsetAsync(workspace, 0, flags + (ns == 2 ? xbytes : 0), stream);
+    if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update (workspace reset)");
+    if (ns == 2) {  // half 1's private copies of every task's parameters / moments
+        const size_t row = (size_t)L.total * sizeof(float);
+        for (int k = 0; k < 3; ++k) {
+            const float* src = k == 0 ? params : k == 1 ? adam_m : adam_v;
+            e = hipMemcpy2DAsync(copies + (size_t)k * L.total, 3 * row, src, row, row, d->P, hipMemcpyDeviceToDevice,
+                                 stream);
+            if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update (half copies)");
+        }
+    }
     return dispatch_dims(d->O, d->A, d->K, "pgm_ppo_update", [&](auto o, auto aa, auto k) -> int {
         constexpr int O = decltype(o)::value, A = decltype(aa)::value, K = decltype(k)::value;
         if constexpr (O <= 32 || O % 8 != 0) {
@@ -646,13 +782,15 @@ int ppo_update_wide(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params,
                 set_error("pgm_ppo_update: LDS image %zu bytes exceeds 160 KiB", smem);
                 return PGM_E_UNSUPPORTED;
             }
-            auto kern = ppo_update_wide_kernel<O, A, K>;
-            hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-            if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update");
-            e = hipMemsetAsync(workspace, 0, ppo_flag_bytes(d->P), stream);
-            if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update (workspace reset)");
-            hipLaunchKernelGGL(kern, dim3(2 * d->P), dim3(MT), smem, stream, a);
-            return launch_status("pgm_ppo_update");
+            auto launch = [&](auto kern, int grid) -> int {
+                hipError_t e2 = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                    (int)smem);
+                if (e2 != hipSuccess) return hip_fail(e2, "pgm_ppo_update");
+                hipLaunchKernelGGL(kern, dim3(grid), dim3(MT), smem, stream, a);
+                return launch_status("pgm_ppo_update");
+            };
+            if (ns == 2) return launch(ppo_update_wide_kernel<O, A, K, 2>, 16 * ((d->P + 3) / 4));
+            return launch(ppo_update_wide_kernel<O, A, K, 1>, 2 * d->P);
         }
     });
 }

@@ -43,6 +43,7 @@ def parse():
     ap.add_argument('--num-mini-batch', type=int, default=32)
     ap.add_argument('--cpu-iters', type=int, default=10, help='oracle iterations timed for cpu_baseline')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-overlap-eval', action='store_true', help='evaluate on the main stream (A/B)')
     ap.add_argument('--traffic-file', default=os.path.join(ROOT, 'profiles', 'r01_ppo_update_pmc.json'))
     return ap.parse_args()
 
@@ -135,12 +136,15 @@ def main():
     history = []  # every iteration's gathered objective vectors (the offspring the EP is built from)
 
     def step(j):
-        tb.iteration(j, 3e-4 * (1 - j / total_updates), carry=True)
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, tb.objs)
-        else:
-            gathered.copy_(tb.objs)
-        history.append(gathered.clone())
+        # the evaluation of iteration j runs on the side stream beside iteration j+1's rollout; the objective
+        # vectors are gathered on that stream behind it
+        tb.iteration(j, 3e-4 * (1 - j / total_updates), carry=True, overlap_eval=not args.no_overlap_eval)
+        with torch.cuda.stream(tb.eval_stream if not args.no_overlap_eval else torch.cuda.current_stream()):
+            if world > 1:
+                dist.all_gather_into_tensor(gathered, tb.objs)
+            else:
+                gathered.copy_(tb.objs)
+            history.append(gathered.clone())
 
     j = 0
     for _ in range(args.warmup):

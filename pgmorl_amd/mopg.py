@@ -133,19 +133,24 @@ class MOPGPopulation:
             for p, task in enumerate(task_batch[lo:hi]):
                 self.load_task(tb, p, task.sample, task.scalarization.weights.numpy())
             tb.env_reset()  # envs are re-created and reset every generation (mopg.py:67-82)
+            objs_i = []  # each iteration's evaluation output (written on the overlapped eval stream)
             for i, j in enumerate(its):
                 lr = linear_lr(j, total, a.lr, a.lr_decay_ratio) if a.use_linear_lr_decay else a.lr
                 noise = perms = None
                 if self.rng == 'host':
                     noise, perms = host_draws(j, a.num_steps, a.num_processes, tb.A, a.ppo_epoch)
-                tb.iteration(j, lr, noise=noise, perms=perms, carry=i > 0)
+                objs_i.append(torch.empty(Pl, tb.K, dtype=torch.float64, device=self.device))
+                tb.iteration(j, lr, noise=noise, perms=perms, carry=i > 0, overlap_eval=True, objs_out=objs_i[-1])
                 snaps32.append(torch.stack([tb.params, tb.adam_m, tb.adam_v], 1))  # [Pl, 3, L] (a copy)
-                recs.append(self._records(tb))
+                recs.append(self._records(tb))  # objs columns filled from objs_i below
                 if rank == 0 and a.rl_log_interval > 0 and (j + 1) % a.rl_log_interval == 0:
                     steps = (j + 1) * a.num_processes * a.num_steps
                     dt = time.time() - start_time
                     log(f'[RL] Updates {j + 1}, num timesteps {steps}, FPS {int(steps / max(dt, 1e-9))}, '
                         f'time {dt:.2f} seconds (x{P} tasks on {ws} device(s))')
+            tb.wait_eval()
+            for rec, ob in zip(recs, objs_i):
+                rec[:, :tb.K] = ob
         probe = self._batch(1) if tb is None else tb
         L, O, K = probe.layout.total, probe.O, probe.K
         if snaps32:

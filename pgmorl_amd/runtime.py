@@ -82,6 +82,8 @@ class TaskBatch:
                              use_clipped_value_loss=int(use_clipped_value_loss))
         self.reset_stats()
         self._build_structs()
+        self._eval_stream, self._eval_done = None, None
+        self._eval_mean, self._eval_var = z(P, O, dt=F64), z(P, O, dt=F64)
         nws = lib().pgm_ppo_update_workspace_bytes(C.byref(self.dims))
         self.update_ws = torch.zeros((nws + 7) // 8, dtype=torch.int64, device=self.dev)
 
@@ -174,19 +176,38 @@ class TaskBatch:
                                    C.byref(self.c_rb), _ptr(self.stats), _ptr(self.update_ws), _stream()),
               'pgm_ppo_update')
 
-    def evaluate(self, ob_mean=None, ob_var=None):
+    def evaluate(self, ob_mean=None, ob_var=None, out=None):
         mean = self.ob_mean if ob_mean is None else ob_mean
         var = self.ob_var if ob_var is None else ob_var
+        out = self.objs if out is None else out
         check(lib().pgm_eval(C.byref(self.dims), _ptr(self.params), C.byref(self.c_spec), _ptr(mean), _ptr(var),
                              _ptr(self.s0_eval), self.eval_num, int(self.use_ob_rms), int(self.raw), self.gamma,
-                             _ptr(self.objs), _stream()), 'pgm_eval')
-        return self.objs
+                             _ptr(out), _stream()), 'pgm_eval')
+        return out
 
-    def iteration(self, j, lr, noise=None, perms=None, carry=True):
+    @property
+    def eval_stream(self):
+        """Side stream of the overlapped evaluation (iteration(..., overlap_eval=True))."""
+        if self._eval_stream is None:
+            self._eval_stream = torch.cuda.Stream(device=self.dev)
+        return self._eval_stream
+
+    def wait_eval(self):
+        """Order the current stream after the last overlapped evaluation (its objs are then readable)."""
+        if self._eval_done is not None:
+            torch.cuda.current_stream().wait_event(self._eval_done)
+
+    def iteration(self, j, lr, noise=None, perms=None, carry=True, overlap_eval=False, objs_out=None):
         """One MOPG iteration for every task: rollout, returns, advantages, PPO update, evaluation.
 
         noise/perms: the reference's RNG draws of iteration j (parity mode); None draws the
-        device counter streams keyed by j (perf mode)."""
+        device counter streams keyed by j (perf mode).
+
+        overlap_eval: the evaluation of this iteration's snapshot (mopg.py:146-155) runs on a side stream,
+        concurrently with the NEXT iteration's rollout / returns / advantages (which only read the
+        parameters); the next PPO update (which writes them) waits for it.  It normalises with a copy of
+        this iteration's ob_rms (the next rollout advances the live one) and writes objs_out (default
+        self.objs), readable after wait_eval() or from work queued on eval_stream."""
         self.lr.fill_(float(lr))
         if noise is None:  # perf mode: the counter stream of iteration j, drawn by one wide kernel up front
             check(lib().pgm_normal_noise(self.noise.numel(), C.c_uint64(j), _ptr(self.noise), _stream()),
@@ -197,8 +218,22 @@ class TaskBatch:
         self.adv_normalize()
         if perms is None:
             self.make_perms(j)
+        self.wait_eval()  # the previous overlapped evaluation still reads the parameters
         self.ppo_update(perms)
-        self.evaluate()
+        if not overlap_eval:
+            self.evaluate(out=objs_out)
+            return
+        self._eval_mean.copy_(self.ob_mean)
+        self._eval_var.copy_(self.ob_var)
+        ready = torch.cuda.Event()
+        ready.record()
+        side = self.eval_stream
+        side.wait_event(ready)
+        with torch.cuda.stream(side):
+            out = self.evaluate(self._eval_mean, self._eval_var, out=objs_out)
+            out.record_stream(side)
+            self._eval_done = torch.cuda.Event()
+            self._eval_done.record(side)
 
     # ------------------------------------------------------------------ host transfer
     def set_task(self, p, state_dict, opt_state=None, env_params=None, weights=None):

@@ -399,3 +399,24 @@ def test_mopg_iterations_end_to_end(gpu):
             ref = tb.layout.flatten(off.actor_critic.state_dict(), dtype=np.float64)
             _close(gpu_params[j][p], ref, 2e-5, 1e-4, f'params iter {j}')
             _close(gpu_objs[j][p], off.objs, 1e-3, 1e-4, f'eval objs iter {j}')
+
+
+def test_overlapped_eval_is_bitwise_identical(gpu):
+    """iteration(..., overlap_eval=True): the snapshot evaluation on the side stream (beside the next rollout)
+    gives the same objectives, parameters and statistics as the in-order schedule, bit for bit."""
+    env, P, N, T = 'MO-Walker2d-v2', 3, 4, 64
+    res = []
+    for overlap in (False, True):
+        spec, tb, _ = _batch_with_policies(env, P, N, T, seed=7, scale=0.05, ppo_epoch=2, num_mini_batch=4)
+        tb.reset_stats()
+        tb.env_reset()
+        objs = []
+        for j in range(3):
+            tb.iteration(j, 3e-4, carry=j > 0, overlap_eval=overlap)
+            with torch.cuda.stream(tb.eval_stream if overlap else torch.cuda.current_stream()):
+                objs.append(tb.objs.clone())
+        tb.wait_eval()
+        torch.cuda.synchronize()
+        res.append((torch.stack(objs).cpu(), tb.params.cpu(), tb.ob_mean.cpu(), tb.obj_var.cpu()))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)

@@ -590,6 +590,10 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                 lds_sync_m();
             }
             PGM_STAMP(2);
+            constexpr int NV4 = IMG / 4, TAIL = IMG - 4 * NV4;
+            constexpr int NG4 = (NV4 + MT - 1) / MT;  // MODE 2: float4 groups per thread
+            float4 ag[NS == 2 ? NG4 : 1], am[NS == 2 ? NG4 : 1], av[NS == 2 ? NG4 : 1], ap[NS == 2 ? NG4 : 1];
+            float agt = 0.f, sq2 = 0.f;
             if constexpr (NS == 2) {
                 // ---- add the other half's gradient image.  Publish: 16-B sc1 (write-through) buffer stores,
                 // every wave drains them, barrier, ONE lane stores the tagged flag granule {step, loss sum}.
@@ -603,7 +607,6 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                 const int slot_other = ((p * 2 + m) * 2 + (1 - hs)) * 2 + par;
                 const int off_mine = slot_mine * a.xslot * 8, off_other = slot_other * a.xslot * 8;
                 const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(a.xb, 0, a.xbytes, 0x00020000);
-                constexpr int NV4 = IMG / 4, TAIL = IMG - 4 * NV4;
                 constexpr int SC1 = 16;  // cache-policy aux bit of the buffer builtins: sc1
                 float* G0 = S.big.GA[0];
                 const float* G1 = S.big.GA[1];
@@ -646,21 +649,37 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                     S.red[12] = hs == 0 ? lsum_wg + lo : lo + lsum_wg;
                 }
                 lds_sync_m();  // the polling lane matched: every wave may load the partner's image
-                for (int i = t; i < NV4; i += MT) {
+                // g = half0 + half1 of this thread's float4 groups i = t + k*MT stays in registers (no LDS
+                // round trip); the sum of squares is fused in, and the Adam operands of the same groups are
+                // read from LDS right away so their latency hides under the norm hand-off below
+#pragma unroll
+                for (int k = 0; k < NG4; ++k) {
+                    const int i = min(t + k * MT, NV4 - 1);
                     const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(xr, off_other + 16 * i, 0, SC1);
+                    const float4 mine = *reinterpret_cast<const float4*>(&G0[4 * i]);
+                    const float mv[4] = {mine.x, mine.y, mine.z, mine.w};
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
                         const float ov = __uint_as_float(v[q]);
-                        G0[4 * i + q] = hs == 0 ? G0[4 * i + q] + ov : ov + G0[4 * i + q];
+                        ag[k][q] = hs == 0 ? mv[q] + ov : ov + mv[q];
+                        if (t + k * MT < NV4) sq2 = fmaf(ag[k][q], ag[k][q], sq2);
                     }
                 }
                 if (t < TAIL) {
                     const float ov = __uint_as_float(
                         __builtin_amdgcn_raw_buffer_load_b32(xr, off_other + 16 * NV4 + 4 * t, 0, SC1));
-                    G0[4 * NV4 + t] = hs == 0 ? G0[4 * NV4 + t] + ov : ov + G0[4 * NV4 + t];
+                    const float mine = G0[4 * NV4 + t];
+                    agt = hs == 0 ? mine + ov : ov + mine;
+                    sq2 = fmaf(agt, agt, sq2);
+                }
+#pragma unroll
+                for (int k = 0; k < NG4; ++k) {
+                    const int i = min(t + k * MT, NV4 - 1);
+                    am[k] = *reinterpret_cast<const float4*>(&S.MV[4 * i]);
+                    av[k] = *reinterpret_cast<const float4*>(&S.MV[IMG + 4 * i]);
+                    ap[k] = *reinterpret_cast<const float4*>(&Pf[4 * i]);
                 }
                 PGM_STAMP(11);
-                lds_sync_m();
             }
             // ---- clip_grad_norm_ over every parameter (padding slots hold zeros)
             constexpr int NG = SPLIT ? IMG : 2 * IMG;
@@ -668,10 +687,12 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
             const float* GA1 = S.big.GA[1];
             // SPLIT: g = GA[0] + GA[1] (MODE 2: already summed into GA[0]); joint: GA[0..1] contiguous
             auto gval = [&](int i) { return SPLIT && NS == 1 ? GA0[i] + GA1[i] : GA0[i]; };
-            float sq = 0.f;
-            for (int i = t; i < NG; i += MT) {
-                const float g = gval(i);
-                sq = fmaf(g, g, sq);
+            float sq = sq2;
+            if constexpr (NS != 2) {
+                for (int i = t; i < NG; i += MT) {
+                    const float g = gval(i);
+                    sq = fmaf(g, g, sq);
+                }
             }
             sq = wave_sum64(sq);
             if (l == 0) S.red[w] = sq;
@@ -724,7 +745,42 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
             const float step_size = (float)(lr / bc1);
             const float bc2s = (float)sqrt(bc2);
             const float inv_bc2s = 1.f / bc2s;
-            if constexpr (SPLIT) {
+            auto adam1 = [&](float g, float& mm, float& vv, float& pp) {
+                const float gc = g * coef;
+                mm = mm + (1.f - b1c) * (gc - mm);
+                vv = vv * b2c + (1.f - b2c) * (gc * gc);
+                // torch: p -= step_size * m / (sqrt(v) / sqrt(bc2) + eps); hardware sqrt / rcp
+                const float den = __builtin_amdgcn_sqrtf(vv) * inv_bc2s + eps;
+                pp -= step_size * mm * __builtin_amdgcn_rcpf(den);
+            };
+            if constexpr (NS == 2) {  // operands already in registers (float4 groups of the gather)
+#pragma unroll
+                for (int k = 0; k < NG4; ++k) {
+                    const int i = t + k * MT;
+                    if (i >= NV4) break;
+                    float* g4 = &ag[k].x;
+                    float* m4 = &am[k].x;
+                    float* v4 = &av[k].x;
+                    float* p4 = &ap[k].x;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        adam1(g4[q], m4[q], v4[q], p4[q]);
+                        if (m == 1 && 4 * i + q >= oLs && 4 * i + q < oLs + A) S.aiv[4 * i + q - oLs] = expf(-2.f * p4[q]);
+                    }
+                    *reinterpret_cast<float4*>(&S.MV[4 * i]) = am[k];
+                    *reinterpret_cast<float4*>(&S.MV[IMG + 4 * i]) = av[k];
+                    *reinterpret_cast<float4*>(&Pf[4 * i]) = ap[k];
+                }
+                if (t < TAIL) {
+                    const int i = 4 * NV4 + t;
+                    float mm = S.MV[i], vv = S.MV[IMG + i], pp = Pf[i];
+                    adam1(agt, mm, vv, pp);
+                    S.MV[i] = mm;
+                    S.MV[IMG + i] = vv;
+                    Pf[i] = pp;
+                    if (m == 1 && i >= oLs && i < oLs + A) S.aiv[i - oLs] = expf(-2.f * pp);
+                }
+            } else if constexpr (SPLIT) {
                 // batches of 4 elements per thread: every LDS read of a batch before any write
                 for (int i0 = t; i0 < IMG; i0 += 4 * MT) {
                     float g[4], mm[4], vv[4], pp[4];

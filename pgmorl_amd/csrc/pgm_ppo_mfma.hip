@@ -434,15 +434,9 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                             dZ2[ob][r] = z[ob][r] * (1.f - H2[ob][r] * H2[ob][r]);
                             gB2[ob] += dZ2[ob][r];
                         }
-                    // ---- dW2^T[in][o] += H1^T dZ2: straight from the C-layout registers
-#pragma unroll
-                    for (int r = 0; r < 16; ++r)
-#pragma unroll
-                        for (int ib = 0; ib < 2; ++ib)
-#pragma unroll
-                            for (int ob = 0; ob < 2; ++ob) gW2[ib][ob] = mfma(H1[ib][r], dZ2[ob][r], gW2[ib][ob]);
                     PGM_STAMP(6);
-                    // ---- dH1 = dZ2 W2  (A = dZ2 through the transpose tile, B = W2t[in][o] column)
+                    // ---- dH1 = dZ2 W2  (A = dZ2 through the transpose tile, B = W2t[in][o] column); the critical
+                    // path, so its MFMAs go into the pipe first and dW2 queues behind them
                     wave_lds_fence();  // heads finished reading the H2 tile
 #pragma unroll
                     for (int ob = 0; ob < 2; ++ob)
@@ -457,6 +451,14 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
 #pragma unroll
                         for (int ib = 0; ib < 2; ++ib) z[ib] = mfma(av, W.W2t[ib * TS + c][k], z[ib]);
                     }
+                    // ---- dW2^T[in][o] += H1^T dZ2: straight from the C-layout registers (runs in the MFMA pipe
+                    // while the VALU forms dZ1 from the dH1 results)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+#pragma unroll
+                        for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+                            for (int ob = 0; ob < 2; ++ob) gW2[ib][ob] = mfma(H1[ib][r], dZ2[ob][r], gW2[ib][ob]);
                     f32x16 dZ1[2];
 #pragma unroll
                     for (int ib = 0; ib < 2; ++ib)

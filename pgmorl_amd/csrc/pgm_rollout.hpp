@@ -41,6 +41,13 @@ __device__ __forceinline__ void chan_merge(double& mean, double& var, double cou
 }
 
 __device__ __forceinline__ double clipd(double x, double lo, double hi) { return fmin(fmax(x, lo), hi); }
+// the same clip as two bare v_max_f64 / v_min_f64: fmin / fmax on values the compiler cannot prove canonical
+// (bounds loaded from memory) cost two extra canonicalising v_max_f64 per call inside the step loop
+__device__ __forceinline__ double clipd_hw(double x, double lo, double hi) {
+    double r;
+    asm volatile("v_max_f64 %0, %1, %2\n\tv_min_f64 %0, %0, %3" : "=&v"(r) : "v"(x), "v"(lo), "v"(hi));
+    return r;
+}
 
 // fp64 tanh as expm1(2y) / (expm1(2y) + 2): a few ulp (the env state's precision is fp64, the
 // observation leaves as fp32), half the instructions of the double-double libm tanh.  |y| is clamped at

@@ -31,6 +31,8 @@ PGM_STAMP_UNIT(lanes)
 
 namespace pgm {
 
+typedef float f2 __attribute__((ext_vector_type(2)));
+
 template <int O, int K>
 constexpr bool lanes_fit() { return O <= 48 && O + K + 1 <= 64; }
 
@@ -70,16 +72,15 @@ struct ActorLane {
         }
         h1[l] = tanh_fast(z0 + z1);
         wave_lds_fence_r();
-        float a0 = b2, a1 = 0.f, a2 = 0.f, a3 = 0.f;  // four short chains instead of one of 64
+        // packed fp32 FMAs over unit pairs (v_pk_fma_f32: two MACs per instruction), two chains of 16
+        f2 a01 = f2{b2, 0.f}, a23 = f2{0.f, 0.f};
 #pragma unroll
         for (int k = 0; k < H; k += 4) {
             const float4 h = *reinterpret_cast<const float4*>(h1 + k);
-            a0 = fmaf(h.x, w2[k], a0);
-            a1 = fmaf(h.y, w2[k + 1], a1);
-            a2 = fmaf(h.z, w2[k + 2], a2);
-            a3 = fmaf(h.w, w2[k + 3], a3);
+            a01 = __builtin_elementwise_fma(f2{h.x, h.y}, f2{w2[k], w2[k + 1]}, a01);
+            a23 = __builtin_elementwise_fma(f2{h.z, h.w}, f2{w2[k + 2], w2[k + 3]}, a23);
         }
-        const float h2 = tanh_fast((a0 + a1) + (a2 + a3));
+        const float h2 = tanh_fast((a01.x + a01.y) + (a23.x + a23.y));
         float pr[A];
 #pragma unroll
         for (int j = 0; j < A; ++j) pr[j] = h2 * wm[j];
@@ -289,7 +290,7 @@ __global__ __launch_bounds__(256) void rollout_lane_kernel(RolloutArgs a) {
             PGM_STAMP(1);
             // Gaussian draw (torch.normal(mean, std) = eps * std + mean), log-prob and clipped action, all
             // wave-uniform: lane j's noise is broadcast by readlane
-            float lpt[A], avl = 0.f;
+            float lpt[A], avs[A];
             double ac[A], sq[A];
 #pragma unroll
             for (int j = 0; j < A; ++j) {
@@ -297,14 +298,18 @@ __global__ __launch_bounds__(256) void rollout_lane_kernel(RolloutArgs a) {
                 const float av = fmaf(ej, pol.sd[j], mu[j]);
                 const float dz = (av - mu[j]) * pol.rsd[j];
                 lpt[j] = -0.5f * dz * dz - pol.ls[j] - LOG_SQRT_2PI;
-                avl = l == j ? av : avl;
-                ac[j] = clipd((double)av, env.lo[j], env.hi[j]);
+                avs[j] = av;
+                ac[j] = clipd_hw((double)av, env.lo[j], env.hi[j]);
                 sq[j] = ac[j] * ac[j];
             }
             const float lp = tree_sum(lpt);
             const double e2 = tree_sum(sq);
-            if (l < A) act[((size_t)step * NN + n) * A + l] = avl;
-            if (l == 0) logp[(size_t)step * NN + n] = lp;
+            if (l == 0) {  // the draws are wave-uniform: lane 0 stores the action row and its log-prob
+                float* ar = act + ((size_t)step * NN + n) * A;
+#pragma unroll
+                for (int j = 0; j < A; ++j) ar[j] = avs[j];
+                logp[(size_t)step * NN + n] = lp;
+            }
             PGM_STAMP(6);
             // dynamics (fp64), time limit, auto-reset, VecNormalize accumulators
             const double sn = env.step(s_o[e], ac, e2, objraw[e]);

@@ -83,6 +83,18 @@ __device__ __forceinline__ double rsqrt_d(double x) {
     return fma(r * e, 0.5, r);
 }
 
+// fp64 tanh for the SynthMO dynamics: 1 - 2 / (exp(2|y|) + 1) with the sign restored; exp through
+// 2^(j/64) table-free range reduction is ocml's, the division is rcp + two Newton steps (~1 ulp).  Absolute
+// error ~1e-16 (relative error grows as |y| -> 0, where the state's absolute precision is what matters).
+__device__ __forceinline__ double tanh_d2(double y) {
+    const double ay = fmin(fabs(y), 20.0);
+    const double e = exp(2.0 * ay) + 1.0;
+    double r = __builtin_amdgcn_rcp(e);
+    r = fma(r, fma(-e, r, 1.0), r);
+    r = fma(r, fma(-e, r, 1.0), r);
+    return copysign(fma(-2.0, r, 1.0), y);
+}
+
 template <int N_>
 __device__ __forceinline__ float sel_lane(const float (&v)[N_], int l) {
     float r = 0.f;

@@ -91,18 +91,6 @@ __device__ __forceinline__ int sel_lane_i(const int (&v)[N_], int i) {
     return r;
 }
 
-// fp64 tanh for the SynthMO dynamics: 1 - 2 / (exp(2|y|) + 1) with the sign restored; exp through
-// 2^(j/64) table-free range reduction is ocml's, the division is rcp + two Newton steps (~1 ulp).  Absolute
-// error ~1e-16 (relative error grows as |y| -> 0, where the state's absolute precision is what matters).
-__device__ __forceinline__ double tanh_d2(double y) {
-    const double ay = fmin(fabs(y), 20.0);
-    const double e = exp(2.0 * ay) + 1.0;
-    double r = __builtin_amdgcn_rcp(e);
-    r = fma(r, fma(-e, r, 1.0), r);
-    r = fma(r, fma(-e, r, 1.0), r);
-    return copysign(fma(-2.0, r, 1.0), y);
-}
-
 // 17-wide (or any A <= 24) action-mean sums: groups of 8 through wave_sum64_multi
 template <int A>
 __device__ __forceinline__ void head_sums(const float (&pr)[A], float (&mu)[A]) {
@@ -350,16 +338,14 @@ __global__ __launch_bounds__(WTH) void rollout_wide_kernel(RolloutArgs a) {
         for (int e = 0; e < EPW; ++e) {
             const int n = w + WW * e;
             if (n >= NN) break;
-            float a0 = b2, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+            f2 a01 = f2{b2, 0.f}, a23 = f2{0.f, 0.f};  // packed fp32 FMAs over unit pairs
 #pragma unroll
             for (int k = 0; k < H; k += 4) {
                 const float4 hv = *reinterpret_cast<const float4*>(&S.h1[n][k]);
-                a0 = fmaf(hv.x, w2[k], a0);
-                a1 = fmaf(hv.y, w2[k + 1], a1);
-                a2 = fmaf(hv.z, w2[k + 2], a2);
-                a3 = fmaf(hv.w, w2[k + 3], a3);
+                a01 = __builtin_elementwise_fma(f2{hv.x, hv.y}, f2{w2[k], w2[k + 1]}, a01);
+                a23 = __builtin_elementwise_fma(f2{hv.z, hv.w}, f2{w2[k + 2], w2[k + 3]}, a23);
             }
-            const float h2 = tanh_fast((a0 + a1) + (a2 + a3));
+            const float h2 = tanh_fast((a01.x + a01.y) + (a23.x + a23.y));
             float pr[A], mu[A];
 #pragma unroll
             for (int j = 0; j < A; ++j) pr[j] = h2 * wm[j];
@@ -380,7 +366,7 @@ __global__ __launch_bounds__(WTH) void rollout_wide_kernel(RolloutArgs a) {
             const float av = fmaf(ej, sd_l, m);
             const float dz = (av - m) * rsd_l;
             const float lpt = al ? -0.5f * dz * dz - ls_l - LOG_SQRT_2PI : 0.f;
-            const double acd = clipd((double)av, lo_l, hi_l);
+            const double acd = clipd_hw((double)av, lo_l, hi_l);
             const float lp = wave_sum64(lpt);
             const double e2 = wave_sum64_d(al ? acd * acd : 0.0);
             if (al) {

@@ -7,9 +7,9 @@
 //     are added through a 16-B sc1 publish + tagged flag hand-off (cdna_hip_programming.md G16 R1), both
 //     halves add them in the same order, so their Adam steps stay bitwise identical; the two towers exchange
 //     the squared gradient norm through one tagged granule per step (the narrow kernel's MODE 2 protocol);
-//   * layer 1 (O x 64 = 96 KB) does not fit LDS next to the rest: the forward streams W1 from L2 (sc1 buffer
-//     loads) and the observation rows straight from the rollout buffer (float4 per lane), both two 4-k-step
-//     groups ahead of the MFMAs.  Layer-1 k-steps pair features (h*KH + ks) of the two lane halves: any
+//   * layer 1 (O x 64 = 96 KB) does not fit LDS next to the rest: the forward streams W1 through L1 (the
+//     four waves read the same rows; the L1 is invalidated after each layer-1 Adam step) and the observation
+//     rows straight from the rollout buffer (float4 per lane), both three 4-k-step groups ahead of the MFMAs.  Layer-1 k-steps pair features (h*KH + ks) of the two lane halves: any
 //     bijection between the MFMA's two k-slots and the features works as long as the A (X) and B (W1)
 //     operands use the same one;
 //   * dW1 stays in REGISTERS: wave w owns the 32-feature tiles kt = w, w + 4, w + 8 of dW1 (96 accumulator
@@ -25,6 +25,8 @@
 
 #include "pgm_dispatch.hpp"
 #include "pgm_mfma.hpp"
+
+PGM_STAMP_UNIT(wupd)
 
 namespace pgm {
 
@@ -159,8 +161,8 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
     const float* rets = a.returns + (size_t)p * (T + 1) * N * K;
     // this workgroup's parameters as a buffer: layer-1 weights are re-read every tile with sc1 (L2) loads
     const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(P, 0, L.total * 4, 0x00020000);
-    auto w1 = [&](int k, int col) {  // W1^T[k][col]
-        return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(prs, (offW1 + k * H + col) * 4, 0, WSPLIT));
+    auto w1 = [&](int k, int col) {  // W1^T[k][col]: through L1 (the 4 waves stream the same rows)
+        return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(prs, (offW1 + k * H + col) * 4, 0, 0));
     };
 
     // ---- small image + its Adam moments
@@ -187,6 +189,7 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
     float* scr = &S.big.scr[w][0][0];  // tile A: H1, then dZ1
     float* scr2 = &S.act2[w][0][0];     // tile B: H2, then dZ2
 
+    PGM_STAMP_DECL
     for (int e = 0; e < E; ++e) {
         for (int bb = 0; bb < nb; ++bb) {
             const int32_t* perm = a.perms + (size_t)e * B + bb * mb + r0;
@@ -214,18 +217,39 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
                 const int row = perm[min(si, mbs - 1)];
                 if (h == 0) S.rowid[w][c] = row;
                 if (i0 < mbs) {  // wave-uniform
+                    // per-sample loss operands of this lane's sample, gathered now (random rows: an HBM round trip
+                    // that the layer-1 stream hides) -- critic: old values, returns; actor: action, old logp, adv
+                    float pa[A], pv[K], pr[K], plp = 0.f, pad = 0.f;
+                    if (m == 0) {
+#pragma unroll
+                        for (int q = 0; q < K; ++q) {
+                            pv[q] = vals[(size_t)row * K + q];
+                            pr[q] = rets[(size_t)row * K + q];
+                        }
+                    } else {
+#pragma unroll
+                        for (int q = 0; q < A; ++q) pa[q] = acts[(size_t)row * A + q];
+                        plp = oldlp[row];
+                        pad = advs[row];
+                    }
                     // ---- layer 1: Z1[s][u] = sum_k X[s][k] W1t[k][u]; X row of sample c, features h*KH + ks;
-                    // groups of KG k-steps, two groups in flight ahead of the MFMAs (static ping-pong)
+                    // groups of KG k-steps, three groups in flight ahead of the MFMAs
                     const float4* xr = reinterpret_cast<const float4*>(obs + (size_t)row * O + h * KH);
                     f32x16 z[2] = {f32x16{0}, f32x16{0}};
-                    float4 xa, xb;
-                    float wa[KG][2], wb[KG][2];
+                    // four register groups in rotation, each loaded three groups (24 MFMAs) ahead of its MFMAs;
+                    // branch-free trips (the group count padded to a multiple of 4, padding groups read clamped
+                    // addresses and contribute X = 0) keep the loads outstanding across trips
+                    float4 xq[4];
+                    float wq[4][KG][2];
+                    constexpr int NGP = (NG + 3) / 4 * 4;
                     auto load_group = [&](int g, float4& x, float (&wv)[KG][2]) {
-                        x = xr[g];
+                        const int gg = min(g, NG - 1);
+                        x = xr[gg];
+                        if (g >= NG) x = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
                         for (int q = 0; q < KG; ++q) {
-                            wv[q][0] = w1(h * KH + g * KG + q, c);
-                            wv[q][1] = w1(h * KH + g * KG + q, TS + c);
+                            wv[q][0] = w1(h * KH + gg * KG + q, c);
+                            wv[q][1] = w1(h * KH + gg * KG + q, TS + c);
                         }
                     };
                     auto mfma_group = [&](const float4& x, const float (&wv)[KG][2]) {
@@ -236,15 +260,14 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
                             z[1] = mfma(xv[q], wv[q][1], z[1]);
                         }
                     };
-                    load_group(0, xa, wa);
-                    if (NG > 1) load_group(1, xb, wb);
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) load_group(b, xq[b], wq[b]);
 #pragma unroll 1
-                    for (int g = 0; g < NG; g += 2) {
-                        mfma_group(xa, wa);
-                        if (g + 2 < NG) load_group(g + 2, xa, wa);
-                        if (g + 1 < NG) {
-                            mfma_group(xb, wb);
-                            if (g + 3 < NG) load_group(g + 3, xb, wb);
+                    for (int g = 0; g < NGP; g += 4) {
+#pragma unroll
+                        for (int b = 0; b < 4; ++b) {
+                            mfma_group(xq[b], wq[b]);
+                            load_group(min(g + b + 4, NGP - 1), xq[b], wq[b]);
                         }
                     }
                     // activations live in two per-wave LDS tiles, not registers (the 230 accumulator registers
@@ -256,6 +279,7 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
                         for (int r = 0; r < 16; ++r) scr[rowof(r, h) * SCR + hb * TS + c] = tanh_fast(z[hb][r] + bias);
                     }
                     wave_lds_fence();
+                    PGM_STAMP(0);
                     // ---- layer 2 (A from tile A, transposed)
                     z[0] = z[1] = f32x16{0};
 #pragma unroll 8
@@ -272,6 +296,7 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
                         for (int r = 0; r < 16; ++r) scr2[rowof(r, h) * SCR + ob * TS + c] = tanh_fast(z[ob][r] + bias);
                     }
                     wave_lds_fence();
+                    PGM_STAMP(1);
                     // ---- heads (VALU): lane = sample c, half h sums units [32h, 32h+32)
                     float outv[Q];
 #pragma unroll
@@ -292,7 +317,7 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
                         float ls = 0.f;
 #pragma unroll
                         for (int q = 0; q < K; ++q) {
-                            const float V = outv[q], Vp = vals[(size_t)row * K + q], R = rets[(size_t)row * K + q];
+                            const float V = outv[q], Vp = pv[q], R = pr[q];
                             float gv;
                             if (a.hp.use_clipped_value_loss) {
                                 const float dv = V - Vp;
@@ -309,11 +334,11 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
                         }
                         if (ok && h == 0) lsum += ls;
                     } else {  // clipped surrogate
-                        const float lpo = oldlp[row], ad = advs[row];
+                        const float lpo = plp, ad = pad;
                         float lp = 0.f;
 #pragma unroll
                         for (int q = 0; q < A; ++q) {
-                            const float diff = acts[(size_t)row * A + q] - outv[q];
+                            const float diff = pa[q] - outv[q];
                             lp += -0.5f * diff * diff * S.aiv[q] - lstd[q] - LOG_SQRT_2PI;
                         }
                         const float ratio = expf(lp - lpo);
@@ -325,7 +350,7 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
                         if (ok && h == 0) lsum += -fminf(s1, s2);
 #pragma unroll
                         for (int q = 0; q < A; ++q) {
-                            const float diff = acts[(size_t)row * A + q] - outv[q];
+                            const float diff = pa[q] - outv[q];
                             const float iv = S.aiv[q];
                             dO[q] = dlp * diff * iv;
                             if (h == 0) gLs[q] += dlp * (diff * diff * iv - 1.f);
@@ -339,6 +364,7 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
                         }
                     }
                     wave_lds_fence();
+                    PGM_STAMP(2);
                     // ---- head-weight grads on the MFMA: gWh^T[u][q] += sum_s H2[s][u] dO[s][q]
                     // (A = H2 in the C layout from tile B: lane u, samples rowof(r, 0/1); B = dO, lane q)
 #pragma unroll
@@ -404,7 +430,9 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
 #pragma unroll
                         for (int r = 0; r < 16; ++r) scr[rowof(r, h) * SCR + ib * TS + c] = dZ1[ib][r];
                 }
+                PGM_STAMP(3);
                 lds_sync_m();  // every tile's dZ1 and rows visible
+                PGM_STAMP(4);
                 // ---- dW1^T[k][u] += X^T dZ1 over the pass's tiles for this wave's feature tiles; the X values
                 // of (tile u, feature tile kt) are gathered from HBM one round ahead (rows of the tile)
                 {
@@ -438,7 +466,9 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
                         }
                     }
                 }
+                PGM_STAMP(5);
                 lds_sync_m();  // transpose tiles / row ids reused by the next pass
+                PGM_STAMP(6);
             }  // passes
 
             // ---- lane halves of the per-column partial sums; 64-lane sums of the per-sample ones
@@ -512,6 +542,7 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
                 lds_sync_m();
             }
             // head rows q >= NQ (critic: 2..16) are exactly zero: dO[q] = 0 for them
+            PGM_STAMP(7);
             float* G0 = S.big.GA[0];
             const float* G1 = S.big.GA[1];
             const float lsum_wg = (S.red[8] + S.red[9]) + (S.red[10] + S.red[11]);
@@ -578,6 +609,7 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
                     const float lo = __uint_as_float((unsigned)x);
                     S.red[12] = hs == 0 ? lsum_wg + lo : lo + lsum_wg;
                 }
+                PGM_STAMP(8);
                 lds_sync_m();  // the polling lane matched: every wave may load the partner's gradients
                 for (int i = t; i < NV4; i += MT) {
                     const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(xr, off_other + 16 * i, 0, WSPLIT);
@@ -614,6 +646,7 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
                 for (int i = t; i < IMG; i += MT) G0[i] = G0[i] + G1[i];
                 lds_sync_m();
             }
+            PGM_STAMP(9);
             // ---- clip_grad_norm_: small image + this wave's dW1 registers (rows k >= O hold zeros)
             float sq = 0.f;
             for (int i = t; i < IMG; i += MT) sq = fmaf(G0[i], G0[i], sq);
@@ -655,6 +688,7 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
                 else st_a += lsum_task / (float)mb;
                 st_e += ent;
             }
+            PGM_STAMP(10);
             // ---- Adam: the small image in LDS, layer 1 from the owning wave's registers (moments in HBM)
             ++nstep;
             b1p *= (double)b1c;
@@ -677,41 +711,51 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
                 if (m == 1 && i >= oLs && i < oLs + A) S.aiv[i - oLs] = expf(-2.f * pp);
             }
             {
-                // layer 1 rows k = (w + 4j)*32 + rowof(r, h) of this lane (column ib*32 + c): lane base + constant
+                // layer 1 rows k = (w + 4j)*32 + rowof(r, h) of this lane (column ib*32 + c): lane base + constant;
+                // the moments / weights of block b + 1 are loaded while block b updates
                 const int kb = opaque(w * TS + 4 * h);
                 const int fb = opaque(offW1 + kb * H + c);
+                constexpr int NBK = NKW * 2;
+                float bm[2][16], bv[2][16], bp[2][16];
+                auto load_blk = [&](int bk, float (&mm)[16], float (&vv)[16], float (&pp)[16]) {
+                    const int j = bk >> 1, ib = bk & 1;
 #pragma unroll
-                for (int j = 0; j < NKW; ++j) {
-                    if (w + 4 * j >= NKT) break;
+                    for (int r = 0; r < 16; ++r) {
+                        const int kr = 4 * j * TS + (r & 3) + 8 * (r >> 2);  // k - kb
+                        const int f = w + 4 * j < NKT && kb + kr < O ? fb + kr * H + ib * TS : offW1;
+                        mm[r] = Mo[f];
+                        vv[r] = Vo[f];
+                        pp[r] = P[f];
+                    }
+                };
+                load_blk(0, bm[0], bv[0], bp[0]);
 #pragma unroll
-                    for (int ib = 0; ib < 2; ++ib) {
-                        float mm[16], vv[16], pp[16];
-#pragma unroll
-                        for (int r = 0; r < 16; ++r) {
-                            const int kr = 4 * j * TS + (r & 3) + 8 * (r >> 2);  // k - kb
-                            const int f = kb + kr < O ? fb + kr * H + ib * TS : offW1;
-                            mm[r] = Mo[f];
-                            vv[r] = Vo[f];
-                            pp[r] = P[f];
-                        }
+                for (int bk = 0; bk < NBK; ++bk) {
+                    const int j = bk >> 1, ib = bk & 1, cur = bk & 1;
+                    if (bk + 1 < NBK) load_blk(bk + 1, bm[cur ^ 1], bv[cur ^ 1], bp[cur ^ 1]);
+                    if (w + 4 * j < NKT) {
 #pragma unroll
                         for (int r = 0; r < 16; ++r) {
                             const int kr = 4 * j * TS + (r & 3) + 8 * (r >> 2);
                             if (kb + kr >= O) continue;
                             const int f = fb + kr * H + ib * TS;
-                            adam(dW1[j][ib][r], mm[r], vv[r], pp[r]);
-                            Mo[f] = mm[r];
-                            Vo[f] = vv[r];
-                            P[f] = pp[r];
+                            adam(dW1[j][ib][r], bm[cur][r], bv[cur][r], bp[cur][r]);
+                            Mo[f] = bm[cur][r];
+                            Vo[f] = bv[cur][r];
+                            P[f] = bp[cur][r];
                         }
-                        __builtin_amdgcn_sched_barrier(0);  // one 48-load block in flight at a time
                     }
                 }
             }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // layer-1 stores land in L2 before any re-read
+            // layer-1 stores land in L2, then this CU's L1 is invalidated: the next step's W1 stream (plain
+            // loads) must not hit lines cached before this update
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             lds_sync_m();
+            PGM_STAMP(11);
         }  // minibatches
     }      // epochs
+    PGM_STAMP_FLUSH;
     if (hs != 0) return;  // half 1 worked on copies
     // ---- write back the small image (layer 1 was updated in place)
     for (int i = t; i < IMG; i += MT) {

@@ -20,6 +20,8 @@
 #include "pgm_dispatch.hpp"
 #include "pgm_rollout.hpp"
 
+PGM_STAMP_UNIT(wide)
+
 namespace pgm {
 
 namespace {
@@ -297,6 +299,7 @@ __global__ __launch_bounds__(WTH) void rollout_wide_kernel(RolloutArgs a) {
         obj_valid = 1;
     };
 
+    PGM_STAMP_DECL
     for (int step = 0; step < T; ++step) {
         const int par = step & 1;
         const int cs = step % WNCH, cb = (step / WNCH) & 1;
@@ -322,7 +325,9 @@ __global__ __launch_bounds__(WTH) void rollout_wide_kernel(RolloutArgs a) {
 #pragma unroll
             for (int n = 0; n < NN; ++n) S.zp[w][n][l] = acc[n].x + acc[n].y;
         }
+        PGM_STAMP(0);
         lds_sync();  // A
+        PGM_STAMP(1);
         // ---- 2. this wave's envs: layer-1 sum + tanh, layer 2, mean head, Gaussian draw, clipped action
 #pragma unroll
         for (int e = 0; e < EPW; ++e) {
@@ -378,7 +383,9 @@ __global__ __launch_bounds__(WTH) void rollout_wide_kernel(RolloutArgs a) {
                 logp[(size_t)step * NN + n] = lp;
             }
         }
+        PGM_STAMP(2);
         lds_sync();  // C
+        PGM_STAMP(3);
         // ---- 3. time limit, fp64 dynamics, objective partial sums, auto-reset, ob_rms, normalised obs
         int done[NN];
 #pragma unroll
@@ -413,7 +420,9 @@ __global__ __launch_bounds__(WTH) void rollout_wide_kernel(RolloutArgs a) {
                     s[j][n] = sn;
                 }
             }
+            PGM_STAMP(4);
             wave_sum16_d(vk, &S.objp[par][w][0]);
+            PGM_STAMP(5);
         }
 #pragma unroll
         for (int j = 0; j < FPL; ++j) {
@@ -444,11 +453,14 @@ __global__ __launch_bounds__(WTH) void rollout_wide_kernel(RolloutArgs a) {
             }
         }
         if (nc.use_ob) cnt += (double)NN;
+        PGM_STAMP(6);
         if (w == SW && step > 0) finish_step(step - 1, par ^ 1);
 #pragma unroll
         for (int n = 0; n < NN; ++n) done_prev[n] = done[n];
         lds_sync();  // D
+        PGM_STAMP(7);
     }
+    PGM_STAMP_FLUSH;
     if (w == SW) finish_step(T - 1, (T - 1) & 1);
 
     // ---- env state and statistics back to HBM

@@ -12,15 +12,18 @@ from pgmorl_amd import _lib
 from pgmorl_amd.policy import new_policy
 from pgmorl_amd.runtime import TaskBatch
 
-P, N, T = int(os.environ.get('P', 40)), 4, 2048
-tb = TaskBatch('MO-Walker2d-v2', P, num_processes=N, num_steps=T)
+ENV = os.environ.get('ENV', 'MO-Walker2d-v2')
+HUM = 'Humanoid' in ENV
+P, N, T = int(os.environ.get('P', 20 if HUM else 40)), 8 if HUM else 4, 2048
+tb = TaskBatch(ENV, P, num_processes=N, num_steps=T)
 for p in range(P):
-    tb.set_task(p, new_policy(17, 6, 2).state_dict(), {}, None, [0.5, 0.5])
+    tb.set_task(p, new_policy(tb.O, tb.A, tb.K).state_dict(), {}, None, [0.5, 0.5])
 tb.env_reset()
 L = _lib.lib()
 buf = (C.c_ulonglong * 64)()
 SB = int(os.environ.get('STAMP_BLOCK', 0))  # workgroup sampled (update SPLIT: 2p = critic, 2p+1 = actor)
-for name in ('rollout', 'update', 'mfma', 'lanes'):
+UNITS = ('rollout', 'update', 'mfma', 'lanes', 'wide', 'wupd')
+for name in UNITS:
     getattr(L, f'pgm_debug_stamps_{name}')(buf, 1)
     getattr(L, f'pgm_debug_stamp_block_{name}')(SB)
 tb.iteration(0, 3e-4)
@@ -32,11 +35,20 @@ mnames = {0: 'stage rows', 1: 'pass end sync', 2: 'grad image rounds', 3: 'Adam'
           4: 'tile: L1 + L2 fwd', 5: 'tile: heads + loss', 6: 'tile: gWh, dH2, gW2', 7: 'tile: dH1, gW1'}
 lnames = {0: 'loop/top', 1: 'actor fwd', 6: 'sample', 7: 'dynamics', 2: 'accumulators + row', 3: 'barrier',
           4: 'stats', 5: 'emit'}
-for name, steps in (('rollout', T), ('update', 320), ('mfma', 320), ('lanes', T)):
+wnames = {0: 'noise + layer-1 slices', 1: 'barrier A', 2: 'L1 sum, L2, head, draw', 3: 'barrier C',
+          4: 'dynamics', 5: 'objective wave sums', 6: 'reset + ob_rms + emit', 7: 'stats wave + barrier D'}
+unames = {0: 'layer 1 (L2 stream)', 1: 'layer 2 + tanh', 2: 'heads + loss', 3: 'gWh, dH2, gW2, dH1',
+          4: 'pass barrier 1', 5: 'dW1 contraction', 6: 'pass barrier 2', 7: 'small-image reduction',
+          8: 'publish + flag wait', 9: 'gather partner', 10: 'sumsq + norm hand-off', 11: 'Adam (LDS + W1 HBM)'}
+for name, steps in (('rollout', T), ('update', 320), ('mfma', 320), ('lanes', T), ('wide', T), ('wupd', 320)):
+    if name == 'wupd':
+        names = unames
     if name == 'mfma':
         names = mnames
     if name == 'lanes':
         names = lnames
+    if name == 'wide':
+        names = wnames
     getattr(L, f'pgm_debug_stamps_{name}')(buf, 1)
     v = np.array(list(buf), dtype=np.float64)
     tot = v.sum()

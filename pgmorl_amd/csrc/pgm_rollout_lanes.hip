@@ -56,6 +56,15 @@ struct ActorLane {
         }
         b1 = prm[L.off[PGM_P_ACTOR_B1] + l];
         b2 = prm[L.off[PGM_P_ACTOR_B2] + l];
+        // the per-action constants are wave-uniform; kept in VGPRs (the SGPR file is the step loop's scarce
+        // resource: spilled SGPRs come back through v_readlane + s_nop every step)
+#pragma unroll
+        for (int j = 0; j < A; ++j) {
+            asm volatile("" : "+v"(bm[j]));
+            asm volatile("" : "+v"(ls[j]));
+            asm volatile("" : "+v"(sd[j]));
+            asm volatile("" : "+v"(rsd[j]));
+        }
     }
     // action mean of the fp32 row x (LDS, read by every lane) -> mu[A], wave-uniform.  h1 is this wave's
     // [H] LDS exchange row.  Ends with h1 free for reuse.
@@ -113,6 +122,16 @@ struct EnvLane {
         }
         d = fl ? g.d[o] : 0.0;
         c = fl ? g.c[o] : 0.0;
+#pragma unroll
+        for (int j = 0; j < A; ++j) {  // wave-uniform constants in VGPRs (see ActorLane::load)
+            asm volatile("" : "+v"(lo[j]));
+            asm volatile("" : "+v"(hi[j]));
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            asm volatile("" : "+v"(ebase[k]));
+            asm volatile("" : "+v"(ecoef[k]));
+        }
     }
     // s' = tanh(d*s + U clip(a) + c) for this lane's feature; raw objectives (wave-uniform):
     // obj_k = V_k . s' + ebase_k - ecoef_k * |clip(a)|^2   (the Walker form, environments/walker2d.py:23-25)

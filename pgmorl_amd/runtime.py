@@ -213,12 +213,22 @@ class TaskBatch:
             check(lib().pgm_normal_noise(self.noise.numel(), C.c_uint64(j), _ptr(self.noise), _stream()),
                   'pgm_normal_noise')
             noise = self.noise
+        perm_ready = None
+        if perms is None and overlap_eval:  # the permutations only feed the update: drawn beside the rollout
+            side = self.eval_stream  # (behind the previous evaluation, itself behind the previous update)
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                self.make_perms(j)
+                perm_ready = torch.cuda.Event()
+                perm_ready.record(side)
         self.rollout(j, noise=noise, carry=carry)
         self.gae()
         self.adv_normalize()
-        if perms is None:
+        if perms is None and perm_ready is None:
             self.make_perms(j)
         self.wait_eval()  # the previous overlapped evaluation still reads the parameters
+        if perm_ready is not None:
+            torch.cuda.current_stream().wait_event(perm_ready)
         self.ppo_update(perms)
         if not overlap_eval:
             self.evaluate(out=objs_out)

@@ -95,6 +95,40 @@ __device__ __forceinline__ double tanh_d2(double y) {
     return copysign(fma(-2.0, r, 1.0), y);
 }
 
+// fp64 lane-half / row folds of the transposing multi-value sum (pgm_common.hpp has the fp32 forms)
+__device__ __forceinline__ double pl32_fold_d(double a, double b) {
+    const auto lo = __builtin_amdgcn_permlane32_swap(__double2loint(a), __double2loint(b), false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap(__double2hiint(a), __double2hiint(b), false, false);
+    return __hiloint2double(hi[0], lo[0]) + __hiloint2double(hi[1], lo[1]);
+}
+__device__ __forceinline__ double pl16_fold_d(double a, double b) {
+    const auto lo = __builtin_amdgcn_permlane16_swap(__double2loint(a), __double2loint(b), false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap(__double2hiint(a), __double2hiint(b), false, false);
+    return __hiloint2double(hi[0], lo[0]) + __hiloint2double(hi[1], lo[1]);
+}
+__device__ __forceinline__ double row_sum16_d(double v) {
+    v += dpp_d<0x128>(v);
+    v += dpp_d<0x124>(v);
+    v += dpp_d<0x122>(v);
+    v += dpp_d<0x121>(v);
+    return v;
+}
+// M <= 4 simultaneous fp64 64-lane sums, results wave-uniform (the fp64 form of wave_sum64_multi): one
+// permlane32 fold per pair, one permlane16 fold of the pairs, one 16-lane row sum, one readlane pair per value
+template <int M>
+__device__ __forceinline__ void wave_sum64_d_multi(const double (&v)[M], double (&out)[M]) {
+    static_assert(M >= 1 && M <= 4, "1..4 values");
+    if constexpr (M == 1) {
+        out[0] = wave_sum64_d(v[0]);
+    } else {
+        auto at = [&](int i) { return i < M ? v[i] : 0.0; };
+        const double r = row_sum16_d(pl16_fold_d(pl32_fold_d(at(0), at(1)), pl32_fold_d(at(2), at(3))));
+        const int lane_of[4] = {0, 32, 16, 48};  // value i sits in row {0, 2, 1, 3}[i]
+#pragma unroll
+        for (int i = 0; i < M; ++i) out[i] = readlane_d(r, lane_of[i]);
+    }
+}
+
 template <int N_>
 __device__ __forceinline__ float sel_lane(const float (&v)[N_], int l) {
     float r = 0.f;

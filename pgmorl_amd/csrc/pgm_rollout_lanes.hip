@@ -141,7 +141,10 @@ struct EnvLane {
         for (int j = 0; j < A; ++j) pu[j] = U[j] * ac[j];
         const double sn = tanh_d(d * s + tree_sum(pu) + c);
 #pragma unroll
-        for (int k = 0; k < K; ++k) objraw[k] = wave_sum64_d(V[k] * sn) + ebase[k] - ecoef[k] * e2;
+        for (int k = 0; k < K; ++k) objraw[k] = V[k] * sn;
+        wave_sum64_d_multi<K>(objraw, objraw);
+#pragma unroll
+        for (int k = 0; k < K; ++k) objraw[k] += ebase[k] - ecoef[k] * e2;
         return sn;
     }
 };

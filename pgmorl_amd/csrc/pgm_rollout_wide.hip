@@ -52,24 +52,6 @@ struct WideSmem {
     double U[A][2 * WTH];                // SynthMO U^T, feature-contiguous (conflict-free per-thread reads)
 };
 
-// fp64 lane-half / row folds of the transposing multi-value sum (pgm_common.hpp has the fp32 forms)
-__device__ __forceinline__ double pl32_fold_d(double a, double b) {
-    const auto lo = __builtin_amdgcn_permlane32_swap(__double2loint(a), __double2loint(b), false, false);
-    const auto hi = __builtin_amdgcn_permlane32_swap(__double2hiint(a), __double2hiint(b), false, false);
-    return __hiloint2double(hi[0], lo[0]) + __hiloint2double(hi[1], lo[1]);
-}
-__device__ __forceinline__ double pl16_fold_d(double a, double b) {
-    const auto lo = __builtin_amdgcn_permlane16_swap(__double2loint(a), __double2loint(b), false, false);
-    const auto hi = __builtin_amdgcn_permlane16_swap(__double2hiint(a), __double2hiint(b), false, false);
-    return __hiloint2double(hi[0], lo[0]) + __hiloint2double(hi[1], lo[1]);
-}
-__device__ __forceinline__ double row_sum16_d(double v) {
-    v += dpp_d<0x128>(v);
-    v += dpp_d<0x124>(v);
-    v += dpp_d<0x122>(v);
-    v += dpp_d<0x121>(v);
-    return v;
-}
 // 16 simultaneous fp64 64-lane sums: after the folds, row R of y[j] holds value j + 4R; lane 16R writes it
 __device__ __forceinline__ void wave_sum16_d(const double (&v)[16], double* out) {
     double x[8], y[4];

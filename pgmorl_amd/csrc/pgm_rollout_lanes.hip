@@ -301,7 +301,12 @@ __global__ __launch_bounds__(256) void rollout_lane_kernel(RolloutArgs a) {
             if (step + NCH < T) load_eps(step / NCH + 1);
             wave_lds_fence_r();
         }
-        itot = 1.0 / (cnt + (double)NN);
+        {  // 1 / (count + N): hardware reciprocal + two Newton steps (~1 ulp; the Chan merge multiplies by it)
+            const double tot = cnt + (double)NN;
+            double r = __builtin_amdgcn_rcp(tot);
+            r = fma(r, fma(-tot, r, 1.0), r);
+            itot = fma(r, fma(-tot, r, 1.0), r);
+        }
         PGM_STAMP(0);
 #pragma unroll
         for (int e = 0; e < NE; ++e) {
@@ -381,13 +386,13 @@ __global__ __launch_bounds__(256) void rollout_lane_kernel(RolloutArgs a) {
             if (n >= NN) break;
             if (role == 0) {
                 double v = s_o[e];
-                if (nc.use_ob) v = clipd((v - mean) * inv, -nc.clipob, nc.clipob);
+                if (nc.use_ob) v = clipd_hw((v - mean) * inv, -nc.clipob, nc.clipob);
                 const float f = (float)v;  // VecPyTorch .float() (envs.py:192)
                 S.x[n][l] = f;
                 obs[((size_t)(step + 1) * NN + n) * O + l] = f;
             } else if (role == 1) {
                 double r = sel_lane_d(objraw[e], ko);
-                if (nc.use_obj) r = clipd(r * inv, -nc.cliprew, nc.cliprew);
+                if (nc.use_obj) r = clipd_hw(r * inv, -nc.cliprew, nc.cliprew);
                 rew[((size_t)step * NN + n) * K + ko] = (float)r;
             }
             if (l == 0) {

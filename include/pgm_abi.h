@@ -172,11 +172,15 @@ int pgm_adv_normalize(const pgm_dims* d, const pgm_rollout_buf* rb, const double
 /* PPO.update minibatch loop: ppo_epoch x (T*N / (T*N/num_mini_batch)) Adam steps per task, rows
  * perms[e][b*mb:(b+1)*mb].  params/adam_m/adam_v [P][L] updated in place, adam_step [P] int32
  * incremented per step, lr [P].  stats [P][3] = mean (value_loss, action_loss, dist_entropy).
- * workspace: caller-owned device bytes (pgm_ppo_update_workspace_bytes), reset inside the call on
- * `stream`; with it the critic and actor towers of a task run on two CUs that exchange the squared
- * gradient norm per minibatch (used when 2P <= CU count).  NULL: one workgroup per task.
+ * workspace: caller-owned device bytes (pgm_ppo_update_workspace_bytes), required (PGM_E_INVALID_ARG
+ * when NULL), reset inside the call on `stream`.  The critic and actor towers of a task run on separate
+ * CUs that exchange the squared gradient norm per minibatch step; each tower is further split over two
+ * CUs (half the minibatch rows each, gradient images added through the workspace) while
+ * 16 * ceil(P/4) <= CU count.  obs_dim <= 32: tower images LDS-resident (falls back to 2 CUs per task,
+ * then 1, as P grows); obs_dim > 32 (Humanoid): layer 1 streamed from L2, needs 2P <= CU count
+ * (PGM_E_UNSUPPORTED otherwise: shard the tasks over more GPUs).  PGM_UPDATE_SPLIT=0/1/2 caps the split.
  * After the call, the 8-byte word at index 2P of the workspace is nonzero iff an exchange timed out
- * (the towers were not co-resident); the results of such a call are invalid. */
+ * (the workgroups were not co-resident); the results of such a call are invalid. */
 int pgm_ppo_update(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params, float* adam_m,
                    float* adam_v, int32_t* adam_step, const float* lr, const int32_t* perms,
                    const pgm_rollout_buf* rb, float* stats, void* workspace, pgm_stream_t stream);

@@ -6,9 +6,9 @@
 // off the step chain here too (value_kernel afterwards).
 //
 // Work split of one step (NN envs, 4 waves, lane l):
-//   1. layer 1 (O x 64 per env, the dominant MACs): wave w owns the k-slice [w*KW, w*KW + KW) of the inputs,
-//      its W1 rows live in registers (lane = hidden unit), every env's input row is an LDS broadcast, the
-//      products are packed fp32 FMAs (two k per instruction); per-wave partial sums go to LDS.   barrier A
+//   1. layer 1 (O x 64 per env, the dominant MACs): wave w owns the k-slice [w*KW, w*KW + KW) of the inputs
+//      and contracts it for all envs on the f32 MFMA (16x16x4: envs on rows, W1 slice as register-resident B
+//      operands); per-wave partial sums go to LDS.                                                  barrier A
 //   2. env n on wave n % 4: sums the 4 partials (fixed order) + bias, tanh -> h1 row (wave-local), layer 2
 //      with its W2 column in registers, the mean head as transposing DPP sums, then the Gaussian draw,
 //      log-prob and clipped action with lane a = action a; clipped actions (fp64) to LDS.          barrier C
@@ -38,10 +38,11 @@ template <int O, int K, int NN>
 constexpr bool wide_fit() { return O > 48 && O <= 2 * WTH && NN * K <= 16 && (K & (K - 1)) == 0; }
 
 typedef float f2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 template <int O, int A, int K, int NN>
 struct WideSmem {
-    alignas(16) float x[NN][wrow<O>()];  // normalised fp32 obs rows (zero padding beyond O)
+    alignas(16) float x[NN][wrow<O>() + 4];  // normalised fp32 obs rows (zero padding beyond O; +4: bank stagger)
     alignas(16) float zp[WW][NN][H];     // layer-1 partial sums, one k-slice per wave
     alignas(16) float h1[NN][H];         // per-env layer-1 row (written / read by wave n)
     float mu[NN][32];                    // per-env action means (lane-distribution staging)
@@ -115,14 +116,18 @@ __global__ __launch_bounds__(WTH) void rollout_wide_kernel(RolloutArgs a) {
     float* bad = a.rb.bad_masks + (size_t)p * (T + 1) * NN;
     const int maxs = a.spec.max_episode_steps;
 
-    // ---- policy registers: W1 rows of this wave's k-slice (lane = unit), W2 column and head row of unit l
-    f2 w1[KW / 2];
+    // ---- policy registers: the B operands of this wave's layer-1 MFMAs (v_mfma_f32_16x16x4_f32: lane (j, g) =
+    // (l & 15, l >> 4) holds W1^T[k][16 jb + j] for k = w*KW + g*KQ + kk: k-slot g of step kk covers a contiguous
+    // KQ-feature run, so the A operand (the env rows) is three float4 LDS reads per lane per 12 steps),
+    // the W2 column and head row of unit l
+    constexpr int KQ = KW / 4;
+    const int lj = l & 15, lg = l >> 4;
+    float wb[KQ][4];
 #pragma unroll
-    for (int i = 0; i < KW / 2; ++i) {
-        const int k0 = min(w * KW + 2 * i, O - 2);  // rows >= O: weight 0 (their inputs are 0 as well)
-        const float2 v = make_float2(prm[L.off[PGM_P_ACTOR_W1] + k0 * H + l], prm[L.off[PGM_P_ACTOR_W1] + (k0 + 1) * H + l]);
-        const bool in0 = w * KW + 2 * i < O, in1 = w * KW + 2 * i + 1 < O;
-        w1[i] = f2{in0 ? v.x : 0.f, in1 ? v.y : 0.f};
+    for (int kk = 0; kk < KQ; ++kk) {
+        const int k = w * KW + lg * KQ + kk;
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb) wb[kk][jb] = k < O ? prm[L.off[PGM_P_ACTOR_W1] + k * H + 16 * jb + lj] : 0.f;
     }
     float w2[H], wm[A];
 #pragma unroll
@@ -289,23 +294,34 @@ __global__ __launch_bounds__(WTH) void rollout_wide_kernel(RolloutArgs a) {
             store_eps(cb);
             if (step + WNCH < T) load_eps(step / WNCH + 1);
         }
-        // ---- 1. layer-1 partial sums of this wave's k-slice, every env (packed fp32 FMAs over k pairs)
+        // ---- 1. layer-1 partial sums of this wave's k-slice for every env on the f32 matrix cores: rows = envs
+        // (16-row tiles, rows >= NN zero), 4 column blocks of 16 units, KQ k-steps; the operands come from
+        // registers (W1) and one contiguous LDS run per lane (x), not 64-lane broadcasts of every input
         {
-            f2 acc[NN];
+            f32x4 acc[4];
 #pragma unroll
-            for (int n = 0; n < NN; ++n) acc[n] = f2{0.f, 0.f};
+            for (int jb = 0; jb < 4; ++jb) acc[jb] = f32x4{0.f, 0.f, 0.f, 0.f};
+            const bool arow = lj < NN;
+            const float* xrow = &S.x[arow ? lj : 0][w * KW + lg * KQ];
 #pragma unroll
-            for (int i = 0; i < KW; i += 4) {
+            for (int q = 0; q < KQ; q += 4) {
+                float4 xv = *reinterpret_cast<const float4*>(xrow + q);
+                if (!arow) xv = make_float4(0.f, 0.f, 0.f, 0.f);
+                const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
 #pragma unroll
-                for (int n = 0; n < NN; ++n) {
-                    const float4 xv = *reinterpret_cast<const float4*>(&S.x[n][w * KW + i]);
-                    acc[n] = __builtin_elementwise_fma(f2{xv.x, xv.y}, w1[i / 2], acc[n]);
-                    acc[n] = __builtin_elementwise_fma(f2{xv.z, xv.w}, w1[i / 2 + 1], acc[n]);
-                }
-                if ((i & 15) == 12) __builtin_amdgcn_sched_barrier(0);  // bound the hoisted input reads
+                for (int e = 0; e < 4; ++e)
+#pragma unroll
+                    for (int jb = 0; jb < 4; ++jb)
+                        acc[jb] = __builtin_amdgcn_mfma_f32_16x16x4f32(xs[e], wb[q + e][jb], acc[jb], 0, 0, 0);
             }
+            // C layout: lane (j, g), register r = Z1[row 4g + r][16 jb + j]
+            if (4 * lg < NN) {
 #pragma unroll
-            for (int n = 0; n < NN; ++n) S.zp[w][n][l] = acc[n].x + acc[n].y;
+                for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (4 * lg + r < NN) S.zp[w][4 * lg + r][16 * jb + lj] = acc[jb][r];
+            }
         }
         PGM_STAMP(0);
         lds_sync();  // A

@@ -70,6 +70,7 @@ struct WSmem {
     SmallImg<A, K> Pm;     // parameters but layer 1
     float MV[2 * IMG];     // Adam exp_avg | exp_avg_sq of the small image
     float dout[4][TS][Q];  // per-wave dL/d(head output) of the current tile
+    float dls[4][TS][Q];   // per-wave per-sample dL/d(logstd) of the current tile (actor)
     float aiv[A];          // actor 1 / std^2
     float red[16];
     int32_t rowid[4][TS];  // rollout rows of every wave's tile of the current pass
@@ -194,7 +195,8 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
         for (int bb = 0; bb < nb; ++bb) {
             const int32_t* perm = a.perms + (size_t)e * B + bb * mb + r0;
             f32x16 gW2[2][2], gWh[2], dW1[NKW][2];
-            float gB1[2], gB2[2], gBh[Q], gLs[A];
+            float gB1[2], gB2[2];
+            float gsm = 0.f;  // lanes q < Q: head-bias gradient q; lanes 32 + q (actor): logstd gradient q
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
 #pragma unroll
@@ -204,10 +206,6 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
             }
 #pragma unroll
             for (int j = 0; j < NKW; ++j) dW1[j][0] = dW1[j][1] = f32x16{0};
-#pragma unroll
-            for (int q = 0; q < Q; ++q) gBh[q] = 0.f;
-#pragma unroll
-            for (int q = 0; q < A; ++q) gLs[q] = 0.f;
             float lsum = 0.f;
 
             for (int ps = 0; ps < npass; ++ps) {
@@ -353,17 +351,20 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
                             const float diff = pa[q] - outv[q];
                             const float iv = S.aiv[q];
                             dO[q] = dlp * diff * iv;
-                            if (h == 0) gLs[q] += dlp * (diff * diff * iv - 1.f);
+                            if (h == 0) S.dls[w][c][q] = dlp * (diff * diff * iv - 1.f);
                         }
                     }
                     if (h == 0) {
 #pragma unroll
-                        for (int q = 0; q < Q; ++q) {
-                            gBh[q] += dO[q];
-                            S.dout[w][c][q] = dO[q];
-                        }
+                        for (int q = 0; q < Q; ++q) S.dout[w][c][q] = dO[q];
                     }
                     wave_lds_fence();
+                    // per-column sums of the tile: lane q sums dO[.][q], lane 32 + q the logstd terms
+                    if (c < (h == 0 ? Q : (m == 1 ? A : 0))) {
+                        const float* src = (h == 0 ? &S.dout[w][0][0] : &S.dls[w][0][0]) + c;
+#pragma unroll 8
+                        for (int cc = 0; cc < TS; ++cc) gsm += src[cc * Q];
+                    }
                     PGM_STAMP(2);
                     // ---- head-weight grads on the MFMA: gWh^T[u][q] += sum_s H2[s][u] dO[s][q]
                     // (A = H2 in the C layout from tile B: lane u, samples rowof(r, 0/1); B = dO, lane q)
@@ -477,10 +478,6 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
                 gB1[i] = half_sum(gB1[i]);
                 gB2[i] = half_sum(gB2[i]);
             }
-#pragma unroll
-            for (int q = 0; q < Q; ++q) gBh[q] = wave_sum64(gBh[q]);
-#pragma unroll
-            for (int q = 0; q < A; ++q) gLs[q] = wave_sum64(gLs[q]);
             lsum = wave_sum64(lsum);
             float ent = 0.f;
 #pragma unroll
@@ -522,15 +519,12 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
                             acc(oB2 + i * TS + c, gB2[i]);
                         }
                     }
+                    if (h == 0 && c < NQ) acc(oBh + c, gsm);
+                    if (m == 1 && h == 1 && c < A) {  // -entropy_coef * d(mean entropy)/d logstd enters once (ppo.py:98)
+                        const float ec = add ? 0.f : a.hp.entropy_coef;
+                        acc(oLs + c, gsm - ec);
+                    }
                     if (l == 0) {
-#pragma unroll
-                        for (int q = 0; q < Q; ++q)
-                            if (q < NQ) acc(oBh + q, gBh[q]);
-                        if (m == 1) {  // -entropy_coef * d(mean entropy)/d logstd enters once (ppo.py:98)
-                            const float ec = add ? 0.f : a.hp.entropy_coef;
-#pragma unroll
-                            for (int q = 0; q < A; ++q) acc(oLs + q, gLs[q] - ec);
-                        }
                         S.red[8 + w] = lsum;
                     }
                     if (!add) {  // padding slots of a freshly written image

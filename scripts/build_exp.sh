@@ -1,0 +1,20 @@
+# diagnostic variants of one source: bash scripts/build_exp.sh <source.hip> <n>... -> pgmorl_amd/libpgm_exp<n>.so
+set -e
+src=$1; shift
+cd "$(dirname "$0")/.."
+python -m pgmorl_amd.build --stamps > /dev/null
+for n in "$@"; do
+  mkdir -p pgmorl_amd/build_exp$n
+  objs=""
+  for o in pgmorl_amd/build_stamps/*.o; do
+    b=$(basename $o)
+    if [ "$b" = "$src.o" ]; then
+      /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I include -DPGM_STAMPS -DPGM_EXP=$n -c pgmorl_amd/csrc/$src -o pgmorl_amd/build_exp$n/$b
+      objs="$objs pgmorl_amd/build_exp$n/$b"
+    else
+      objs="$objs $o"
+    fi
+  done
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $objs -o pgmorl_amd/libpgm_exp$n.so
+  echo pgmorl_amd/libpgm_exp$n.so
+done

@@ -6,3 +6,5 @@ PGM_UPDATE_SPLIT=1 timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.
 tail -1 gpurun_out/t_wide1.log
 timeout -k 10 300 python -u bench.py --env-name MO-Humanoid-v2 --tasks 20 --num-processes 8 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/bench_hum.json 2> gpurun_out/bench_hum.err || { tail -30 gpurun_out/bench_hum.err; exit 1; }
 cat gpurun_out/bench_hum.json
+ENV=MO-Humanoid-v2 PGM_LIB=pgmorl_amd/libpgm_stamps.so timeout -k 10 200 python -u scripts/stamps.py > gpurun_out/stamps_hum.txt 2>&1 || { tail -30 gpurun_out/stamps_hum.txt; exit 1; }
+sed -n '/== wupd/,$p' gpurun_out/stamps_hum.txt

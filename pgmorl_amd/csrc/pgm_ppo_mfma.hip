@@ -120,6 +120,7 @@ struct MSmemT {
     alignas(16) float RB[NBUF][SBk * RSL]; // packed rows of the current / next pass
     int32_t IB[2][SBk];                    // sample indices of the next two passes
     float dout[4][TS][Q];                  // per-wave dL/d(head output) of the current tile
+    float dls[4][TS][Q];                   // per-wave per-sample dL/d(logstd) of the current tile (actor)
     float aiv[A];                          // actor 1 / std^2 = exp(-2 logstd), refreshed by Adam
     float red[16];
     union Big {                            // transpose tiles during the passes, gradient images after
@@ -264,7 +265,8 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
     for (int e = 0; e < E; ++e) {
         for (int bb = 0; bb < nb; ++bb) {
             f32x16 gW2[2][2], gW1[2];  // [in tile][out tile], [out tile] (O <= 32: one in tile)
-            float gWh[2][Q], gB1[2], gB2[2], gBh[Q], gLs[A];
+            float gWh[2][Q], gB1[2], gB2[2];
+            float gsm = 0.f;  // lanes q < Q: head-bias gradient q; lanes 32 + q (actor): logstd gradient q
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
 #pragma unroll
@@ -274,10 +276,6 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
 #pragma unroll
                 for (int q = 0; q < Q; ++q) gWh[i][q] = 0.f;
             }
-#pragma unroll
-            for (int q = 0; q < Q; ++q) gBh[q] = 0.f;
-#pragma unroll
-            for (int q = 0; q < A; ++q) gLs[q] = 0.f;
             float lsum = 0.f;
 
             for (int s0 = 0; s0 < mbs; s0 += SBk, ++gp) {
@@ -396,17 +394,21 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                             const float diff = rowf(rt, c, O + q) - outv[q];
                             const float iv = S.aiv[q];
                             dO[q] = dlp * diff * iv;
-                            if (h == 0) gLs[q] += dlp * (diff * diff * iv - 1.f);
+                            if (h == 0) S.dls[w][c][q] = dlp * (diff * diff * iv - 1.f);
                         }
                     }
                     if (h == 0) {
 #pragma unroll
-                        for (int q = 0; q < Q; ++q) {
-                            gBh[q] += dO[q];
-                            S.dout[w][c][q] = dO[q];
-                        }
+                        for (int q = 0; q < Q; ++q) S.dout[w][c][q] = dO[q];
                     }
                     wave_lds_fence();
+                    // per-column sums of the tile (registers: one accumulator per lane instead of Q + A):
+                    // lane q sums dO[.][q], lane 32 + q the logstd terms
+                    if (c < (h == 0 ? Q : (m == 1 ? A : 0))) {
+                        const float* src = (h == 0 ? &S.dout[w][0][0] : &S.dls[w][0][0]) + c;
+#pragma unroll 8
+                        for (int cc = 0; cc < TS; ++cc) gsm += src[cc * Q];
+                    }
                     PGM_STAMP(5);
                     // ---- head-weight grads (VALU, C layout): gWh[ob][q] += sum_r H2[s][u] dO[s][q]
 #pragma unroll
@@ -498,16 +500,12 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
 #pragma unroll
                 for (int q = 0; q < Q; ++q) gWh[i][q] = half_sum(gWh[i][q]);
             }
-            // per-sample partials (held by half 0 lanes): 64-lane sums (half 1 holds zeros)
-#pragma unroll
-            for (int q = 0; q < Q; ++q) gBh[q] = wave_sum64(gBh[q]);
-#pragma unroll
-            for (int q = 0; q < A; ++q) gLs[q] = wave_sum64(gLs[q]);
             lsum = wave_sum64(lsum);
             // entropy with the logstd of this step (before Adam)
             float ent = 0.f;
 #pragma unroll
             for (int q = 0; q < A; ++q) ent += 0.5f + LOG_SQRT_2PI + lstd[q];
+            PGM_STAMP(12);
 
             // ---- gradient images.  SPLIT: waves 1 / 3 store their partials into GA[0] / GA[1], then
             // waves 0 / 2 add theirs; g = GA[0] + GA[1].  Joint: the sh=1 wave of tower m stores into
@@ -571,17 +569,12 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                             for (int j = 0; j < NU; ++j) Gt[idx[j]] = val[j];
                         }
                     }
-                    if (l == 0) {
-#pragma unroll
-                        for (int q = 0; q < Q; ++q)
-                            if (q < NQ) acc(oBh + q, gBh[q]);
-                        if (m == 1) {  // -entropy_coef * d(mean entropy)/d logstd enters once (ppo.py:98)
-                            const float ec = add ? 0.f : a.hp.entropy_coef;
-#pragma unroll
-                            for (int q = 0; q < A; ++q) acc(oLs + q, gLs[q] - ec);
-                        }
-                        S.red[8 + w] = lsum;
+                    if (h == 0 && c < NQ) acc(oBh + c, gsm);
+                    if (m == 1 && h == 1 && c < A) {  // -entropy_coef * d(mean entropy)/d logstd enters once (ppo.py:98)
+                        const float ec = add ? 0.f : a.hp.entropy_coef;
+                        acc(oLs + c, gsm - ec);
                     }
+                    if (l == 0) S.red[8 + w] = lsum;
                     if (!add) {  // padding slots of a freshly written image
                         Gt[oW2 + l * SCR + H] = 0.f;
                         for (int q = NQ; q < Q; ++q) Gt[oWh + q * H + l] = 0.f;
@@ -589,6 +582,7 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                         if (m == 0 && l < A) Gt[oLs + l] = 0.f;
                     }
                 }
+                PGM_STAMP(13 + stage);
                 lds_sync_m();
             }
             PGM_STAMP(2);

@@ -507,14 +507,17 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
             for (int q = 0; q < A; ++q) ent += 0.5f + LOG_SQRT_2PI + lstd[q];
             PGM_STAMP(12);
 
-            // ---- gradient images.  SPLIT: waves 1 / 3 store their partials into GA[0] / GA[1], then
-            // waves 0 / 2 add theirs; g = GA[0] + GA[1].  Joint: the sh=1 wave of tower m stores into
-            // GA[m], the sh=0 wave adds; g = GA[m].  Fixed order => deterministic sums.
-            for (int stage = 0; stage < 2; ++stage) {
-                const bool mine = SPLIT ? ((w & 1) != stage) : (sh != stage);
-                if (mine) {
-                    float* Gt = S.big.GA[SPLIT ? (w >> 1) : m];
+            // ---- gradient images.  The two waves of a pair (SPLIT: waves 0/1 -> GA[0], 2/3 -> GA[1]; joint: the
+            // two waves of tower m -> GA[m]) split the image in two halves: in stage 0 each stores its partial of
+            // one half, in stage 1 it adds its partial of the other half; g = GA[0] + GA[1] (joint: GA[m]).
+            // Every element is (partial of one wave) + (partial of the other): deterministic.
+            if (l == 0) S.red[8 + w] = lsum;
+            {
+                const int pr = SPLIT ? (w & 1) : sh;  // position in the pair
+                float* Gt = S.big.GA[SPLIT ? (w >> 1) : m];
+                for (int stage = 0; stage < 2; ++stage) {
                     const bool add = stage == 1;
+                    const int half = (stage == 0) == (pr == 1) ? 0 : 1;  // image half handled in this stage
                     auto acc = [&](int idx, float val) { Gt[idx] = add ? Gt[idx] + val : val; };
                     // 16-register blocks: all reads of a block are issued before its writes, so the
                     // read-modify-write pays one LDS latency per block, not one per element
@@ -531,59 +534,58 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                         }
                     };
 #pragma unroll
-                    for (int ib = 0; ib < 2; ++ib)
+                    for (int i = 0; i < 2; ++i) {
+                        if (i != half) continue;
 #pragma unroll
                         for (int ob = 0; ob < 2; ++ob)
-                            acc16([&](int r) { return oW2 + (ib * TS + rowof(r, h)) * SCR + ob * TS + c; }, gW2[ib][ob]);
-                    // rows k >= O of dW1 are exactly zero (A operand 0); they go to distinct W2 padding
-                    // slots (column H of row k), which are re-zeroed below
-#pragma unroll
-                    for (int hb = 0; hb < 2; ++hb)
+                            acc16([&](int r) { return oW2 + (i * TS + rowof(r, h)) * SCR + ob * TS + c; }, gW2[i][ob]);
+                        // rows k >= O of dW1 are exactly zero (A operand 0); they go to distinct W2 padding
+                        // slots (column H of row k), which hold zeros
                         acc16([&](int r) {
                             const int k = rowof(r, h);
-                            return k < O ? k * H + hb * TS + c : oW2 + k * SCR + H;
-                        }, gW1[hb]);
-                    if (h == 0) {  // per-unit sums: b1, b2 and the head weights (2 x (2 + Q) values)
-                        constexpr int NU = 2 * (2 + Q);
-                        float val[NU], tmp[NU];
-                        int idx[NU];
-#pragma unroll
-                        for (int i = 0; i < 2; ++i) {
-                            idx[i * (2 + Q)] = oB1 + i * TS + c;
-                            val[i * (2 + Q)] = gB1[i];
-                            idx[i * (2 + Q) + 1] = oB2 + i * TS + c;
-                            val[i * (2 + Q) + 1] = gB2[i];
+                            return k < O ? k * H + i * TS + c : oW2 + k * SCR + H;
+                        }, gW1[i]);
+                        if (h == 0) {  // per-unit sums of unit block i: b1, b2 and the head weights
+                            constexpr int NU = 2 + Q;
+                            float val[NU], tmp[NU];
+                            int idx[NU];
+                            idx[0] = oB1 + i * TS + c;
+                            val[0] = gB1[i];
+                            idx[1] = oB2 + i * TS + c;
+                            val[1] = gB2[i];
 #pragma unroll
                             for (int q = 0; q < Q; ++q) {  // rows q >= NQ are padding (zeroed below)
-                                idx[i * (2 + Q) + 2 + q] = oWh + q * H + i * TS + c;
-                                val[i * (2 + Q) + 2 + q] = q < NQ ? gWh[i][q] : 0.f;
+                                idx[2 + q] = oWh + q * H + i * TS + c;
+                                val[2 + q] = q < NQ ? gWh[i][q] : 0.f;
+                            }
+                            if (add) {
+#pragma unroll
+                                for (int j = 0; j < NU; ++j) tmp[j] = Gt[idx[j]];
+#pragma unroll
+                                for (int j = 0; j < NU; ++j) Gt[idx[j]] = tmp[j] + val[j];
+                            } else {
+#pragma unroll
+                                for (int j = 0; j < NU; ++j) Gt[idx[j]] = val[j];
                             }
                         }
-                        if (add) {
-#pragma unroll
-                            for (int j = 0; j < NU; ++j) tmp[j] = Gt[idx[j]];
-#pragma unroll
-                            for (int j = 0; j < NU; ++j) Gt[idx[j]] = tmp[j] + val[j];
-                        } else {
-#pragma unroll
-                            for (int j = 0; j < NU; ++j) Gt[idx[j]] = val[j];
+                    }
+                    if (half == 1) {
+                        if (h == 0 && c < NQ) acc(oBh + c, gsm);
+                        if (m == 1 && h == 1 && c < A) {  // -entropy_coef * d(mean entropy)/d logstd enters once (ppo.py:98)
+                            const float ec = add ? 0.f : a.hp.entropy_coef;
+                            acc(oLs + c, gsm - ec);
+                        }
+                        if (!add) {  // padding slots of a freshly written image
+                            Gt[oW2 + l * SCR + H] = 0.f;
+                            for (int q = NQ; q < Q; ++q) Gt[oWh + q * H + l] = 0.f;
+                            if (l >= NQ && l < Q) Gt[oBh + l] = 0.f;
+                            if (m == 0 && l < A) Gt[oLs + l] = 0.f;
                         }
                     }
-                    if (h == 0 && c < NQ) acc(oBh + c, gsm);
-                    if (m == 1 && h == 1 && c < A) {  // -entropy_coef * d(mean entropy)/d logstd enters once (ppo.py:98)
-                        const float ec = add ? 0.f : a.hp.entropy_coef;
-                        acc(oLs + c, gsm - ec);
-                    }
-                    if (l == 0) S.red[8 + w] = lsum;
-                    if (!add) {  // padding slots of a freshly written image
-                        Gt[oW2 + l * SCR + H] = 0.f;
-                        for (int q = NQ; q < Q; ++q) Gt[oWh + q * H + l] = 0.f;
-                        if (l >= NQ && l < Q) Gt[oBh + l] = 0.f;
-                        if (m == 0 && l < A) Gt[oLs + l] = 0.f;
-                    }
+                    PGM_STAMP(13 + stage);
+                    lds_sync_m();
+                    if (stage == 0) PGM_STAMP(15);
                 }
-                PGM_STAMP(13 + stage);
-                lds_sync_m();
             }
             PGM_STAMP(2);
             constexpr int NV4 = IMG / 4, TAIL = IMG - 4 * NV4;

@@ -9,7 +9,7 @@ for n in "$@"; do
   for o in pgmorl_amd/build_stamps/*.o; do
     b=$(basename $o)
     if [ "$b" = "$src.o" ]; then
-      /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I include -DPGM_STAMPS -DPGM_EXP=$n -c pgmorl_amd/csrc/$src -o pgmorl_amd/build_exp$n/$b
+      /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I include -DPGM_STAMPS -DPGM_EXP=$n $EXTRA -c pgmorl_amd/csrc/$src -o pgmorl_amd/build_exp$n/$b
       objs="$objs pgmorl_amd/build_exp$n/$b"
     else
       objs="$objs $o"

@@ -33,7 +33,7 @@ names = {0: "loop/top", 1: 'policy fwd', 2: 'store val + sample', 3: 'logp + dyn
 mnames = {0: 'stage rows', 1: 'pass end sync', 2: 'grad image rounds', 3: 'Adam', 8: 'sumsq', 9: 'norm exchange',
           10: 'half image publish + drain', 11: 'flag hand-off + image gather',
           4: 'tile: L1 + L2 fwd', 5: 'tile: heads + loss', 6: 'tile: gWh, dH2, gW2', 7: 'tile: dH1, gW1',
-          12: 'image: lane sums', 13: 'image: stage 0 work', 14: 'image: stage 1 work'}
+          12: 'image: lane sums', 13: 'image: stage 0 work', 14: 'image: stage 1 work', 15: 'image: stage 0 barrier'}
 lnames = {0: 'loop/top', 1: 'actor fwd', 6: 'sample', 7: 'dynamics', 2: 'accumulators + row', 3: 'barrier',
           4: 'stats', 5: 'emit'}
 wnames = {0: 'noise + layer-1 slices', 1: 'barrier A', 2: 'L1 sum, L2, head, draw', 3: 'barrier C',

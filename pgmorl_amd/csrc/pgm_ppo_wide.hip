@@ -483,11 +483,15 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
 #pragma unroll
             for (int q = 0; q < A; ++q) ent += 0.5f + LOG_SQRT_2PI + lstd[q];
 
-            // ---- small-image gradients: waves 1 / 3 store into GA[0] / GA[1], then waves 0 / 2 add theirs
-            for (int stage = 0; stage < 2; ++stage) {
-                if ((w & 1) != stage) {
-                    float* Gt = S.big.GA[w >> 1];
+            // ---- small-image gradients: waves 0/1 -> GA[0], 2/3 -> GA[1]; the two waves of a pair split the
+            // image in two halves: in stage 0 each stores its partial of one half, in stage 1 it adds its partial
+            // of the other half (every element = one wave's partial + the other's: deterministic)
+            if (l == 0) S.red[8 + w] = lsum;
+            {
+                float* Gt = S.big.GA[w >> 1];
+                for (int stage = 0; stage < 2; ++stage) {
                     const bool add = stage == 1;
+                    const int half = (stage == 0) == ((w & 1) == 1) ? 0 : 1;
                     auto acc = [&](int idx, float val) { Gt[idx] = add ? Gt[idx] + val : val; };
                     auto acc16 = [&](auto idx, const f32x16& val) {
                         if (add) {
@@ -502,38 +506,32 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
                         }
                     };
 #pragma unroll
-                    for (int ib = 0; ib < 2; ++ib)
+                    for (int ib = 0; ib < 2; ++ib) {
+                        if (ib != half) continue;
 #pragma unroll
                         for (int ob = 0; ob < 2; ++ob)
                             acc16([&](int r) { return (ib * TS + rowof(r, h)) * SCR + ob * TS + c; }, gW2[ib][ob]);
-                    // head weights: gWh[ob] row rowof(r,h) = unit ob*32 + rowof, column c = output q (c < Q)
-                    if (c < Q) {
-#pragma unroll
-                        for (int ob = 0; ob < 2; ++ob)
-                            acc16([&](int r) { return oWh + c * H + ob * TS + rowof(r, h); }, gWh[ob]);
-                    }
-                    if (h == 0) {
-#pragma unroll
-                        for (int i = 0; i < 2; ++i) {
-                            acc(oB1 + i * TS + c, gB1[i]);
-                            acc(oB2 + i * TS + c, gB2[i]);
+                        // head weights: gWh[ob] row rowof(r,h) = unit ob*32 + rowof, column c = output q (c < Q)
+                        if (c < Q) acc16([&](int r) { return oWh + c * H + ib * TS + rowof(r, h); }, gWh[ib]);
+                        if (h == 0) {
+                            acc(oB1 + ib * TS + c, gB1[ib]);
+                            acc(oB2 + ib * TS + c, gB2[ib]);
                         }
                     }
-                    if (h == 0 && c < NQ) acc(oBh + c, gsm);
-                    if (m == 1 && h == 1 && c < A) {  // -entropy_coef * d(mean entropy)/d logstd enters once (ppo.py:98)
-                        const float ec = add ? 0.f : a.hp.entropy_coef;
-                        acc(oLs + c, gsm - ec);
+                    if (half == 1) {
+                        if (h == 0 && c < NQ) acc(oBh + c, gsm);
+                        if (m == 1 && h == 1 && c < A) {  // -entropy_coef * d(mean entropy)/d logstd enters once (ppo.py:98)
+                            const float ec = add ? 0.f : a.hp.entropy_coef;
+                            acc(oLs + c, gsm - ec);
+                        }
+                        if (!add) {  // padding slots of a freshly written image
+                            Gt[l * SCR + H] = 0.f;
+                            if (l >= NQ && l < Q) Gt[oBh + l] = 0.f;
+                            if (m == 0 && l < A) Gt[oLs + l] = 0.f;
+                        }
                     }
-                    if (l == 0) {
-                        S.red[8 + w] = lsum;
-                    }
-                    if (!add) {  // padding slots of a freshly written image
-                        Gt[l * SCR + H] = 0.f;
-                        if (l >= NQ && l < Q) Gt[oBh + l] = 0.f;
-                        if (m == 0 && l < A) Gt[oLs + l] = 0.f;
-                    }
+                    lds_sync_m();
                 }
-                lds_sync_m();
             }
             // head rows q >= NQ (critic: 2..16) are exactly zero: dO[q] = 0 for them
             PGM_STAMP(7);

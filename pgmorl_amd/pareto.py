@@ -56,6 +56,8 @@ class OptGraph:
         self.weights, self.objs, self.delta_objs, self.prev, self.succ = [], [], [], [], []
 
     def insert(self, weights, objs, prev):
+        if hasattr(weights, 'detach'):  # a scalarisation's torch weight vector
+            weights = weights.detach().cpu().numpy()
         w = np.array(weights, dtype=np.float64)
         self.weights.append(w / np.linalg.norm(w))
         objs = np.array(objs, dtype=np.float64)

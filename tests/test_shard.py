@@ -68,3 +68,62 @@ def test_allgather_rows_gloo(ws, P):
     assert not errs, errs
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
 
+
+def _selection_worker(rank, ws, port, K, errq):
+    """Generation boundary on ws ranks (morl/morl.py:100-169): every rank owns a block of the offspring,
+    all-gathers the (objs, optgraph_id) rows, then runs prediction-guided selection itself from the same
+    seed; every rank must pick the same elites, weights and predictions as the single-process run."""
+    try:
+        import numpy as np
+        from pgmorl_amd import pareto, population
+        from pgmorl_amd.sample import WeightedSumScalarization
+        from tests.test_population import _EP, _S, _args, _history
+        os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+        dist.init_process_group('gloo', rank=rank, world_size=ws)
+        og, offspring = _history(K, 1)
+        P = len(offspring)
+        lo, hi = task_block(P, rank, ws)
+        mine = torch.tensor([list(s.objs) + [s.optgraph_id] for s in offspring[lo:hi]], dtype=torch.float64)
+        rows = allgather_rows(mine.reshape(hi - lo, K + 1), P).numpy()
+        gathered = [_S(r[:K], int(r[K])) for r in rows]
+
+        def select(samples):
+            args = _args(K, pbuffer_num=10 if K == 2 else 6, num_tasks=6, sparsity=0.5)
+            pop = population.make_population(args)
+            pop.update(samples)
+            objs = np.array([s.objs for s in samples])
+            ep = _EP([samples[i] for i in pareto.get_ep_indices(objs)])
+            np.random.seed(7)
+            el, sc, pr = pop.prediction_guided_selection(
+                args, 0, ep, og, WeightedSumScalarization(num_objs=K, weights=np.ones(K) / K))
+            return ([e.optgraph_id for e in el], np.array([s.weights.numpy() for s in sc]), np.array(pr))
+
+        ids, w, pr = select(gathered)
+        ids0, w0, pr0 = select(offspring)
+        assert ids == ids0 and np.array_equal(w, w0) and np.array_equal(pr, pr0)
+        pick = torch.tensor(np.concatenate([np.array(ids, dtype=np.float64), w.ravel(), pr.ravel()]))
+        every = [torch.empty_like(pick) for _ in range(ws)]
+        dist.all_gather(every, pick)
+        assert all(torch.equal(every[0], t) for t in every)
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # surfaced by the parent
+        errq.put(f'rank {rank}: {e!r}')
+        raise
+
+
+@pytest.mark.parametrize('ws,K', [(2, 2), (2, 3)])
+def test_selection_agrees_across_ranks_gloo(ws, K):
+    ctx = mp.get_context('spawn')
+    errq = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_selection_worker, args=(r, ws, port, K, errq)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    errs = []
+    while not errq.empty():
+        errs.append(errq.get())
+    assert not errs, errs
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]

@@ -36,7 +36,11 @@ def parse():
     ap.add_argument('--steps', type=int, default=5)
     ap.add_argument('--warmup', type=int, default=2)
     ap.add_argument('--env-name', default='MO-Walker2d-v2')
-    ap.add_argument('--tasks', type=int, default=40, help='tasks (policies) per GPU')
+    ap.add_argument('--tasks', type=int, default=40,
+                    help='tasks (policies) per GPU (--scaling weak) or in total (--scaling strong)')
+    ap.add_argument('--scaling', choices=['weak', 'strong'], default='weak',
+                    help='weak: --tasks on every GPU; strong: --tasks in total, split in contiguous blocks '
+                         '(shard.task_block, the SURVEY §8(e) 40 -> 20/10/5 partition)')
     ap.add_argument('--num-processes', type=int, default=4)
     ap.add_argument('--num-steps', type=int, default=2048)
     ap.add_argument('--ppo-epoch', type=int, default=10)
@@ -119,18 +123,29 @@ def main():
     from pgmorl_amd import envspec
     from pgmorl_amd.policy import new_policy
     from pgmorl_amd.runtime import TaskBatch
-    from pgmorl_amd.shard import allreduce_max
+    from pgmorl_amd.shard import allreduce_max, task_block
     spec = envspec.make_spec(args.env_name)
-    P, N, T, E, M = args.tasks, args.num_processes, args.num_steps, args.ppo_epoch, args.num_mini_batch
+    N, T, E, M = args.num_processes, args.num_steps, args.ppo_epoch, args.num_mini_batch
+    if args.scaling == 'strong':
+        G = args.tasks  # global population, rank r trains its contiguous block
+        lo, hi = task_block(G, rank, world)
+    else:
+        G = args.tasks * world
+        lo, hi = rank * args.tasks, (rank + 1) * args.tasks
+    P = hi - lo
+    if P <= 0:
+        raise SystemExit(f'rank {rank}: no tasks (global {G} over {world} ranks)')
     tb = TaskBatch(args.env_name, P, num_processes=N, num_steps=T, ppo_epoch=E, num_mini_batch=M, device=dev)
     torch.manual_seed(rank * 1000)
-    w = np.linspace(0, 1, P * world)[rank * P:(rank + 1) * P]
+    w = np.linspace(0, 1, G)[lo:hi]
     for p in range(P):
         pol = new_policy(spec['obs_dim'], spec['act_dim'], spec['obj_num'])
         tb.set_task(p, pol.state_dict(), {}, None, [w[p], 1 - w[p]] if spec['obj_num'] == 2 else
                     np.ones(spec['obj_num']) / spec['obj_num'])
     tb.env_reset()
-    gathered = torch.zeros(world * P, spec['obj_num'], dtype=torch.float64, device=dev)
+    per = -(-G // world)  # all-gather rows per rank (blocks padded to the largest)
+    gathered = torch.zeros(world * per, spec['obj_num'], dtype=torch.float64, device=dev)
+    mine = torch.zeros(per, spec['obj_num'], dtype=torch.float64, device=dev)
     total_updates = 5_000_000 // T // N
 
     history = []  # every iteration's gathered objective vectors (the offspring the EP is built from)
@@ -139,12 +154,20 @@ def main():
         # the evaluation of iteration j runs on the side stream beside iteration j+1's rollout; the objective
         # vectors are gathered on that stream behind it
         tb.iteration(j, 3e-4 * (1 - j / total_updates), carry=True, overlap_eval=not args.no_overlap_eval)
-        with torch.cuda.stream(tb.eval_stream if not args.no_overlap_eval else torch.cuda.current_stream()):
+        side = tb.eval_stream if not args.no_overlap_eval else torch.cuda.current_stream()
+        with torch.cuda.stream(side):
             if world > 1:
-                dist.all_gather_into_tensor(gathered, tb.objs)
+                mine[:P].copy_(tb.objs)
+                dist.all_gather_into_tensor(gathered, mine)
             else:
                 gathered.copy_(tb.objs)
-            history.append(gathered.clone())
+            history.append(torch.cat([gathered[r * per:r * per + task_block(G, r, world)[1] - task_block(G, r, world)[0]]
+                                      for r in range(world)]) if args.scaling == 'strong' else gathered.clone())
+            if not args.no_overlap_eval:
+                # the next PPO update waits on this event: the RCCL gather never runs beside the update's
+                # co-resident exchange workgroups
+                tb._eval_done = torch.cuda.Event()
+                tb._eval_done.record(side)
 
     j = 0
     for _ in range(args.warmup):
@@ -155,16 +178,16 @@ def main():
         dist.barrier()
     # per-launch duration of the dominant kernel (ppo_update) with events on the launch stream
     ev = []
-    orig_update = tb.ppo_update
+    orig_update = tb.ppo_update_launch
 
-    def timed_update(perms=None):
+    def timed_update():
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
-        orig_update(perms)
+        orig_update()
         e.record()
         ev.append((s, e))
 
-    tb.ppo_update = timed_update
+    tb.ppo_update_launch = timed_update
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -174,10 +197,11 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    tb.ppo_update = orig_update
+    tb.ppo_update_launch = orig_update
+    tb.check_update()  # a timed-out exchange invalidates the run: raises PGMError (after the timed region)
     upd_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
     dt, upd_ms = allreduce_max([dt, upd_ms], dev)  # the slowest rank defines the step
-    env_steps = world * P * N * T * args.steps
+    env_steps = G * N * T * args.steps  # every rank's tasks (the max-over-ranks time covers them all)
     value = env_steps / dt
     mf = mflops_per_row(spec['obs_dim'], spec['act_dim'], spec['obj_num'])
     upd_flop = P * T * N * E * 6 * mf          # fwd (2 M_f) + bwd (4 M_f) per row per epoch, one launch
@@ -192,11 +216,11 @@ def main():
             traffic = None
     out = {
         'metric': METRIC, 'value': value, 'unit': 'env steps/sec', 'n_gpus': world, 'steps': args.steps,
-        'warmup': args.warmup, 'ms_per_step': dt / args.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak',
+        'warmup': args.warmup, 'ms_per_step': dt / args.steps * 1e3, 'higher_is_better': True, 'scaling': args.scaling,
         'vs_baseline': None, 'dtype': 'fp32', 'data': f"synthetic (SynthMO-{args.env_name.split('-')[1]} env, reference-order random init)",
-        'config': {'workload': f'{args.env_name} (SynthMO) pop={P}/GPU, N={N}, T={T}, ppo_epoch={E}, '
-                               f'num_mini_batch={M}, eval_num=1, perf-mode device RNG',
-                   'env': args.env_name, 'tasks_per_gpu': P, 'global_tasks': P * world, 'num_processes': N,
+        'config': {'workload': f'{args.env_name} (SynthMO) pop={G} ({args.scaling} scaling, {P} tasks on rank 0), '
+                               f'N={N}, T={T}, ppo_epoch={E}, num_mini_batch={M}, eval_num=1, perf-mode device RNG',
+                   'env': args.env_name, 'tasks_per_gpu': P, 'global_tasks': G, 'num_processes': N,
                    'num_steps': T, 'ppo_epoch': E, 'num_mini_batch': M, 'parallelism': f'task-sharded x{world}'},
         'roofline': {'bound': 'mfma', 'kernel': 'ppo_update_mfma_kernel' if spec['obs_dim'] <= 32 else 'ppo_update_wide_kernel', 'achieved': achieved,
                      'peak': PEAK_FP32_TFLOPS, 'unit': 'TFLOP/s', 'frac': achieved / PEAK_FP32_TFLOPS,
@@ -211,7 +235,7 @@ def main():
                           'hbm_frac': value * bytes_per_env_step(spec['obs_dim'], spec['act_dim'], spec['obj_num'],
                                                                  E) / (world * PEAK_HBM_GBS * 1e9)},
     }
-    out['hypervolume'] = hypervolume(args, history, world * P * N * T * len(history))
+    out['hypervolume'] = hypervolume(args, history, G * N * T * len(history))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out['cpu_baseline'] = cb = cpu_baseline(args, spec)
         out['vs_96vcpu_extrapolated'] = value / cb['extrapolated_96vcpu']

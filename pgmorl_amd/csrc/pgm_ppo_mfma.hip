@@ -869,10 +869,10 @@ int launch_mode(const pgm_dims* d, const MArgs& a, hipStream_t stream) {
     auto kern = ppo_update_mfma_kernel<O, A, K, MODE>;
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update");
-    if (SPLIT) {  // norm granules, timeout flag (and MODE 2: the exchange slots) start at tag 0
-        e = hipMemsetAsync(a.ws, 0, ppo_flag_bytes(d->P) + (MODE == 2 ? ppo_xbuf_bytes(d) : 0), stream);
-        if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update (workspace reset)");
-    }
+    // norm granules, timeout flag (and MODE 2: the exchange slots) start at tag 0; MODE 0 resets the flag
+    // word too, so word 2P always reports THIS call
+    e = hipMemsetAsync(a.ws, 0, ppo_flag_bytes(d->P) + (MODE == 2 ? ppo_xbuf_bytes(d) : 0), stream);
+    if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update (workspace reset)");
     const int grid = MODE == 2 ? 16 * ((d->P + 3) / 4) : SPLIT ? 2 * d->P : d->P;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(MT), smem, stream, a);
     return launch_status("pgm_ppo_update");

@@ -567,6 +567,10 @@ extern "C" int pgm_ppo_update(const pgm_dims* d, const pgm_ppo_hparams* hp, floa
             auto kern = ppo_update_kernel<O, A, K>;
             hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
             if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update");
+            if (workspace) {  // no exchange in this kernel: the timeout word (2P) reads 0 for this call
+                e = hipMemsetAsync(workspace, 0, ppo_flag_bytes(d->P), (hipStream_t)stream);
+                if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update (workspace reset)");
+            }
             hipLaunchKernelGGL(kern, dim3(d->P), dim3(UT), smem, (hipStream_t)stream, a);
             return launch_status("pgm_ppo_update");
         }

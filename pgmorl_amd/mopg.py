@@ -20,7 +20,7 @@ import torch
 
 from .runtime import TaskBatch
 from .sample import DeviceSnapshot, RunningMeanStd, Sample
-from .shard import allgather_rows, task_block, world
+from .shard import allgather_rows, move_rows, owner_of, task_block, world
 
 
 def host_draws(j, T, N, A, E):
@@ -42,6 +42,7 @@ class MOPGPopulation:
         self.device = torch.device(device)
         self.rng = rng
         self.tb = None
+        self.moved_bytes = 0  # snapshot bytes this rank contributed to move_rows (multi-GPU)
 
     @property
     def layout(self):
@@ -111,17 +112,41 @@ class MOPGPopulation:
             ep['obj_rms'] = r
         return objs, ep, int(step)
 
+    def place(self, samples, dsts):
+        """Collective (every rank, same arguments): move each sample's snapshot to rank dsts[k] when it lives
+        elsewhere (shard.move_rows).  A no-op in one process."""
+        rank, ws = world()
+        if ws == 1:
+            return 0
+        snaps = [s.snapshot for s in samples]
+        moves = [(sn.owner if sn.owner is not None else -1, d) for sn, d in zip(snaps, dsts)]
+        local = {k: snaps[k].stacked() for k, (src, _) in enumerate(moves) if src == rank}
+        L = self.layout.total
+        got, nbytes = move_rows(moves, local, (3, L), torch.float32, self.device)
+        for k, rows in got.items():  # owner metadata stays as it is on every rank (identical move lists)
+            snaps[k].adopt(rows)
+        self.moved_bytes += nbytes
+        return nbytes
+
+    def materialize(self, samples, dst=0):
+        """Collective: gather the snapshots of ``samples`` onto rank ``dst`` (final/EP_policy_*.pt)."""
+        return self.place(samples, [dst] * len(samples))
+
     def run(self, task_batch, iteration, num_updates, start_time=None, log=print):
         """Every task's MOPG iterations [iteration, iteration + num_updates) -> all_offspring_batch.
 
         Multi-GPU (torch.distributed initialised, one process per GPU): this rank runs its contiguous
-        block of tasks (shard.task_block); at the end of the generation one all-gather of the offspring
-        snapshots (params / Adam state fp32, records fp64) gives every rank the full result."""
+        block of tasks (shard.task_block).  Elites whose snapshot lives on another rank are moved first
+        (place); at the end of the generation only the fp64 records (objectives + running statistics) are
+        all-gathered, and each offspring's parameters / Adam state stay on the rank that produced them
+        (remote handles elsewhere) until a later generation or the final writer needs them."""
         a = self.args
         P = len(task_batch)
         rank, ws = world()
         lo, hi = task_block(P, rank, ws)
         Pl = hi - lo
+        if ws > 1:
+            self.place([t.sample for t in task_batch], [owner_of(p, P, ws) for p in range(P)])
         total = int(a.num_env_steps) // a.num_steps // a.num_processes
         its = list(range(iteration, min(iteration + num_updates, total)))
         start_time = time.time() if start_time is None else start_time
@@ -149,23 +174,28 @@ class MOPGPopulation:
                     log(f'[RL] Updates {j + 1}, num timesteps {steps}, FPS {int(steps / max(dt, 1e-9))}, '
                         f'time {dt:.2f} seconds (x{P} tasks on {ws} device(s))')
             tb.wait_eval()
+            tb.check_update()  # a timed-out exchange never becomes an offspring (raises PGMError)
             for rec, ob in zip(recs, objs_i):
                 rec[:, :tb.K] = ob
         probe = self._batch(1) if tb is None else tb
         L, O, K = probe.layout.total, probe.O, probe.K
-        if snaps32:
-            s32, r64 = torch.stack(snaps32, 1), torch.stack(recs, 1)  # [Pl, I, 3, L], [Pl, I, S]
+        if recs:
+            r64 = torch.stack(recs, 1)  # [Pl, I, S]
         else:
-            s32 = torch.zeros(Pl, len(its), 3, L, device=self.device)
             r64 = torch.zeros(Pl, len(its), self._record_width(probe), dtype=torch.float64, device=self.device)
-        if ws > 1:  # generation boundary: the only collective of the path
-            s32, r64 = allgather_rows(s32, P), allgather_rows(r64, P)
+        if ws > 1:  # generation boundary: objective + statistics records only (a few KB)
+            r64 = allgather_rows(r64, P)
         host = r64.cpu().numpy()
         offspring = [[] for _ in range(P)]
         for p in range(P):
+            own = owner_of(p, P, ws)
             for i in range(len(its)):
                 objs, envp, step = self._unpack(host[p, i], O, K)
-                snap = DeviceSnapshot(probe.layout, s32[p, i, 0], s32[p, i, 1], s32[p, i, 2], step)
+                if own == rank:  # each survivor pins only its own [3, L] (the stacked block is freed)
+                    blk = snaps32[i][p - lo].clone()  # [3, L]
+                    snap = DeviceSnapshot(probe.layout, blk[0], blk[1], blk[2], step, owner=rank if ws > 1 else None)
+                else:
+                    snap = DeviceSnapshot.remote(probe.layout, step, own)
                 offspring[p].append(Sample.from_snapshot(snap, envp, objs))
         return offspring
 

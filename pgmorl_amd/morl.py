@@ -23,6 +23,7 @@ from .pareto import EP, OptGraph, weight_grid
 from .policy import new_policy
 from .population import make_population
 from .sample import DeviceSnapshot, RunningMeanStd, Sample, Task, WeightedSumScalarization
+from .shard import world
 
 
 def _fmt(n):
@@ -67,7 +68,8 @@ def run(args, device='cuda', rng='device', log=print):
         s.optgraph_id = opt_graph.insert(deepcopy(sc.weights), deepcopy(s.objs), -1)
     rl_num_updates = args.warmup_iter
     episode = iteration = 0
-    fmt = _fmt(args.obj_num)
+    rank, ws = world()
+    writer = rank == 0  # every rank holds the same host state; one writes the results tree
     while iteration < total_num_updates:
         log('\n------------------------------- Warm-up Stage -------------------------------' if episode == 0 else
             f'\n-------------------- Evolutionary Stage: Generation {episode:3} --------------------')
@@ -134,39 +136,54 @@ def run(args, device='cuda', rng='device', log=print):
             log(f'objs = {e.objs}, weight = {sc.weights}')
         iteration = min(iteration + rl_num_updates, total_num_updates)
         rl_num_updates = args.update_iter
-        # ---------------- per-generation dumps (morl/morl.py:179-218)
-        base = os.path.join(args.save_dir, str(iteration))
-        os.makedirs(os.path.join(base, 'ep'), exist_ok=True)
-        with open(os.path.join(base, 'ep', 'objs.txt'), 'w') as fp:
-            for obj in ep.obj_batch:
-                fp.write((fmt + '\n').format(*obj))
-        os.makedirs(os.path.join(base, 'population'), exist_ok=True)
-        with open(os.path.join(base, 'population', 'objs.txt'), 'w') as fp:
-            for s in population.sample_batch:
-                fp.write((fmt + '\n').format(*s.objs))
-        with open(os.path.join(base, 'population', 'optgraph.txt'), 'w') as fp:
-            fp.write('{}\n'.format(len(opt_graph.objs)))
-            for i in range(len(opt_graph.objs)):
-                fp.write((fmt + ';' + fmt + ';{}\n').format(*opt_graph.weights[i], *opt_graph.objs[i], opt_graph.prev[i]))
-            fp.write('{}\n'.format(len(population.sample_batch)))
-            for s in population.sample_batch:
-                fp.write('{}\n'.format(s.optgraph_id))
-        os.makedirs(os.path.join(base, 'elites'), exist_ok=True)
-        with open(os.path.join(base, 'elites', 'elites.txt'), 'w') as fp:
-            for e in elite_batch:
-                fp.write((fmt + '\n').format(*e.objs))
-        with open(os.path.join(base, 'elites', 'weights.txt'), 'w') as fp:
-            for sc in scalarization_batch:
-                fp.write((fmt + '\n').format(*sc.weights))
-        if args.selection_method == 'prediction-guided':
-            with open(os.path.join(base, 'elites', 'predictions.txt'), 'w') as fp:
-                for objs in predicted_offspring_objs:
-                    fp.write((fmt + '\n').format(*objs))
-        with open(os.path.join(base, 'elites', 'offsprings.txt'), 'w') as fp:
-            for offs in all_offspring_batch:
-                for s in offs:
-                    fp.write((fmt + '\n').format(*s.objs))
-    # ---------------- final artefacts (morl/morl.py:220-239)
+        if writer:
+            write_generation(args.save_dir, iteration, args.obj_num, ep, population, opt_graph, elite_batch,
+                             scalarization_batch, all_offspring_batch,
+                             predicted_offspring_objs if args.selection_method == 'prediction-guided' else None)
+    runtime.materialize(list(ep.sample_batch), dst=0)  # collective: EP snapshots onto the writing rank
+    if writer:
+        write_final(args, ep)
+    if ws > 1:
+        torch.distributed.barrier()  # the results tree is complete before any rank returns
+    return ep
+
+
+def write_generation(save_dir, iteration, obj_num, ep, population, opt_graph, elite_batch, scalarization_batch,
+                     all_offspring_batch, predicted_offspring_objs=None):
+    """The per-generation text dumps of morl/morl.py:182-221: ep/objs.txt, population/{objs,optgraph}.txt,
+    elites/{elites,weights,predictions,offsprings}.txt under save_dir/<iteration>/ ('{:5f}' CSV rows;
+    optgraph.txt = node count, 'w;objs;prev' rows, population count, the members' node ids).
+    predictions.txt is written only for prediction-guided selection (predicted_offspring_objs not None)."""
+    fmt = _fmt(obj_num)
+    base = os.path.join(save_dir, str(iteration))
+
+    def rows(path, vecs):
+        with open(path, 'w') as fp:
+            for v in vecs:
+                fp.write((fmt + '\n').format(*v))
+
+    os.makedirs(os.path.join(base, 'ep'), exist_ok=True)
+    rows(os.path.join(base, 'ep', 'objs.txt'), ep.obj_batch)
+    os.makedirs(os.path.join(base, 'population'), exist_ok=True)
+    rows(os.path.join(base, 'population', 'objs.txt'), [s.objs for s in population.sample_batch])
+    with open(os.path.join(base, 'population', 'optgraph.txt'), 'w') as fp:
+        fp.write('{}\n'.format(len(opt_graph.objs)))
+        for i in range(len(opt_graph.objs)):
+            fp.write((fmt + ';' + fmt + ';{}\n').format(*opt_graph.weights[i], *opt_graph.objs[i], opt_graph.prev[i]))
+        fp.write('{}\n'.format(len(population.sample_batch)))
+        for s in population.sample_batch:
+            fp.write('{}\n'.format(s.optgraph_id))
+    os.makedirs(os.path.join(base, 'elites'), exist_ok=True)
+    rows(os.path.join(base, 'elites', 'elites.txt'), [e.objs for e in elite_batch])
+    rows(os.path.join(base, 'elites', 'weights.txt'), [sc.weights for sc in scalarization_batch])
+    if predicted_offspring_objs is not None:
+        rows(os.path.join(base, 'elites', 'predictions.txt'), predicted_offspring_objs)
+    rows(os.path.join(base, 'elites', 'offsprings.txt'), [s.objs for offs in all_offspring_batch for s in offs])
+
+
+def write_final(args, ep):
+    """morl/morl.py:223-245: final/EP_policy_i.pt, EP_env_params_i.pkl, objs.txt, env_params.txt."""
+    fmt = _fmt(args.obj_num)
     final = os.path.join(args.save_dir, 'final')
     os.makedirs(final, exist_ok=True)
     for i, s in enumerate(ep.sample_batch):
@@ -180,4 +197,3 @@ def run(args, device='cuda', rng='device', log=print):
         with open(os.path.join(final, 'env_params.txt'), 'w') as fp:
             for s in ep.sample_batch:
                 fp.write('obj_rms: mean: {} var: {}\n'.format(s.env_params['obj_rms'].mean, s.env_params['obj_rms'].var))
-    return ep

@@ -17,7 +17,7 @@ import numpy as np
 import torch
 
 from . import envspec
-from ._lib import (Dims, EnvSpec, EnvState, NormState, PPOHParams, RolloutBuf, check, lib)
+from ._lib import (Dims, EnvSpec, EnvState, NormState, PGMError, PPOHParams, RolloutBuf, check, lib)
 from .layout import ParamLayout
 
 F32, F64, I32 = torch.float32, torch.float64, torch.int32
@@ -86,6 +86,9 @@ class TaskBatch:
         self._eval_mean, self._eval_var = z(P, O, dt=F64), z(P, O, dt=F64)
         nws = lib().pgm_ppo_update_workspace_bytes(C.byref(self.dims))
         self.update_ws = torch.zeros((nws + 7) // 8, dtype=torch.int64, device=self.dev)
+        # sticky OR of every update's exchange-timeout word (workspace word 2P, include/pgm_abi.h): a launch
+        # whose spin-wait gave up produced invalid parameters; check_update() turns that into PGMError
+        self.update_failed = torch.zeros(1, dtype=torch.int64, device=self.dev)
 
     # ------------------------------------------------------------------ structs
     def _build_structs(self):
@@ -171,10 +174,25 @@ class TaskBatch:
     def ppo_update(self, perms=None):
         if perms is not None:
             self.perms.copy_(torch.as_tensor(np.asarray(perms), dtype=I32))
+        self.ppo_update_launch()
+        flag = self.update_ws[2 * self.P:2 * self.P + 1]
+        torch.bitwise_or(self.update_failed, flag, out=self.update_failed)  # stream-ordered, no host sync
+
+    def ppo_update_launch(self):
+        """pgm_ppo_update alone (packed rows + the update kernel) on the current stream."""
         check(lib().pgm_ppo_update(C.byref(self.dims), C.byref(self.hp), _ptr(self.params), _ptr(self.adam_m),
                                    _ptr(self.adam_v), _ptr(self.adam_step), _ptr(self.lr), _ptr(self.perms),
                                    C.byref(self.c_rb), _ptr(self.stats), _ptr(self.update_ws), _stream()),
               'pgm_ppo_update')
+
+    def check_update(self):
+        """Raise PGMError if any PPO update since the last check timed out in a cross-workgroup exchange
+        (its parameters / Adam state are invalid).  Synchronises with the stream; call it once per
+        generation (MOPGPopulation.run) or after a timed region, not per update."""
+        if int(self.update_failed.item()) != 0:
+            self.update_failed.zero_()
+            raise PGMError('pgm_ppo_update: a cross-workgroup exchange timed out (workspace word 2P set); '
+                           'the update kernel\'s workgroups were not co-resident -- the parameters are invalid')
 
     def evaluate(self, ob_mean=None, ob_var=None, out=None):
         mean = self.ob_mean if ob_mean is None else ob_mean

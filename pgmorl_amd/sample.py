@@ -51,16 +51,50 @@ class WeightedSumScalarization:
 
 
 class DeviceSnapshot:
-    """Parameters + Adam state of one task, kept on the device."""
+    """Parameters + Adam state of one task, kept on the device of the rank that produced it.
 
-    def __init__(self, layout, params, adam_m, adam_v, adam_step):
+    Multi-GPU: every rank holds the same Samples (identical host state), but a snapshot's tensors live
+    only on its ``owner`` rank; elsewhere it is a remote handle (``data is None``) that
+    ``MOPGPopulation`` moves to the rank that next trains it, or to rank 0 for the final artefacts
+    (shard.move_rows: bytes scale with the moved snapshots, not with the population).  owner None =
+    local (single process, or replicated on every rank like the warm-up policies)."""
+
+    def __init__(self, layout, params, adam_m, adam_v, adam_step, owner=None):
         self.layout = layout
-        self.params, self.adam_m, self.adam_v = params, adam_m, adam_v
+        self.data = None if params is None else (params, adam_m, adam_v)
         self.adam_step = int(adam_step)
+        self.owner = owner
+
+    @classmethod
+    def remote(cls, layout, adam_step, owner):
+        return cls(layout, None, None, None, adam_step, owner)
+
+    @property
+    def is_local(self):
+        return self.data is not None
+
+    def _part(self, i):
+        if self.data is None:
+            raise RuntimeError(f'snapshot lives on rank {self.owner}: move it first (MOPGPopulation.materialize)')
+        return self.data[i]
+
+    params = property(lambda self: self._part(0))
+    adam_m = property(lambda self: self._part(1))
+    adam_v = property(lambda self: self._part(2))
+
+    def stacked(self):
+        """[3, L] params | exp_avg | exp_avg_sq (a new tensor)."""
+        return torch.stack([self.params, self.adam_m, self.adam_v])
+
+    def adopt(self, rows):
+        """Materialise a remote handle from a received [3, L] block (it becomes local)."""
+        self.data = (rows[0].clone(), rows[1].clone(), rows[2].clone())
 
     def clone(self):
+        if self.data is None:
+            return DeviceSnapshot.remote(self.layout, self.adam_step, self.owner)
         return DeviceSnapshot(self.layout, self.params.clone(), self.adam_m.clone(), self.adam_v.clone(),
-                              self.adam_step)
+                              self.adam_step, self.owner)
 
 
 class PolicyHandle:

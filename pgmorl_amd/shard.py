@@ -24,6 +24,12 @@ def task_block(P, rank, world_size):
     return lo, min(P, lo + per)
 
 
+def owner_of(p, P, world_size):
+    """The rank whose task_block holds task p."""
+    per = -(-P // world_size)
+    return min(p // per, world_size - 1)
+
+
 def allgather_rows(local, P, group=None):
     """Concatenate every rank's ``local`` rows ([P_local, ...], rank order) into [P, ...] on every rank.
 
@@ -49,3 +55,32 @@ def allreduce_max(values, device):
     if world()[1] > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return [float(x) for x in t]
+
+
+def move_rows(moves, local_rows, shape, dtype, device, group=None):
+    """Collective point-to-multipoint move of fixed-shape rows (the elite snapshots whose next task runs on
+    another rank, or the EP snapshots rank 0 writes out).
+
+    ``moves``: [(src, dst)] per item, in an order identical on every rank; ``local_rows[k]`` is item k's
+    tensor on its src rank.  Returns ({k: tensor} of the items whose dst is this rank, bytes each rank
+    contributed).  One all-gather of [max items sent by one rank, *shape]: the payload scales with the moved
+    rows, not with the population (items with src == dst or src < 0, i.e. replicated, are not sent)."""
+    rank, ws = (dist.get_rank(group), dist.get_world_size(group)) if group is not None else world()
+    live = [(k, s, d) for k, (s, d) in enumerate(moves) if s is not None and s >= 0 and s != d]
+    if ws == 1 or not live:
+        return {}, 0
+    sends = [[] for _ in range(ws)]
+    for k, s, d in live:
+        sends[s].append(k)
+    per = max(len(x) for x in sends)
+    buf = torch.zeros((per,) + tuple(shape), dtype=dtype, device=device)
+    for j, k in enumerate(sends[rank]):
+        buf[j].copy_(local_rows[k])
+    parts = [torch.empty_like(buf) for _ in range(ws)]
+    dist.all_gather(parts, buf, group=group)
+    got = {}
+    for s in range(ws):
+        for j, k in enumerate(sends[s]):
+            if moves[k][1] == rank:
+                got[k] = parts[s][j].clone()
+    return got, buf.numel() * buf.element_size()

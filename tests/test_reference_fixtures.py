@@ -1,0 +1,219 @@
+"""Parity pinned by the reference's OWN result files (tests/golden/working_morl_dst/, copied verbatim from
+/root/reference/WorkingMorl/deep_sea_treasure_results/<iteration>/ for the generations 20..78 of one run).
+
+Those files were written by the reference's generation loop (WorkingMorl/morl/morl.py:182-221, the same
+writer as morl/morl.py:180-218) for a Deep-Sea-Treasure run with warmup_iter 20, update_iter 10,
+delta_weight 0.02 (51 warm-up tasks), num_tasks 8, pbuffer_num 20, pbuffer_size 1, 8 weight candidates
+(WorkingMorl/deep_sea_treasure_config.py:187-203).  Every generation boundary of that run is replayed
+here from the previous generation's files:
+
+  * EP:  ep.update(all offspring) (morl/morl.py:124) => EP_{k+1} = get_ep_indices(EP_k ++ offsprings_{k+1})
+         -- membership, ORDER and DUPLICATES, bit for bit, for the product (pgmorl_amd.pareto) and the oracle;
+  * population: population.update(every update_iter-th offspring) (morl/morl.py:125), objs and node ids;
+  * OptGraph: the nodes the generation appends (weight / objs / prev chain, morl/morl.py:108-118);
+  * writer: pgmorl_amd.morl.write_generation re-emits every file byte for byte from the parsed values;
+  * selection: prediction-guided selection of generation 20 reproduces the reference's first six picks
+    (elite objs exactly, weights and predicted objs to 2e-6: the files round their inputs to 6 dp).  The
+    seventh pick depends on one soft-L1 least_squares fit (node 128) that lands in a different local
+    minimum here (scipy 1.15, inputs rounded to 6 dp): documented in DESIGN.md §5 as unpinned.
+
+The fork differs from morl/ in two places that matter for selection (population_2d.py diff): the 2-D
+neighbourhood search has the 3-D ``threshold >= 1.0`` exit, and candidates are scored by
+utils.update_ep + compute_hypervolume / compute_sparsity (the 3-D scoring).  ``_ForkPopulation2d`` below
+applies exactly those two changes to the product class for this test only.
+"""
+import argparse
+import os
+
+import numpy as np
+import pytest
+
+from oracle import pareto as oracle_pareto
+from pgmorl_amd import pareto
+from pgmorl_amd.morl import write_generation
+from pgmorl_amd.population import Population2d, Population3d
+from pgmorl_amd.sample import WeightedSumScalarization
+
+ROOT = os.path.join(os.path.dirname(__file__), 'golden', 'working_morl_dst')
+GENS = [20, 30, 40, 50, 60, 70, 78]
+NUM_TASKS, WARMUP_TASKS, UPDATE_ITER = 8, 51, 10
+ARGS = argparse.Namespace(obj_num=2, pbuffer_num=20, pbuffer_size=1, num_weight_candidates=8, num_tasks=NUM_TASKS,
+                          sparsity=1.0, min_weight=0.0, max_weight=1.0, delta_weight=0.02, selection_method='prediction-guided')
+FILES = ['ep/objs.txt', 'population/objs.txt', 'population/optgraph.txt', 'elites/elites.txt', 'elites/weights.txt',
+         'elites/predictions.txt', 'elites/offsprings.txt']
+
+
+def _path(gen, name):
+    return os.path.join(ROOT, str(gen), name)
+
+
+def _rows(gen, name):
+    p = _path(gen, name)
+    if os.path.getsize(p) == 0:
+        return np.zeros((0, 2))
+    return np.loadtxt(p, delimiter=',', ndmin=2)
+
+
+def _graph(gen):
+    """population/optgraph.txt -> (weights, objs, prev, population node ids)."""
+    lines = open(_path(gen, 'population/optgraph.txt')).read().split('\n')
+    n = int(lines[0])
+    W, O, P = [], [], []
+    for line in lines[1:1 + n]:
+        w, o, p = line.split(';')
+        W.append(np.array(w.split(','), dtype=np.float64))
+        O.append(np.array(o.split(','), dtype=np.float64))
+        P.append(int(p))
+    m = int(lines[1 + n])
+    return W, O, P, [int(x) for x in lines[2 + n:2 + n + m]]
+
+
+def _optgraph(gen):
+    W, O, P, ids = _graph(gen)
+    g = pareto.OptGraph()
+    for w, o, p in zip(W, O, P):  # rebuild with the stored (already normalised) weights
+        g.weights.append(w)
+        g.objs.append(o)
+        g.prev.append(p)
+        g.delta_objs.append(np.zeros_like(o) if p == -1 else o - g.objs[p])
+        if p != -1:
+            g.succ[p].append(len(g.objs) - 1)
+        g.succ.append([])
+    return g, ids
+
+
+class _S:
+    def __init__(self, objs, optgraph_id=-1):
+        self.objs = np.asarray(objs, dtype=np.float64)
+        self.optgraph_id = optgraph_id
+
+
+def _offsprings_per_task(gen):
+    off = _rows(gen, 'elites/offsprings.txt')
+    tasks = WARMUP_TASKS if gen == GENS[0] else NUM_TASKS
+    assert len(off) % tasks == 0
+    n = len(off) // tasks
+    return [off[t * n:(t + 1) * n] for t in range(tasks)]
+
+
+def test_fixture_files_present():
+    for g in GENS:
+        for f in FILES:
+            assert os.path.exists(_path(g, f)), (g, f)
+
+
+@pytest.mark.parametrize('impl', ['product', 'oracle'])
+def test_ep_replay_order_and_duplicates(impl):
+    """EP_{k+1} == get_ep_indices(EP_k ++ offsprings_{k+1}) row for row (morl/ep.py:23-31, morl/utils.py:24-39)."""
+    get = pareto.get_ep_indices if impl == 'product' else oracle_pareto.get_ep_indices
+    prev = np.zeros((0, 2))
+    for g in GENS:
+        allo = np.concatenate([prev, _rows(g, 'elites/offsprings.txt')])
+        got = allo[list(get(allo))]
+        ref = _rows(g, 'ep/objs.txt')
+        np.testing.assert_array_equal(got, ref, err_msg=f'EP after generation {g}')
+        prev = ref
+    assert len(np.unique(ref, axis=0)) < len(ref)  # the archive keeps duplicates
+
+
+def test_ep_class_replay():
+    """The EP class itself (append + re-index), fed Samples, across every generation."""
+    ep = pareto.EP()
+    for g in GENS:
+        ep.update([_S(o) for o in _rows(g, 'elites/offsprings.txt')])
+        np.testing.assert_array_equal(ep.obj_batch, _rows(g, 'ep/objs.txt'))
+        assert [tuple(s.objs) for s in ep.sample_batch] == [tuple(o) for o in ep.obj_batch]
+
+
+def test_population_and_optgraph_replay():
+    """population.update(every update_iter-th offspring) (morl/morl.py:104-125) and the OptGraph nodes it
+    appends: objs, member node ids, node weights (the selected weights, L2-normalised), prev chains."""
+    # generation 20: warm-up nodes 0..50 are the warm-up elites (the fork also seeds the population with
+    # them, WorkingMorl/morl/morl.py:61); each warm-up task appends its 10th and 20th offspring
+    W, O, P, ids = _graph(GENS[0])
+    pop = Population2d(ARGS)
+    pop.update([_S(O[i], i) for i in range(WARMUP_TASKS)])
+    node = WARMUP_TASKS
+    batch = []
+    for t, offs in enumerate(_offsprings_per_task(GENS[0])):
+        prev = t
+        for i, o in enumerate(offs):
+            if (i + 1) % UPDATE_ITER == 0:
+                np.testing.assert_array_equal(O[node], o)
+                assert P[node] == prev and np.allclose(W[node], W[t], atol=2e-6)
+                batch.append(_S(o, node))
+                prev, node = node, node + 1
+    pop.update(batch)
+    np.testing.assert_array_equal([s.objs for s in pop.sample_batch], _rows(GENS[0], 'population/objs.txt'))
+    assert [s.optgraph_id for s in pop.sample_batch] == ids
+    # later generations: start from the previous generation's files
+    for a, b in zip(GENS[:-1], GENS[1:]):
+        Wa, Oa, Pa, ida = _graph(a)
+        Wb, Ob, Pb, idb = _graph(b)
+        assert all(np.array_equal(Wa[i], Wb[i]) and np.array_equal(Oa[i], Ob[i]) and Pa[i] == Pb[i]
+                   for i in range(len(Wa))), 'nodes are never rewritten'
+        pop = Population2d(ARGS)
+        pop.sample_batch = [_S(o, i) for o, i in zip(_rows(a, 'population/objs.txt'), ida)]
+        weights, elites = _rows(a, 'elites/weights.txt'), _rows(a, 'elites/elites.txt')
+        node, batch = len(Wa), []
+        for t, offs in enumerate(_offsprings_per_task(b)):
+            w = weights[t] / np.linalg.norm(weights[t])
+            for i, o in enumerate(offs):
+                if (i + 1) % UPDATE_ITER:
+                    continue
+                np.testing.assert_array_equal(Ob[node], o)
+                np.testing.assert_allclose(Wb[node], w, atol=2e-6)
+                if i + 1 == UPDATE_ITER:  # first node of the task hangs off the elite's node
+                    np.testing.assert_allclose(Ob[Pb[node]], elites[t], atol=1e-6)
+                else:
+                    assert Pb[node] == node - 1
+                batch.append(_S(o, node))
+                node += 1
+        assert node == len(Wb)
+        pop.update(batch)
+        np.testing.assert_array_equal([s.objs for s in pop.sample_batch], _rows(b, 'population/objs.txt'))
+        assert [s.optgraph_id for s in pop.sample_batch] == idb
+
+
+@pytest.mark.parametrize('gen', GENS)
+def test_writer_byte_identical(gen, tmp_path):
+    """write_generation (morl/morl.py:182-221 formats) re-emits the reference's bytes from the parsed values."""
+    g, ids = _optgraph(gen)
+    ep = pareto.EP()
+    ep.obj_batch = _rows(gen, 'ep/objs.txt')
+    pop = Population2d(ARGS)
+    pop.sample_batch = [_S(o, i) for o, i in zip(_rows(gen, 'population/objs.txt'), ids)]
+    elites = [_S(o) for o in _rows(gen, 'elites/elites.txt')]
+    scal = [WeightedSumScalarization(num_objs=2, weights=w) for w in _rows(gen, 'elites/weights.txt')]
+    offs = [[_S(o) for o in _rows(gen, 'elites/offsprings.txt')]]
+    write_generation(str(tmp_path), gen, 2, ep, pop, g, elites, scal, offs, list(_rows(gen, 'elites/predictions.txt')))
+    for f in FILES:
+        got = open(os.path.join(tmp_path, str(gen), f), 'rb').read()
+        assert got == open(_path(gen, f), 'rb').read(), f'{gen}/{f}'
+
+
+class _ForkPopulation2d(Population2d):
+    """The fork's two selection changes (WorkingMorl/morl/population_2d.py vs morl/population_2d.py):
+    bounded neighbourhood search and update_ep-based hypervolume / sparsity scoring."""
+    bounded_search = True
+    _evaluate = Population3d._evaluate
+    _virtual_insert = Population3d._virtual_insert
+
+
+def test_prediction_guided_selection_first_picks():
+    """Generation 20's prediction-guided selection (population_2d.py:229-304) from the reference's own
+    population / OptGraph / EP files: the first six of eight picks agree."""
+    g, ids = _optgraph(GENS[0])
+    pop = _ForkPopulation2d(ARGS)
+    pop.sample_batch = [_S(o, i) for o, i in zip(_rows(GENS[0], 'population/objs.txt'), ids)]
+    ep = pareto.EP()
+    ep.obj_batch = _rows(GENS[0], 'ep/objs.txt')
+    ep.sample_batch = np.array([_S(o) for o in ep.obj_batch], dtype=object)
+    tmpl = WeightedSumScalarization(num_objs=2, weights=np.ones(2) / 2)
+    elites, scal, preds = pop.prediction_guided_selection(ARGS, GENS[0], ep, g, tmpl)
+    n = 6
+    ref_e, ref_w, ref_p = (_rows(GENS[0], f'elites/{f}.txt') for f in ('elites', 'weights', 'predictions'))
+    assert len(elites) == len(ref_e) == NUM_TASKS
+    np.testing.assert_array_equal(np.round([e.objs for e in elites[:n]], 6), ref_e[:n])
+    np.testing.assert_allclose([s.weights.numpy() for s in scal[:n]], ref_w[:n], atol=2e-6)
+    np.testing.assert_allclose(np.array(preds[:n]), ref_p[:n], atol=2e-6)

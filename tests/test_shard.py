@@ -127,3 +127,74 @@ def test_selection_agrees_across_ranks_gloo(ws, K):
         errs.append(errq.get())
     assert not errs, errs
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+
+
+def _spawn(target, ws, *args):
+    ctx = mp.get_context('spawn')
+    errq = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, ws, port) + args + (errq,)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    errs = []
+    while not errq.empty():
+        errs.append(errq.get())
+    assert not errs, errs
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+
+
+def _place_worker(rank, ws, port, P, errq):
+    """MOPGPopulation.place / materialize over gloo with CPU tensors: the elites of the next generation
+    (drawn from the previous generation's offspring, each owned by the rank that produced it) move to the
+    ranks that train them; only moved snapshots are sent, and bytes scale with the moves, not with P."""
+    try:
+        import argparse
+        from pgmorl_amd.mopg import MOPGPopulation
+        from pgmorl_amd.sample import DeviceSnapshot, Sample
+        from pgmorl_amd.shard import owner_of
+        os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+        dist.init_process_group('gloo', rank=rank, world_size=ws)
+        rt = MOPGPopulation(argparse.Namespace(env_name='MO-Hopper-v2'), device='cpu')
+        lay = rt.layout
+        L = lay.total
+
+        def content(p):  # what the offspring of task p holds: params | m | v
+            return torch.arange(3 * L, dtype=torch.float32).reshape(3, L) + 1000.0 * p
+
+        # previous generation's offspring: task p ran on owner_of(p); elsewhere a remote handle
+        prev = []
+        for p in range(P):
+            own = owner_of(p, P, ws)
+            if own == rank:
+                c = content(p)
+                snap = DeviceSnapshot(lay, c[0], c[1], c[2], 7, owner=own)
+            else:
+                snap = DeviceSnapshot.remote(lay, 7, own)
+            prev.append(Sample.from_snapshot(snap, {}, objs=None))
+        # next generation's elites (a deterministic reshuffle, identical on every rank)
+        pick = [(3 * p + 1) % P for p in range(P)]
+        elites = [Sample.copy_from(prev[q]) for q in pick]
+        nbytes = rt.place(elites, [owner_of(p, P, ws) for p in range(P)])
+        moves = [(owner_of(q, P, ws), owner_of(p, P, ws)) for p, q in enumerate(pick)]
+        sent = [sum(1 for s, d in moves if s == r and s != d) for r in range(ws)]
+        assert nbytes == (max(sent) * 3 * L * 4 if max(sent) else 0)
+        for p, q in enumerate(pick):
+            if owner_of(p, P, ws) == rank:
+                assert torch.equal(elites[p].snapshot.stacked(), content(q)), (p, q)
+        # final writer: every offspring onto rank 0
+        rt.materialize(prev, dst=0)
+        if rank == 0:
+            for p in range(P):
+                assert torch.equal(prev[p].snapshot.stacked(), content(p))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # surfaced by the parent
+        errq.put(f'rank {rank}: {e!r}')
+        raise
+
+
+@pytest.mark.parametrize('ws,P', [(2, 5), (2, 8), (3, 7)])
+def test_place_moves_only_relocated_snapshots_gloo(ws, P):
+    _spawn(_place_worker, ws, P)

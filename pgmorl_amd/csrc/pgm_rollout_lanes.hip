@@ -135,6 +135,21 @@ struct EnvLane {
     }
     // s' = tanh(d*s + U clip(a) + c) for this lane's feature; raw objectives (wave-uniform):
     // obj_k = V_k . s' + ebase_k - ecoef_k * |clip(a)|^2   (the Walker form, environments/walker2d.py:23-25)
+    // s' of this lane's feature (rcp-based fp64 tanh: no IEEE division on the step chain)
+    __device__ double next_state(double s, const double (&ac)[A]) const {
+        double pu[A];
+#pragma unroll
+        for (int j = 0; j < A; ++j) pu[j] = U[j] * ac[j];
+        return tanh_d2(d * s + tree_sum(pu) + c);
+    }
+    // raw objectives of next state sn (wave-uniform)
+    __device__ void objectives(double sn, double e2, double (&objraw)[K]) const {
+#pragma unroll
+        for (int k = 0; k < K; ++k) objraw[k] = V[k] * sn;
+        wave_sum64_d_multi<K>(objraw, objraw);
+#pragma unroll
+        for (int k = 0; k < K; ++k) objraw[k] += ebase[k] - ecoef[k] * e2;
+    }
     __device__ double step(double s, const double (&ac)[A], double e2, double (&objraw)[K]) const {
         double pu[A];
 #pragma unroll
@@ -160,6 +175,22 @@ struct LaneSmem {
     alignas(16) float eps[2][NN][NCH * A];  // action noise of env n for NCH steps, double-buffered
 };
 
+// raw buffer store of one dword per lane; a lane whose offset is OOB_OFF stores nothing (the buffer's range
+// check drops it), so the per-role output stores need no exec-mask branches inside the step loop
+constexpr uint32_t OOB_OFF = 0xFFFFFFF0u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t out_rsrc(const void* base, size_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ void store_lane(__amdgpu_buffer_rsrc_t r, uint32_t off, float v) {
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (int)off, 0, 0);
+}
+// clip as two bare v_max_f64 / v_min_f64 that the scheduler may move (clipd_hw is a volatile asm barrier)
+__device__ __forceinline__ double clipd_s(double x, double lo, double hi) {
+    double r;
+    asm("v_max_f64 %0, %1, %2\n\tv_min_f64 %0, %0, %3" : "=&v"(r) : "v"(x), "v"(lo), "v"(hi));
+    return r;
+}
+
 template <int O, int A, int K, int NN>
 __global__ __launch_bounds__(256) void rollout_lane_kernel(RolloutArgs a) {
     static_assert(lanes_fit<O, K>(), "lane roles need O + K + 1 <= 64");
@@ -179,6 +210,13 @@ __global__ __launch_bounds__(256) void rollout_lane_kernel(RolloutArgs a) {
     float* masks = a.rb.masks + (size_t)p * (T + 1) * NN;
     float* bad = a.rb.bad_masks + (size_t)p * (T + 1) * NN;
     const int maxs = a.spec.max_episode_steps;
+    // per-task output ranges as buffer resources (branch-free masked stores)
+    const auto r_obs = out_rsrc(obs, (size_t)(T + 1) * NN * O * 4);
+    const auto r_act = out_rsrc(act, (size_t)T * NN * A * 4);
+    const auto r_logp = out_rsrc(logp, (size_t)T * NN * 4);
+    const auto r_rew = out_rsrc(rew, (size_t)T * NN * K * 4);
+    const auto r_msk = out_rsrc(masks, (size_t)(T + 1) * NN * 4);
+    const auto r_bad = out_rsrc(bad, (size_t)(T + 1) * NN * 4);
 
     ActorLane<O, A> pol;
     pol.load(prm, L, l);
@@ -188,8 +226,8 @@ __global__ __launch_bounds__(256) void rollout_lane_kernel(RolloutArgs a) {
     // ---- env state of this wave's envs (feature l), VecNormalize accumulators (wave-uniform)
     const bool fl = l < O;
     const int lo = fl ? l : 0;
-    double s_o[NE], s0_o[NE], objacc[NE][K], ret[NE], objraw[NE][K];
-    int elapsed[NE], done[NE], badf[NE];
+    double s_o[NE], s0_o[NE], sn_e[NE], e2_e[NE], objacc[NE][K], ret[NE], objraw[NE][K];
+    int elapsed[NE], dprev[NE], dcur[NE];  // done of step t - 1 (consumed after step t's barrier) and of step t
 #pragma unroll
     for (int e = 0; e < NE; ++e) {
         const int n = min(w + 4 * e, NN - 1);
@@ -202,12 +240,17 @@ __global__ __launch_bounds__(256) void rollout_lane_kernel(RolloutArgs a) {
         }
         ret[e] = a.st.ret[p * NN + n];
         elapsed[e] = a.st.elapsed[p * NN + n];
-        done[e] = badf[e] = 0;
+        dprev[e] = dcur[e] = 0;
+        sn_e[e] = e2_e[e] = 0.0;
     }
     int obj_valid = a.st.obj_acc_valid[p];
 
     // ---- running statistics, one lane per statistic (role 0: ob feature l, 1: objective l - O, 2: ret),
-    // replicated in every wave
+    // replicated in every wave.  The objective / ret statistics (roles 1, 2) run ONE STEP BEHIND the
+    // observation statistics: step t's objective sums, accumulators and reward are formed after step t's
+    // barrier, merged after step t + 1's (the row of step t + 1 carries them) and the reward of step t is
+    // emitted then -- so nothing but the observation chain (policy -> dynamics -> ob_rms -> next input) sits
+    // between two barriers.  A drain step after the loop merges the last step.
     const int role = l < O ? 0 : l < O + K ? 1 : l == O + K ? 2 : 3;
     const int ko = role == 1 ? l - O : 0;
     double mean = 0.0, var = 1.0, cnt = 1.0;
@@ -225,8 +268,9 @@ __global__ __launch_bounds__(256) void rollout_lane_kernel(RolloutArgs a) {
         cnt = a.ns.ret_count[p];
     }
     const bool upd = role == 0 ? nc.use_ob != 0 : role == 1 ? nc.use_obj != 0 : role == 2;
-    double itot = 1.0;  // 1 / (count + batch) of this step's merge, computed at the top of the step
     double inv = 1.0;
+    const double clip_lo = role == 0 ? -nc.clipob : -nc.cliprew, clip_hi = role == 0 ? nc.clipob : nc.cliprew;
+    const bool scale_out = role == 0 ? nc.use_ob != 0 : nc.use_obj != 0;
 
     // ---- slot 0: after_update() carry (storage.py:71-75) and the first policy input
 #pragma unroll
@@ -245,8 +289,7 @@ __global__ __launch_bounds__(256) void rollout_lane_kernel(RolloutArgs a) {
     }
     // action noise, staged per wave in LDS chunks of NCH steps: the next chunk is loaded into registers a
     // whole chunk ahead and written to LDS at the chunk boundary, so its vmcnt wait (which also drains the
-    // wave's rollout-storage stores) is paid once per NCH steps.  (LDS-DMA would make the compiler wait on
-    // vmcnt before every read of the buffer.)  NULL noise: the perf-mode counter stream, drawn by the lanes.
+    // wave's rollout-storage stores) is paid once per NCH steps.  NULL noise: the perf-mode counter stream.
     constexpr int CA = NCH * A, CR = (CA + 63) / 64;
     float nreg[NE][CR];
     auto load_eps = [&](int c) {
@@ -285,13 +328,60 @@ __global__ __launch_bounds__(256) void rollout_lane_kernel(RolloutArgs a) {
     };
     load_eps(0);
     store_eps(0);
-    // every preamble load (weights, constants, state) retired here with a wait the compiler's scoreboard
-    // sees: otherwise their first uses inside the step loop get vmcnt waits that, from the second step on,
-    // drain the previous step's rollout-storage stores
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): preamble loads retired where the compiler sees it
     if (NCH < T) load_eps(1);
     wave_lds_fence_r();
     PGM_STAMP_DECL
+
+    // statistics merge of this lane's role (counts from before the merge; numpy's mean / var divide by N,
+    // exact for N a power of two)
+    auto merge = [&](int buf, bool active) {
+        const double tot = cnt + (double)NN;  // 1 / (count + N): hardware reciprocal + two Newton steps
+        double r = __builtin_amdgcn_rcp(tot);
+        r = fma(r, fma(-tot, r, 1.0), r);
+        const double itot = fma(r, fma(-tot, r, 1.0), r);
+        double v[NN], sum = 0.0;
+#pragma unroll
+        for (int n = 0; n < NN; ++n) {
+            v[n] = S.sr[buf][n][l];
+            sum += v[n];
+        }
+        constexpr double rn = 1.0 / NN;
+        const double bm = sum * rn;
+        double sq = 0.0;
+#pragma unroll
+        for (int n = 0; n < NN; ++n) sq = fma(v[n] - bm, v[n] - bm, sq);
+        if (upd && active) {
+            const double delta = bm - mean;
+            mean = mean + delta * (double)NN * itot;
+            var = (var * cnt + (sq * rn) * (double)NN + delta * delta * cnt * (double)NN * itot) * itot;
+            cnt += (double)NN;
+            inv = rsqrt_d(var + nc.eps);
+        }
+    };
+    // objective side of step t for env slot e (after step t's barrier): reset by done_{t-1}, raw objectives
+    // (wave sums), discounted accumulators (vec_normalize.py:32-45), kept for the next step's row
+    auto objective_side = [&](int e) {
+        if (dprev[e]) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) objacc[e][k] = 0.0;
+            ret[e] = 0.0;
+        }
+        double ob[K];
+        env.objectives(sn_e[e], e2_e[e], ob);
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            objraw[e][k] = ob[k];
+            objacc[e][k] = obj_valid ? objacc[e][k] * nc.gamma + ob[k] : ob[k];
+        }
+        ret[e] = ret[e] * nc.gamma + 0.0;  // SynthMO's scalar reward is 0 (vec_normalize.py:32)
+    };
+    // reward of step ts (role-1 lanes, after the merge of its accumulators): clip(obj / sqrt(var + eps))
+    auto emit_reward = [&](int e, int n, int ts) {
+        double r = sel_lane_d(objraw[e], ko);
+        if (scale_out) r = clipd_s(r * inv, clip_lo, clip_hi);
+        store_lane(r_rew, role == 1 ? (uint32_t)((((size_t)ts * NN + n) * K + ko) * 4) : OOB_OFF, (float)r);
+    };
 
     for (int step = 0; step < T; ++step) {
         const int buf = step & 1;
@@ -301,112 +391,98 @@ __global__ __launch_bounds__(256) void rollout_lane_kernel(RolloutArgs a) {
             if (step + NCH < T) load_eps(step / NCH + 1);
             wave_lds_fence_r();
         }
-        {  // 1 / (count + N): hardware reciprocal + two Newton steps (~1 ulp; the Chan merge multiplies by it)
-            const double tot = cnt + (double)NN;
-            double r = __builtin_amdgcn_rcp(tot);
-            r = fma(r, fma(-tot, r, 1.0), r);
-            itot = fma(r, fma(-tot, r, 1.0), r);
-        }
         PGM_STAMP(0);
 #pragma unroll
         for (int e = 0; e < NE; ++e) {
             const int n = w + 4 * e;
             if (n >= NN) break;
+            float ej[A];  // this step's noise, read before the forward so its LDS latency hides there
+#pragma unroll
+            for (int j = 0; j < A; ++j) ej[j] = S.eps[cb][n][cs * A + j];
             float mu[A];
             pol.forward(S.x[n], S.h1[w], l, mu);
             PGM_STAMP(1);
             // Gaussian draw (torch.normal(mean, std) = eps * std + mean), log-prob and clipped action, all
-            // wave-uniform: lane j's noise is broadcast by readlane
+            // wave-uniform; lanes 0..A-1 store the action row, lane 0 its log-prob
             float lpt[A], avs[A];
             double ac[A], sq[A];
 #pragma unroll
             for (int j = 0; j < A; ++j) {
-                const float ej = S.eps[cb][n][cs * A + j];
-                const float av = fmaf(ej, pol.sd[j], mu[j]);
+                const float av = fmaf(ej[j], pol.sd[j], mu[j]);
                 const float dz = (av - mu[j]) * pol.rsd[j];
                 lpt[j] = -0.5f * dz * dz - pol.ls[j] - LOG_SQRT_2PI;
                 avs[j] = av;
-                ac[j] = clipd_hw((double)av, env.lo[j], env.hi[j]);
+                ac[j] = clipd_s((double)av, env.lo[j], env.hi[j]);
                 sq[j] = ac[j] * ac[j];
             }
             const float lp = tree_sum(lpt);
-            const double e2 = tree_sum(sq);
-            if (l == 0) {  // the draws are wave-uniform: lane 0 stores the action row and its log-prob
-                float* ar = act + ((size_t)step * NN + n) * A;
-#pragma unroll
-                for (int j = 0; j < A; ++j) ar[j] = avs[j];
-                logp[(size_t)step * NN + n] = lp;
-            }
+            e2_e[e] = tree_sum(sq);
+            store_lane(r_act, l < A ? (uint32_t)(((size_t)step * NN + n) * A + l) * 4 : OOB_OFF, sel_lane(avs, l));
+            store_lane(r_logp, l == 0 ? (uint32_t)((size_t)step * NN + n) * 4 : OOB_OFF, lp);
             PGM_STAMP(6);
-            // dynamics (fp64), time limit, auto-reset, VecNormalize accumulators
-            const double sn = env.step(s_o[e], ac, e2, objraw[e]);
+            // dynamics (fp64, lane = feature), time limit, auto-reset
+            sn_e[e] = env.next_state(s_o[e], ac);
             PGM_STAMP(7);
             const int el = elapsed[e] + 1;
-            done[e] = el >= maxs;
-            badf[e] = done[e] && el == maxs;
-            elapsed[e] = done[e] ? 0 : el;
-            s_o[e] = done[e] ? s0_o[e] : sn;
-#pragma unroll
-            for (int k = 0; k < K; ++k) objacc[e][k] = obj_valid ? objacc[e][k] * nc.gamma + objraw[e][k] : objraw[e][k];
-            ret[e] = ret[e] * nc.gamma + 0.0;  // SynthMO's scalar reward is 0 (vec_normalize.py:32)
+            const int dn = el >= maxs;
+            const int bf = dn && el == maxs;
+            elapsed[e] = dn ? 0 : el;
+            dcur[e] = dn;
+            s_o[e] = dn ? s0_o[e] : sn_e[e];
+            // statistics row: the observation now, the objective / ret accumulators of the previous step
             const double rv = role == 0 ? s_o[e] : role == 1 ? sel_lane_d(objacc[e], ko) : role == 2 ? ret[e] : 0.0;
             S.sr[buf][n][l] = rv;
-            PGM_STAMP(2);
+            // masks of step + 1 (lane 0: masks, lane 1: bad_masks)
+            const uint32_t moff = (uint32_t)((size_t)(step + 1) * NN + n) * 4;
+            store_lane(r_msk, l == 0 ? moff : OOB_OFF, dn ? 0.f : 1.f);
+            store_lane(r_bad, l == 0 ? moff : OOB_OFF, bf ? 0.f : 1.f);
+            if (e == 0) PGM_STAMP(2);
         }
-        obj_valid = 1;
         lds_sync();
         PGM_STAMP(3);
-        // ---- VecNormalize statistics, every wave (counts from before this step; numpy's mean / var
-        // divide by N, exact for N a power of two)
-        {
-            double v[NN], sum = 0.0;
-#pragma unroll
-            for (int n = 0; n < NN; ++n) {
-                v[n] = S.sr[buf][n][l];
-                sum += v[n];
-            }
-            constexpr double rn = 1.0 / NN;
-            const double bm = sum * rn;
-            double sq = 0.0;
-#pragma unroll
-            for (int n = 0; n < NN; ++n) sq = fma(v[n] - bm, v[n] - bm, sq);
-            if (upd) {
-                const double delta = bm - mean;
-                mean = mean + delta * (double)NN * itot;
-                var = (var * cnt + (sq * rn) * (double)NN + delta * delta * cnt * (double)NN * itot) * itot;
-                cnt += (double)NN;
-                inv = rsqrt_d(var + nc.eps);
-            }
-        }
+        merge(buf, role == 0 || step > 0);
         PGM_STAMP(4);
-        // ---- emit: normalised fp32 obs (next input), scaled objectives, masks
+        // ---- emit: normalised fp32 obs (next input); then the objective side, off the observation chain
 #pragma unroll
         for (int e = 0; e < NE; ++e) {
             const int n = w + 4 * e;
             if (n >= NN) break;
-            if (role == 0) {
+            {
                 double v = s_o[e];
-                if (nc.use_ob) v = clipd_hw((v - mean) * inv, -nc.clipob, nc.clipob);
+                if (nc.use_ob) v = clipd_s((v - mean) * inv, -nc.clipob, nc.clipob);
                 const float f = (float)v;  // VecPyTorch .float() (envs.py:192)
-                S.x[n][l] = f;
-                obs[((size_t)(step + 1) * NN + n) * O + l] = f;
-            } else if (role == 1) {
-                double r = sel_lane_d(objraw[e], ko);
-                if (nc.use_obj) r = clipd_hw(r * inv, -nc.cliprew, nc.cliprew);
-                rew[((size_t)step * NN + n) * K + ko] = (float)r;
+                if (role == 0) S.x[n][l] = f;
+                store_lane(r_obs, role == 0 ? (uint32_t)(((size_t)(step + 1) * NN + n) * O + l) * 4 : OOB_OFF, f);
             }
-            if (l == 0) {
-                masks[(size_t)(step + 1) * NN + n] = done[e] ? 0.f : 1.f;
-                bad[(size_t)(step + 1) * NN + n] = badf[e] ? 0.f : 1.f;
-            }
-            if (done[e]) {
-#pragma unroll
-                for (int k = 0; k < K; ++k) objacc[e][k] = 0.0;
-                ret[e] = 0.0;
-            }
+            if (step > 0) emit_reward(e, n, step - 1);
+            objective_side(e);  // resets by done_{t-1} first
+            dprev[e] = dcur[e];
         }
+        obj_valid = 1;
         wave_lds_fence_r();
         PGM_STAMP(5);
+    }
+
+    // ---- drain: merge the last step's objective / ret accumulators, its reward, the done reset
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+        const int n = w + 4 * e;
+        if (n >= NN) break;
+        const double rv = role == 1 ? sel_lane_d(objacc[e], ko) : role == 2 ? ret[e] : 0.0;
+        S.sr[T & 1][n][l] = rv;
+    }
+    lds_sync();
+    merge(T & 1, role == 1 || role == 2);
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+        const int n = w + 4 * e;
+        if (n >= NN) break;
+        emit_reward(e, n, T - 1);
+        if (dprev[e]) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) objacc[e][k] = 0.0;
+            ret[e] = 0.0;
+        }
     }
 
     // ---- env state and statistics back to HBM
@@ -439,7 +515,6 @@ __global__ __launch_bounds__(256) void rollout_lane_kernel(RolloutArgs a) {
     }
     PGM_STAMP_FLUSH;
 }
-
 // ------------------------------------------------------------------------------------------ critic values
 // values[p][i][:] = critic(obs[p][i]) for all (T+1) x N stored rows of a task (get_value on every step's
 // obs, model.py:71-73, and the bootstrap value on obs[T]).  One thread per row, critic tower in LDS

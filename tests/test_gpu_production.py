@@ -138,9 +138,17 @@ def test_production_iteration(gpu, env, P, N):
 @pytest.mark.parametrize('env,P,eval_num', [('MO-Walker2d-v2', 40, 1), ('MO-HalfCheetah-v2', 20, 1),
                                              ('MO-Hopper-v3', 27, 2), ('MO-Humanoid-v2', 20, 6)])
 def test_production_eval_all_tasks(gpu, env, P, eval_num):
-    """pgm_eval over the production population (Humanoid: eval_num 6, scripts/humanoid-v2.py:45).  Humanoid's
-    1000-step episodes are chaotic under a 376-input fp32 policy (see test_gpu_kernels.test_rollout), so its
-    episodes are cut to 30 steps on both sides (the time limit is a field of the env spec)."""
+    """pgm_eval over the production population (Humanoid: eval_num 6, scripts/humanoid-v2.py:45), every task.
+
+    A deterministic episode can be chaotic: for some policies a 1e-7 relative change of the parameters
+    moves the 500-step objective sums of SynthMO-Walker by ~11 (measured with the fp64 oracle alone), so a
+    fixed fp32-vs-fp64 tolerance is meaningless for them.  Each task's tolerance is therefore
+    1e-4 + 1e-5 |ref| + 10 x the oracle's OWN change under a random relative parameter perturbation (its
+    sensitivity, max of two draws at the scale of fp32 rounding over a layer's fan-in, 2^-24 sqrt(O + 64));
+    most tasks stay at the tight bar (asserted).  Humanoid episodes are cut to 30 steps on
+    both sides (the time limit is a field of the env spec): its 376-input policy is chaotic within tens of
+    steps (see test_gpu_kernels.test_rollout)."""
+    import copy
     from oracle.mopg import evaluation as oracle_evaluation
     from oracle.vecenv import RunningMeanStd
     spec, tb, pols = _batch_with_policies(env, P, 4, 8, seed=5, scale=0.1, eval_num=eval_num)
@@ -158,5 +166,21 @@ def test_production_eval_all_tasks(gpu, env, P, eval_num):
         tb.set_env_params(p, {'ob_rms': r})
     objs = tb.evaluate().cpu().numpy()
     s0_eval = envspec.reset_table(spec['obs_dim'], 0, eval_num)
+    gen = torch.Generator().manual_seed(99)
+    # perturbation scale: fp32 rounding accumulated over a layer's fan-in, 2^-24 sqrt(obs_dim + H)
+    eps = 2.0 ** -24 * np.sqrt(spec['obs_dim'] + 64)
+    tight = 0
     for p in range(P):
-        _close(objs[p], oracle_evaluation(args, spec, s0_eval, pols[p], rms[p]), 1e-4, 1e-5, f'{env} task {p}: objs')
+        ref = oracle_evaluation(args, spec, s0_eval, pols[p], rms[p])
+        sens = np.zeros_like(ref)
+        for _ in range(2):
+            q = copy.deepcopy(pols[p])
+            with torch.no_grad():
+                for prm in q.parameters():
+                    prm.mul_(1 + eps * torch.randn(prm.shape, generator=gen, dtype=torch.float64))
+            sens = np.maximum(sens, np.abs(oracle_evaluation(args, spec, s0_eval, q, rms[p]) - ref))
+        tight += bool((sens < 1e-5 * np.abs(ref) + 1e-4).all())
+        err = np.abs(objs[p] - ref)
+        tol = 1e-4 + 1e-5 * np.abs(ref) + 10 * sens
+        assert (err <= tol).all(), f'{env} task {p}: objs {objs[p]} vs oracle {ref}, err {err}, tol {tol}'
+    assert tight >= P // 2, f'only {tight}/{P} tasks non-chaotic: the check lost its teeth'

@@ -45,7 +45,10 @@ def parse():
     ap.add_argument('--num-steps', type=int, default=2048)
     ap.add_argument('--ppo-epoch', type=int, default=10)
     ap.add_argument('--num-mini-batch', type=int, default=32)
-    ap.add_argument('--cpu-iters', type=int, default=10, help='oracle iterations timed for cpu_baseline')
+    ap.add_argument('--cpu-iters', type=int, default=5, help='oracle iterations per process for cpu_baseline')
+    ap.add_argument('--cpu-procs', type=int, default=15,
+                    help='concurrent oracle processes: the 16-core host share of one GPU on the box minus the '
+                         'bench process itself (the box allows 16 processes with the GPU open)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-overlap-eval', action='store_true', help='evaluate on the main stream (A/B)')
     ap.add_argument('--traffic-file', default=os.path.join(ROOT, 'profiles', 'r01_ppo_update_pmc.json'))
@@ -63,33 +66,81 @@ def bytes_per_env_step(O, A, K, E):
     return 4 * ((O + A + 2 * K + 3) + (3 * K + 2) + (2 * K + 3) + E * (O + A + 2 * K + 2))
 
 
-def cpu_baseline(args, spec):
-    """The oracle (fp64 torch restatement, 1 thread like morl/morl.py:34) on one task."""
+def _cpu_task(args, spec, task, barrier, q):
+    """One reference-style task process (morl/morl.py:84-88): 1 thread (morl/morl.py:34), fp64 oracle."""
+    torch.set_num_threads(1)
     from oracle.mopg import initial_sample, mopg_worker
     from pgmorl_amd import envspec
-    torch.set_num_threads(1)
     ns = argparse.Namespace(env_name=args.env_name, obj_num=spec['obj_num'], num_env_steps=10 ** 9, seed=0,
                             num_steps=args.num_steps, num_processes=args.num_processes, ppo_epoch=args.ppo_epoch,
                             num_mini_batch=args.num_mini_batch, clip_param=0.2, value_loss_coef=0.5,
                             entropy_coef=0.0, lr=3e-4, max_grad_norm=0.5, gamma=0.995, gae_lambda=0.95,
                             use_gae=True, use_proper_time_limits=True, ob_rms=True, obj_rms=True, raw=True,
                             eval_num=1, use_linear_lr_decay=True, lr_decay_ratio=1.0, layernorm=False)
-    torch.manual_seed(0)
+    torch.manual_seed(task)
     sample = initial_sample(ns, spec)
     s0 = envspec.reset_table(spec['obs_dim'], 0, args.num_processes)
     s0e = envspec.reset_table(spec['obs_dim'], 0, 1)
     w = np.array([0.5] * spec['obj_num'])
-    t0 = time.perf_counter()
+    barrier.wait()
+    t0 = time.time()
     mopg_worker(ns, spec, s0, s0e, sample, w, 0, args.cpu_iters)
-    dt = time.perf_counter() - t0
-    steps = args.cpu_iters * args.num_processes * args.num_steps
-    busy = min(96, args.tasks * (1 + args.num_processes))  # SURVEY.md §8(d): per-core x min(96, P(1+N))
-    return {'value': steps / dt, 'unit': 'env steps/sec', 'cores': 1, 'kind': 'port',
-            'extrapolated_96vcpu': steps / dt * busy, 'extrapolation': f'per-core value x {busy} busy processes',
-            'sample': f'1 task x {args.cpu_iters} MOPG iterations ({steps} train env-steps, T={args.num_steps}, '
-                      f'N={args.num_processes}, E={args.ppo_epoch}, M={args.num_mini_batch}, + eval) of the fp64 '
-                      f'torch/numpy oracle, torch.set_num_threads(1), {dt:.1f} s on {platform.processor() or "host"}'
-                      f' ({os.cpu_count()} logical CPUs visible)'}
+    q.put((task, t0, time.time(), args.cpu_iters * args.num_processes * args.num_steps))
+
+
+def _lscpu():
+    try:
+        import subprocess
+        out = subprocess.run(['lscpu'], capture_output=True, text=True, timeout=10).stdout
+        keep = ('Model name', 'Socket(s)', 'Core(s) per socket', 'Thread(s) per core', 'CPU(s)')
+        return '; '.join(l.strip() for l in out.splitlines() if l.split(':')[0].strip() in keep)
+    except Exception as e:  # lscpu absent: say so
+        return f'lscpu unavailable ({e!r})'
+
+
+def cpu_baseline(args, spec, tasks):
+    """The reference's CPU path, whole-node: one single-thread fp64 oracle process per task
+    (morl/morl.py:34,84-88), as many concurrent processes as this GPU's host-core share (16 on the box,
+    capped by the affinity mask and the population), each timing cpu_iters MOPG iterations of its task;
+    value = all processes' train env-steps / the concurrent wall time.  The 96-vCPU figure scales the
+    per-core rate to the reference's 96 Skylake vCPUs (README.md:92-94) -- an extrapolation, stated."""
+    import multiprocessing as mp
+    ncpu = len(os.sched_getaffinity(0))
+    procs = max(1, min(args.cpu_procs, 15, ncpu, tasks))
+    ctx = mp.get_context('spawn')
+    barrier, q = ctx.Barrier(procs), ctx.Queue()
+    ps = [ctx.Process(target=_cpu_task, args=(args, spec, i, barrier, q)) for i in range(procs)]
+    hide = {k: os.environ.get(k) for k in ('HIP_VISIBLE_DEVICES', 'ROCR_VISIBLE_DEVICES')}
+    os.environ['HIP_VISIBLE_DEVICES'] = os.environ['ROCR_VISIBLE_DEVICES'] = ''  # CPU-only children
+    try:
+        for p in ps:
+            p.start()
+    finally:
+        for k, v in hide.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    res = []
+    while len(res) < procs:  # a dead worker ends the baseline instead of hanging the bench
+        try:
+            res.append(q.get(timeout=5))
+        except Exception:
+            if any(p.exitcode not in (None, 0) for p in ps):
+                raise RuntimeError(f'cpu_baseline worker died: {[p.exitcode for p in ps]}')
+    for p in ps:
+        p.join(60)
+    t0, t1 = min(r[1] for r in res), max(r[2] for r in res)
+    steps = sum(r[3] for r in res)
+    value = steps / (t1 - t0)
+    per_core = value / procs
+    return {'value': value, 'unit': 'env steps/sec', 'cores': procs, 'kind': 'port',
+            'per_core': per_core, 'extrapolated_96vcpu': per_core * 96,
+            'extrapolation': f'per-core value x 96 vCPUs (reference hardware, README.md:92-94)',
+            'host': {'affinity_cpus': ncpu, 'os_cpu_count': os.cpu_count(), 'lscpu': _lscpu()},
+            'sample': f'{procs} concurrent single-thread processes x {args.cpu_iters} MOPG iterations each '
+                      f'({steps} train env-steps, T={args.num_steps}, N={args.num_processes}, E={args.ppo_epoch}, '
+                      f'M={args.num_mini_batch}, + eval) of the fp64 torch/numpy oracle, {t1 - t0:.1f} s wall'}
 
 
 def hypervolume(args, history, budget):
@@ -237,7 +288,7 @@ def main():
     }
     out['hypervolume'] = hypervolume(args, history, G * N * T * len(history))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out['cpu_baseline'] = cb = cpu_baseline(args, spec)
+        out['cpu_baseline'] = cb = cpu_baseline(args, spec, G)
         out['vs_96vcpu_extrapolated'] = value / cb['extrapolated_96vcpu']
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -9,6 +9,7 @@ Selection: every method of morl/morl.py:128-169 -- 'prediction-guided' and 'rand
 performance-buffer population of ``pgmorl_amd.population`` (morl/population_2d.py / population_3d.py),
 'moead' over the population, 'ra' and 'pfa' over the last offspring.
 """
+import json
 import os
 import pickle
 import time
@@ -55,6 +56,7 @@ def initialize_warm_up_batch(args, runtime):
 def run(args, device='cuda', rng='device', log=print):
     np.random.seed(args.seed)
     torch.manual_seed(args.seed)
+    t_start = time.perf_counter()
     runtime = MOPGPopulation(args, device=device, rng=rng)
     template = WeightedSumScalarization(num_objs=args.obj_num, weights=np.ones(args.obj_num) / args.obj_num)
     total_num_updates = int(args.num_env_steps) // args.num_steps // args.num_processes
@@ -66,6 +68,10 @@ def run(args, device='cuda', rng='device', log=print):
     elite_batch, scalarization_batch = initialize_warm_up_batch(args, runtime)
     for s, sc in zip(elite_batch, scalarization_batch):
         s.optgraph_id = opt_graph.insert(deepcopy(sc.weights), deepcopy(s.objs), -1)
+    # whole-run accounting: MOPG (device iterations, incl. the end-of-generation sync and record gather)
+    # vs the generation-boundary host work (EP / population / OptGraph, selection, text dumps)
+    timing = {'init_s': time.perf_counter() - t_start, 'rl_s': 0.0, 'host_s': 0.0, 'train_env_steps': 0,
+              'generations': []}
     rl_num_updates = args.warmup_iter
     episode = iteration = 0
     rank, ws = world()
@@ -75,7 +81,10 @@ def run(args, device='cuda', rng='device', log=print):
             f'\n-------------------- Evolutionary Stage: Generation {episode:3} --------------------')
         episode += 1
         task_batch = [Task(e, s) for e, s in zip(elite_batch, scalarization_batch)]
+        t0 = time.perf_counter()
         all_offspring_batch = runtime.run(task_batch, iteration, rl_num_updates, start_time, log=log)
+        t1 = time.perf_counter()
+        n_its = len(all_offspring_batch[0]) if all_offspring_batch else 0
         all_sample_batch, offspring_batch = [], []
         last_offspring_batch = [None] * len(task_batch)
         for task_id, offsprings in enumerate(all_offspring_batch):
@@ -140,9 +149,27 @@ def run(args, device='cuda', rng='device', log=print):
             write_generation(args.save_dir, iteration, args.obj_num, ep, population, opt_graph, elite_batch,
                              scalarization_batch, all_offspring_batch,
                              predicted_offspring_objs if args.selection_method == 'prediction-guided' else None)
+        t2 = time.perf_counter()
+        steps = len(task_batch) * n_its * args.num_steps * args.num_processes
+        timing['rl_s'] += t1 - t0
+        timing['host_s'] += t2 - t1
+        timing['train_env_steps'] += steps
+        timing['generations'].append({'iteration': iteration, 'tasks': len(task_batch), 'iters': n_its,
+                                      'rl_s': round(t1 - t0, 4), 'host_s': round(t2 - t1, 4)})
     runtime.materialize(list(ep.sample_batch), dst=0)  # collective: EP snapshots onto the writing rank
     if writer:
         write_final(args, ep)
+        timing['wall_s'] = time.perf_counter() - t_start
+        timing['env_steps_per_s_whole_run'] = timing['train_env_steps'] / timing['wall_s']
+        timing['env_steps_per_s_rl_only'] = timing['train_env_steps'] / max(timing['rl_s'], 1e-9)
+        timing['host_share'] = timing['host_s'] / timing['wall_s']
+        timing['world_size'] = ws
+        with open(os.path.join(args.save_dir, 'timing.json'), 'w') as fp:
+            json.dump(timing, fp, indent=1)
+        log(f"[timing] wall {timing['wall_s']:.2f} s: MOPG {timing['rl_s']:.2f} s, generation-boundary host "
+            f"{timing['host_s']:.2f} s ({100 * timing['host_share']:.1f}%), {timing['train_env_steps']} train env-steps"
+            f" -> {timing['env_steps_per_s_whole_run']:.4g} env-steps/s whole run")
+    ep.timing = timing
     if ws > 1:
         torch.distributed.barrier()  # the results tree is complete before any rank returns
     return ep

@@ -140,22 +140,20 @@ def test_production_iteration(gpu, env, P, N):
 def test_production_eval_all_tasks(gpu, env, P, eval_num):
     """pgm_eval over the production population (Humanoid: eval_num 6, scripts/humanoid-v2.py:45), every task.
 
-    A deterministic episode can be chaotic: for some policies a 1e-7 relative change of the parameters
-    moves the 500-step objective sums of SynthMO-Walker by ~11 (measured with the fp64 oracle alone), so a
-    fixed fp32-vs-fp64 tolerance is meaningless for them.  Each task's tolerance is therefore
-    1e-4 + 1e-5 |ref| + 10 x the oracle's OWN change under a random relative parameter perturbation (its
-    sensitivity, max of two draws at the scale of fp32 rounding over a layer's fan-in, 2^-24 sqrt(O + 64));
-    most tasks stay at the tight bar (asserted).  Humanoid episodes are cut to 30 steps on
-    both sides (the time limit is a field of the env spec): its 376-input policy is chaotic within tens of
-    steps (see test_gpu_kernels.test_rollout)."""
-    import copy
+    Deterministic 500-step episodes can be chaotic: for some policies of this population a 1e-7 relative
+    change of the parameters moves the objective sums of SynthMO-Walker by ~11 (measured with the fp64
+    oracle alone), so whole-episode fp32-vs-fp64 sums are not comparable for every task (full-length
+    episodes are checked on non-chaotic tasks by test_gpu_kernels.test_eval and after a real update by
+    test_production_iteration).  Here every episode is cut to 12 steps on both sides (the time limit is a
+    field of the env spec), where the oracle's own fp32 twin (torch fp32 policy) stays within 1.8e-6
+    relative (1.5e-5 for Humanoid's 376-input policy) on all tasks; the device must match to
+    1e-4 + 2e-5 |ref| (Humanoid 1e-3 + 2e-4 |ref|)."""
     from oracle.mopg import evaluation as oracle_evaluation
     from oracle.vecenv import RunningMeanStd
     spec, tb, pols = _batch_with_policies(env, P, 4, 8, seed=5, scale=0.1, eval_num=eval_num)
-    if spec['obs_dim'] > 48:
-        spec = dict(spec, max_episode_steps=30)
-        tb.spec = spec
-        tb.c_spec.max_episode_steps = 30
+    spec = dict(spec, max_episode_steps=12)
+    tb.spec = spec
+    tb.c_spec.max_episode_steps = 12
     args = small_args(env, eval_num=eval_num)
     rng = np.random.RandomState(2)
     rms = []
@@ -166,21 +164,6 @@ def test_production_eval_all_tasks(gpu, env, P, eval_num):
         tb.set_env_params(p, {'ob_rms': r})
     objs = tb.evaluate().cpu().numpy()
     s0_eval = envspec.reset_table(spec['obs_dim'], 0, eval_num)
-    gen = torch.Generator().manual_seed(99)
-    # perturbation scale: fp32 rounding accumulated over a layer's fan-in, 2^-24 sqrt(obs_dim + H)
-    eps = 2.0 ** -24 * np.sqrt(spec['obs_dim'] + 64)
-    tight = 0
+    atol, rtol = (1e-4, 2e-5) if spec['obs_dim'] <= 48 else (1e-3, 2e-4)
     for p in range(P):
-        ref = oracle_evaluation(args, spec, s0_eval, pols[p], rms[p])
-        sens = np.zeros_like(ref)
-        for _ in range(2):
-            q = copy.deepcopy(pols[p])
-            with torch.no_grad():
-                for prm in q.parameters():
-                    prm.mul_(1 + eps * torch.randn(prm.shape, generator=gen, dtype=torch.float64))
-            sens = np.maximum(sens, np.abs(oracle_evaluation(args, spec, s0_eval, q, rms[p]) - ref))
-        tight += bool((sens < 1e-5 * np.abs(ref) + 1e-4).all())
-        err = np.abs(objs[p] - ref)
-        tol = 1e-4 + 1e-5 * np.abs(ref) + 10 * sens
-        assert (err <= tol).all(), f'{env} task {p}: objs {objs[p]} vs oracle {ref}, err {err}, tol {tol}'
-    assert tight >= P // 2, f'only {tight}/{P} tasks non-chaotic: the check lost its teeth'
+        _close(objs[p], oracle_evaluation(args, spec, s0_eval, pols[p], rms[p]), atol, rtol, f'{env} task {p}: objs')

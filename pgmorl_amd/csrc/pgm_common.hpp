@@ -21,10 +21,11 @@ struct Layout {
     int32_t total;
 };
 Layout make_layout(int O, int A, int K, int Hd);
-// pgm_ppo_update workspace: [4P + 1] tagged 8-byte granules (tower-norm hand-offs; word 2P = timeout flag),
-// padded to 256 bytes; the gradient exchange of the half-split update, [P][2 towers][2 halves][2 parities]
-// slots of (tower image + 1) granules; then the packed sample table [P][T*N][RS] fp32 (obs | action |
-// old logp | adv | old value | return, RS a power of 2)
+// pgm_ppo_update workspace: [2 PGM_NS_MAX P + 1] tagged 8-byte granules (tower-norm hand-offs of every
+// (task, tower, row part); word 2P = timeout flag), padded to 256 bytes; the gradient exchange of the
+// row-split updates, [P][2 towers][PGM_NS_MAX row parts][2 parities] slots of (tower image + 1) granules; then
+// the packed sample table [P][T*N][RS] fp32 (obs | action | old logp | adv | old value | return, RS a power
+// of 2)
 inline int ppo_row_stride(int O, int A, int K) {
     const int n = O + A + 2 + 2 * K;
     return n <= 16 ? 16 : n <= 32 ? 32 : n <= 64 ? 64 : 128;
@@ -33,10 +34,15 @@ constexpr int ppo_img_floats(int O, int A, int K) {  // TowerImg<O, A, K> of pgm
     const int Q = A > K ? A : K;
     return O * H + H * (H + 1) + Q * H + 2 * H + Q + A;
 }
-inline size_t ppo_flag_bytes(int P) { return ((size_t)(4 * P + 1) * 8 + 255) / 256 * 256; }
+constexpr int PGM_NS_MAX = 4;  // workgroups per tower of the row-split updates
+inline size_t ppo_flag_bytes(int P) { return ((size_t)(2 * PGM_NS_MAX * P + 1) * 8 + 255) / 256 * 256; }
+// norm granule of (task p, tower m, row part hs): row part 0 below the timeout word, the others above it
+__host__ __device__ inline int ppo_norm_granule(int P, int p, int m, int hs) {
+    return hs == 0 ? 2 * p + m : 2 * P + 1 + 2 * P * (hs - 1) + 2 * p + m;
+}
 inline int ppo_xslot(int O, int A, int K) { return (ppo_img_floats(O, A, K) + 1 + 31) / 32 * 32; }  // granules
-inline size_t ppo_xbuf_bytes(const pgm_dims* d) {
-    return d->O <= 32 ? (size_t)d->P * 8 * ppo_xslot(d->O, d->A, d->K) * 8 : 0;
+inline size_t ppo_xbuf_bytes(const pgm_dims* d, int ns = PGM_NS_MAX) {
+    return d->O <= 32 ? (size_t)d->P * 2 * ns * 2 * ppo_xslot(d->O, d->A, d->K) * 8 : 0;
 }
 int wide_xslot_words(int O, int A, int K);  // pgm_ppo_wide.hip: small image + dW1 + flag granule, 8-B words
 // obs_dim > 32 (wide kernel): flags, exchange slots [P][2 towers][2 halves][2 parities], half 1's private

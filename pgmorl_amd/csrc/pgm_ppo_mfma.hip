@@ -856,6 +856,704 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
     PGM_STAMP_FLUSH;
 }
 
+// ================================================================ 16-row tiles, NS workgroups per tower
+// ppo_update_t16_kernel<O, A, K, NS, W>: each tower of a task runs on NS workgroups of W waves; workgroup hs
+// takes rows [hs mb / NS, (hs + 1) mb / NS) of every minibatch, one 16-sample tile per wave on the
+// v_mfma_f32_16x16x4_f32 (half the rows of the 32x32x2 tile, so a tile's dependent chain is about half as
+// long, and with W = 8 two waves share each SIMD's matrix pipe).  Layout of the 16x16x4 form:
+//     C/D:  lane l, register r  <->  (sample 4(l >> 4) + r, feature l & 15)
+//     A:    lane l holds A[i = l & 15][k = l >> 4];   B: lane l holds B[k = l >> 4][j = l & 15]
+// so, as in the 32-row kernel, weight gradients (sums over samples) take both operands straight from the C
+// registers (register r = k-step r), and only the feature-contracting products (Z2 = H1 W2^T,
+// dH1 = dZ2 W2, the heads) transpose through a per-wave LDS tile.  The heads run on the MFMA too, which
+// leaves every per-(sample, output) loss term in C layout: the actor's log-prob sums over the outputs of a
+// sample are 16-lane DPP row sums.
+//
+// Per minibatch step: the W waves' register partials are summed into ONE LDS image in W rounds (round j:
+// wave w adds its blocks of slice (w + j) mod W; every slice is summed in a fixed wave order), the NS
+// images of a tower are exchanged through 16-B sc1 publishes + tagged flags (every workgroup sums them in
+// row-part order h = 0..NS-1, so all NS copies of the Adam step are bitwise identical), the two towers
+// exchange their squared norms as tagged 8-byte granules, and Adam runs from registers.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int T16 = 16;       // samples per tile
+constexpr int S16 = H + 2;    // transpose-tile row stride: conflict-free A-operand reads, 2-way (free) writes
+constexpr int DQ = 8;         // head-output columns of the dO transpose tile (Q <= 8)
+constexpr int DQS = DQ + 1;
+
+__device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+// sum over the four 16-lane groups (lanes c, c + 16, c + 32, c + 48), result in all of them
+__device__ __forceinline__ float group4_sum(float v) {
+    v = half_sum(v);                                               // l ^ 32 (v_permlane32_swap)
+    return v + __shfl_xor(v, 16, 64);                              // l ^ 16
+}
+
+template <int O, int A, int K, int W, int NBUF>
+struct T16SmemT {
+    static constexpr int Q = qmax<A, K>();
+    static constexpr int IMG = img_floats<O, A, K>();
+    static constexpr int RS = row_stride<O, A, K>();
+    static constexpr int SBk = W * T16;     // samples staged per pass (one tile per wave)
+    static constexpr int RSL = RS + 4;
+    TowerImg<O, A, K> Pm;                   // parameters of this workgroup's tower
+    float MV[2 * IMG];                      // Adam exp_avg | exp_avg_sq images
+    alignas(16) float RB[NBUF][SBk * RSL];  // packed rows of the current / next pass
+    int32_t IB[2][SBk];                     // sample indices of the next two passes
+    float dout[W][T16][DQS];                // per-wave dL/d(head output), transposed for dH2
+    float aiv[A];                           // actor 1 / std^2
+    float red[32];
+    union Big {
+        float scr[W][T16][S16];             // transpose tiles during the passes
+        float GA[IMG];                      // the workgroup's gradient image after them
+    } big;
+};
+template <int O, int A, int K, int W>
+constexpr int t16_nbuf() { return sizeof(T16SmemT<O, A, K, W, 2>) <= 160 * 1024 ? 2 : 1; }
+template <int O, int A, int K, int W>
+using T16Smem = T16SmemT<O, A, K, W, t16_nbuf<O, A, K, W>()>;
+
+template <int O, int A, int K, int NS, int W>
+__global__ __launch_bounds__(64 * W) void ppo_update_t16_kernel(MArgs a) {
+    static_assert(O <= 32, "two 16-feature blocks of layer-1 inputs");
+    using Sm = T16Smem<O, A, K, W>;
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    auto& S = *reinterpret_cast<Sm*>(smem_raw);
+    constexpr int NT = 64 * W;
+    constexpr int Q = qmax<A, K>();
+    static_assert(Q <= DQ, "head outputs beyond the dO tile");
+    constexpr int KS1 = (O + 3) / 4;   // k-steps of layer 1
+    constexpr int K1B = (O + 15) / 16; // 16-feature blocks of the layer-1 inputs
+    constexpr int IMG = Sm::IMG, SBk = Sm::SBk, RS = Sm::RS, RSL = Sm::RSL;
+    constexpr int NBUF = t16_nbuf<O, A, K, W>();
+    constexpr int CR = RS / 4;
+    constexpr int NDT = (SBk * RSL) / 256;
+    static_assert(NDT * 256 == SBk * RSL, "staging split");
+    constexpr int oW2 = O * H, oWh = oW2 + H * SCR, oB1 = oWh + Q * H, oB2 = oB1 + H, oBh = oB2 + H, oLs = oBh + Q;
+    const int t = threadIdx.x, l = t & 63, g = l >> 4, c = l & 15;
+    const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+    // block map: in each group of 8 NS blocks, block r holds row part r >> 3 of tower r & 1 of task
+    // 4 G + ((r & 7) >> 1): the NS parts of a tower are blocks b, b + 8, b + 16, ... (one XCD under round-robin
+    // placement -- speed only, the hand-off is correct anywhere)
+    const int bx = (int)blockIdx.x, r8 = bx % (8 * NS);
+    const int p = 4 * (bx / (8 * NS)) + ((r8 & 7) >> 1);
+    const int hs = r8 >> 3, m = r8 & 1;
+    if (p >= a.P) return;
+    const int NQ = m == 0 ? K : A;
+    const int N = a.N, T = a.T, B = T * N;
+    const int E = a.hp.ppo_epoch, M = a.hp.num_mini_batch;
+    const int mb = B / M, nb = B / mb;
+    const int r0 = hs * mb / NS, mbs = (hs + 1) * mb / NS - r0;
+    const int npm = (mbs + SBk - 1) / SBk;
+    const int npass = E * nb * npm;
+    const float clip = a.hp.clip_param;
+    const Layout& L = a.L;
+    float* __restrict__ P = a.params + (size_t)p * L.total;
+    float* __restrict__ Mo = a.m + (size_t)p * L.total;
+    float* __restrict__ Vo = a.v + (size_t)p * L.total;
+    const float* rows = a.rows + (size_t)p * B * RS;
+
+    auto issue_idx = [&](int gi, int buf) {
+        const int e = gi / (nb * npm), rem = gi - e * nb * npm, bb = rem / npm, j = rem - bb * npm;
+        const int ns = min(SBk, mbs - j * SBk);
+        const int32_t* src = a.perms + (size_t)e * B + bb * mb + r0 + j * SBk;
+        for (int q0 = w * 64; q0 < SBk; q0 += NT)  // rows beyond ns re-read the last valid index
+            __builtin_amdgcn_global_load_lds((const void*)(src + min(q0 + l, ns - 1)),
+                                             (lds_void_t*)&S.IB[buf][q0], 4, 0, 0);
+    };
+    auto issue_rows = [&](int buf, int ibuf) {
+        float* base = &S.RB[buf][0];
+        constexpr int NI = (NDT + W - 1) / W;
+        int idx[NI];
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int d = w + W * i, pos = d * 256 + 4 * l, row = min(pos / RSL, SBk - 1);
+            idx[i] = S.IB[ibuf][row];
+        }
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int d = w + W * i;
+            if (d < NDT) {
+                const int pos = d * 256 + 4 * l, row = pos / RSL, chunk = (pos - row * RSL) >> 2;
+                const float* src = rows + (size_t)idx[i] * RS + (chunk < CR ? chunk : 0) * 4;
+                __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_t*)(base + d * 256), 16, 0, 0);
+            }
+        }
+    };
+
+    // ---- parameter and Adam moment images from the flat HBM vectors
+    float* Pf = &S.Pm.W1t[0][0];
+    if (t < A) S.aiv[t] = expf(-2.f * P[L.off[PGM_P_LOGSTD] + t]);
+    for (int i = t; i < IMG; i += NT) {
+        const int f = img_to_flat<O, A, K>(i, m, L);
+        Pf[i] = f >= 0 ? P[f] : 0.f;
+        S.MV[i] = f >= 0 ? Mo[f] : 0.f;
+        S.MV[IMG + i] = f >= 0 ? Vo[f] : 0.f;
+    }
+    issue_idx(0, 0);
+    if (npass > 1) issue_idx(1, 1);
+    dma_sync_m();
+    issue_rows(0, 0);
+    dma_sync_m();
+    auto& Wt = S.Pm;
+    const float* lstd = S.Pm.logstd;  // actor logstd (critic: zeros, unused)
+
+    const int step0 = a.step[p];
+    const double lr = a.lr[p];
+    const float b1c = a.hp.beta1, b2c = a.hp.beta2, eps = a.hp.adam_eps;
+    const float vscale = a.hp.value_loss_coef * 0.5f / (float)(mb * K);
+    const float ascale = -1.f / (float)mb;
+    float st_v = 0.f, st_a = 0.f, st_e = 0.f;
+    int nstep = 0, gp = 0;
+    double b1p = pow((double)b1c, (double)step0), b2p = pow((double)b2c, (double)step0);
+    float* scr = &S.big.scr[w][0][0];
+    float* dtile = &S.dout[w][0][0];
+    PGM_STAMP_DECL
+
+    for (int e = 0; e < E; ++e) {
+        for (int bb = 0; bb < nb; ++bb) {
+            f32x4 gW2[4][4], gW1[K1B][4], gWh[4];
+            float gB1[4], gB2[4], gbh = 0.f, gls = 0.f, lsum = 0.f;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) gW2[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int kb = 0; kb < K1B; ++kb) gW1[kb][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+                gWh[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+                gB1[i] = gB2[i] = 0.f;
+            }
+
+            for (int s0 = 0; s0 < mbs; s0 += SBk, ++gp) {
+                const int ns = min(SBk, mbs - s0);
+                const int cur = NBUF == 2 ? (gp & 1) : 0;
+                if constexpr (NBUF == 2) {
+                    if (gp + 1 < npass) issue_rows(cur ^ 1, (gp + 1) & 1);
+                    if (gp + 2 < npass) issue_idx(gp + 2, gp & 1);
+                }
+                const float* rb = &S.RB[cur][0];
+                PGM_STAMP(0);
+
+                for (int tile = w; tile * T16 < ns; tile += W) {
+                    const int ts0 = tile * T16;
+                    const float* rt = rb + ts0 * RSL;
+                    // ---- layer 1: Z1[s][h] = X[s][:] . W1t[:][h]
+                    f32x4 z[4] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f},
+                                  f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+                    for (int ks = 0; ks < KS1; ++ks) {
+                        const int k = 4 * ks + g;
+                        const bool kv = k < O;
+                        const float av = kv ? rt[c * RSL + k] : 0.f;
+#pragma unroll
+                        for (int hb = 0; hb < 4; ++hb) z[hb] = mfma16(av, kv ? Wt.W1t[kv ? k : 0][hb * T16 + c] : 0.f, z[hb]);
+                    }
+                    f32x4 H1[4];
+#pragma unroll
+                    for (int hb = 0; hb < 4; ++hb) {
+                        const float bias = Wt.b1[hb * T16 + c];
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            H1[hb][r] = tanh_fast(z[hb][r] + bias);
+                            scr[(4 * g + r) * S16 + hb * T16 + c] = H1[hb][r];
+                        }
+                    }
+                    wave_lds_fence();
+                    // ---- layer 2: Z2[s][o] = H1[s][:] . W2t[:][o]  (A from the transpose tile)
+#pragma unroll
+                    for (int ob = 0; ob < 4; ++ob) z[ob] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+                    for (int ks = 0; ks < H / 4; ++ks) {
+                        const int k = 4 * ks + g;
+                        const float av = scr[c * S16 + k];
+#pragma unroll
+                        for (int ob = 0; ob < 4; ++ob) z[ob] = mfma16(av, Wt.W2t[k][ob * T16 + c], z[ob]);
+                    }
+                    f32x4 H2[4];
+#pragma unroll
+                    for (int ob = 0; ob < 4; ++ob) {
+                        const float bias = Wt.b2[ob * T16 + c];
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) H2[ob][r] = tanh_fast(z[ob][r] + bias);
+                    }
+                    PGM_STAMP(4);
+                    wave_lds_fence();  // every lane finished reading the H1 tile
+#pragma unroll
+                    for (int ob = 0; ob < 4; ++ob)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) scr[(4 * g + r) * S16 + ob * T16 + c] = H2[ob][r];
+                    wave_lds_fence();
+                    // ---- heads on the MFMA: out[s][q] = H2[s][:] . Wh[q][:]  (q = lane column, < Q)
+                    f32x4 ho = f32x4{0.f, 0.f, 0.f, 0.f};
+                    const bool qv = c < Q;
+#pragma unroll 4
+                    for (int ks = 0; ks < H / 4; ++ks) {
+                        const int k = 4 * ks + g;
+                        ho = mfma16(scr[c * S16 + k], qv ? Wt.Wh[qv ? c : 0][k] : 0.f, ho);
+                    }
+                    // ---- per-(sample, output) loss gradients in C layout (ppo.py:80-96): register r is sample
+                    // 4g + r of the tile, lane column c is head output q
+                    const float bh = qv ? Wt.bh[c] : 0.f;
+                    f32x4 dO;
+                    if (m == 0) {  // value loss over the K objectives
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int s = 4 * g + r;
+                            const bool ok = ts0 + s < ns && c < K;
+                            const float V = ho[r] + bh;
+                            const float Vold = rt[s * RSL + O + A + 2 + (c < K ? c : 0)];
+                            const float R = rt[s * RSL + O + A + 2 + K + (c < K ? c : 0)];
+                            float gv, ls;
+                            if (a.hp.use_clipped_value_loss) {
+                                const float dv = V - Vold;
+                                const float vc = Vold + fminf(fmaxf(dv, -clip), clip);
+                                const float l1 = (V - R) * (V - R), l2 = (vc - R) * (vc - R);
+                                const float inr = (dv >= -clip && dv <= clip) ? 1.f : 0.f;
+                                gv = wmax2(l1, l2) * 2.f * (V - R) + wmax2(l2, l1) * 2.f * (vc - R) * inr;
+                                ls = fmaxf(l1, l2);
+                            } else {
+                                gv = 2.f * (V - R);
+                                ls = (R - V) * (R - V);
+                            }
+                            dO[r] = ok ? vscale * gv : 0.f;
+                            lsum += ok ? ls : 0.f;
+                        }
+                    } else {  // clipped surrogate; the log-prob of a sample is a row sum over its outputs
+                        const bool av_ = c < A;
+                        const float aiv = S.aiv[av_ ? c : 0], ls_c = av_ ? lstd[c] : 0.f;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int s = 4 * g + r;
+                            const bool ok = ts0 + s < ns;
+                            const float diff = av_ ? rt[s * RSL + O + c] - (ho[r] + bh) : 0.f;
+                            const float lpe = av_ ? -0.5f * diff * diff * aiv - ls_c - LOG_SQRT_2PI : 0.f;
+                            const float lp = row_sum16(lpe);
+                            const float ratio = expf(lp - rt[s * RSL + O + A]);
+                            const float ad = rt[s * RSL + O + A + 1];
+                            const float s1 = ratio * ad;
+                            const float s2 = fminf(fmaxf(ratio, 1.f - clip), 1.f + clip) * ad;
+                            const float inr = (ratio >= 1.f - clip && ratio <= 1.f + clip) ? 1.f : 0.f;
+                            const float gr = ad * (wmin2(s1, s2) + wmin2(s2, s1) * inr);
+                            const float dlp = ok ? ascale * gr * ratio : 0.f;
+                            lsum += (ok && c == 0) ? -fminf(s1, s2) : 0.f;
+                            dO[r] = av_ ? dlp * diff * aiv : 0.f;
+                            gls += av_ ? dlp * (diff * diff * aiv - 1.f) : 0.f;
+                        }
+                    }
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        gbh += dO[r];
+                        if (c < DQ) dtile[(4 * g + r) * DQS + c] = dO[r];
+                    }
+                    PGM_STAMP(5);
+                    // ---- head-weight gradient gWh^T[u][q] += H2^T dO  (both operands in C registers)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+#pragma unroll
+                        for (int ub = 0; ub < 4; ++ub) gWh[ub] = mfma16(H2[ub][r], dO[r], gWh[ub]);
+                    wave_lds_fence();  // dO tile written; H2 tile reads (heads) done
+                    // ---- dH2 = dO . Wh  (A = dO through its transpose tile) -> dZ2
+#pragma unroll
+                    for (int ob = 0; ob < 4; ++ob) z[ob] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int ks = 0; ks < (Q + 3) / 4; ++ks) {
+                        const int q = 4 * ks + g;
+                        const float av = q < Q ? dtile[c * DQS + q] : 0.f;
+#pragma unroll
+                        for (int ob = 0; ob < 4; ++ob) z[ob] = mfma16(av, q < Q ? Wt.Wh[q < Q ? q : 0][ob * T16 + c] : 0.f, z[ob]);
+                    }
+                    f32x4 dZ2[4];
+#pragma unroll
+                    for (int ob = 0; ob < 4; ++ob)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            dZ2[ob][r] = z[ob][r] * (1.f - H2[ob][r] * H2[ob][r]);
+                            gB2[ob] += dZ2[ob][r];
+                        }
+                    PGM_STAMP(6);
+#pragma unroll
+                    for (int ob = 0; ob < 4; ++ob)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) scr[(4 * g + r) * S16 + ob * T16 + c] = dZ2[ob][r];
+                    wave_lds_fence();
+                    // ---- dH1 = dZ2 W2 (A = dZ2 through the transpose tile, B = W2t[in][o] column); its MFMAs go
+                    // into the pipe first, dW2 queues behind them
+#pragma unroll
+                    for (int ib = 0; ib < 4; ++ib) z[ib] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+                    for (int ks = 0; ks < H / 4; ++ks) {
+                        const int k = 4 * ks + g;  // output unit o
+                        const float av = scr[c * S16 + k];
+#pragma unroll
+                        for (int ib = 0; ib < 4; ++ib) z[ib] = mfma16(av, Wt.W2t[ib * T16 + c][k], z[ib]);
+                    }
+                    // ---- dW2^T[in][o] += H1^T dZ2 straight from the C registers
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+#pragma unroll
+                        for (int ib = 0; ib < 4; ++ib)
+#pragma unroll
+                            for (int ob = 0; ob < 4; ++ob) gW2[ib][ob] = mfma16(H1[ib][r], dZ2[ob][r], gW2[ib][ob]);
+                    f32x4 dZ1[4];
+#pragma unroll
+                    for (int ib = 0; ib < 4; ++ib)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            dZ1[ib][r] = z[ib][r] * (1.f - H1[ib][r] * H1[ib][r]);
+                            gB1[ib] += dZ1[ib][r];
+                        }
+                    // ---- dW1^T[k][h] += X^T dZ1  (A = X[sample 4g + r][feature 16 kb + c], B = dZ1 register r)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+                        for (int kb = 0; kb < K1B; ++kb) {
+                            const int k = kb * T16 + c;
+                            const float ax = k < O ? rt[(4 * g + r) * RSL + (k < O ? k : 0)] : 0.f;
+#pragma unroll
+                            for (int hb = 0; hb < 4; ++hb) gW1[kb][hb] = mfma16(ax, dZ1[hb][r], gW1[kb][hb]);
+                        }
+                    }
+                    wave_lds_fence();  // dH1 finished reading the dZ2 tile before the next tile's writes
+                    PGM_STAMP(7);
+                }  // tiles
+                if constexpr (NBUF == 2) {
+                    dma_sync_m();
+                } else {
+                    lds_sync_m();
+                    if (gp + 1 < npass) {
+                        issue_rows(0, (gp + 1) & 1);
+                        if (gp + 2 < npass) issue_idx(gp + 2, gp & 1);
+                        dma_sync_m();
+                    }
+                }
+                PGM_STAMP(1);
+            }  // passes
+
+            // ---- per-column sums over the four lane groups (column c of block i)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                gB1[i] = group4_sum(gB1[i]);
+                gB2[i] = group4_sum(gB2[i]);
+            }
+            gbh = group4_sum(gbh);
+            gls = group4_sum(gls);
+            lsum = wave_sum64(lsum);
+            float ent = 0.f;
+#pragma unroll
+            for (int q = 0; q < A; ++q) ent += 0.5f + LOG_SQRT_2PI + lstd[q];
+            if (l == 0) S.red[8 + w] = lsum;
+            PGM_STAMP(12);
+
+            // ---- the W waves' register partials -> ONE image, W rounds: in round j wave w owns slice
+            // (w + j) mod W (blocks b with b mod W == slice; round 0 stores, later rounds add), so every
+            // element is summed in a fixed wave order.  Blocks: 0-15 dW2, 16-16+4 K1B dW1, then dWh, then the
+            // vectors (b1, b2, head bias, logstd).
+            {
+                float* Gt = S.big.GA;
+                constexpr int BW1 = 16, BWH = 16 + 4 * K1B, BV = BWH + 4, NBLK = BV + 1;
+                for (int j = 0; j < W; ++j) {
+                    const int sl = (w + j) % W;
+                    const bool add = j > 0;
+                    auto put = [&](int idx, float v) { Gt[idx] = add ? Gt[idx] + v : v; };
+                    auto put4 = [&](auto idx, const f32x4& v) {
+                        if (add) {
+                            float tmp[4];
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) tmp[r] = Gt[idx(r)];
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) Gt[idx(r)] = tmp[r] + v[r];
+                        } else {
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) Gt[idx(r)] = v[r];
+                        }
+                    };
+#pragma unroll
+                    for (int ib = 0; ib < 4; ++ib)
+#pragma unroll
+                        for (int ob = 0; ob < 4; ++ob)
+                            if ((ib * 4 + ob) % W == sl)
+                                put4([&](int r) { return oW2 + (ib * T16 + 4 * g + r) * SCR + ob * T16 + c; }, gW2[ib][ob]);
+#pragma unroll
+                    for (int kb = 0; kb < K1B; ++kb)
+#pragma unroll
+                        for (int hb = 0; hb < 4; ++hb)
+                            if ((BW1 + kb * 4 + hb) % W == sl) {
+                                // rows k >= O are exactly zero (A operand 0): they land in distinct W2 padding
+                                // slots (column H of row k), which the vector block zeroes afterwards... so
+                                // write them only to the in-range rows
+                                const int kr = kb * T16 + 4 * g;
+                                if (kr + 3 < O) {
+                                    put4([&](int r) { return (kr + r) * H + hb * T16 + c; }, gW1[kb][hb]);
+                                } else {
+#pragma unroll
+                                    for (int r = 0; r < 4; ++r)
+                                        if (kr + r < O) put((kr + r) * H + hb * T16 + c, gW1[kb][hb][r]);
+                                }
+                            }
+#pragma unroll
+                    for (int ub = 0; ub < 4; ++ub)
+                        if ((BWH + ub) % W == sl && c < Q)
+                            put4([&](int r) { return oWh + c * H + ub * T16 + 4 * g + r; }, gWh[ub]);
+                    if (BV % W == sl && g == 0) {
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            put(oB1 + i * T16 + c, gB1[i]);
+                            put(oB2 + i * T16 + c, gB2[i]);
+                        }
+                        if (c < Q) put(oBh + c, c < NQ ? gbh : 0.f);
+                        if (c < A) {  // -entropy_coef * d(mean entropy)/d logstd enters once (ppo.py:98)
+                            const float ec = add ? 0.f : a.hp.entropy_coef;
+                            put(oLs + c, m == 1 ? gls - ec : 0.f);
+                        }
+                        if (!add) Gt[oW2 + c * SCR + H] = 0.f;  // W2 padding column (rows 0..15 here,
+                    }
+                    if (BV % W == sl && g != 0 && !add) Gt[oW2 + (g * T16 + c) * SCR + H] = 0.f;  // rows 16..63)
+                    (void)NBLK;
+                    lds_sync_m();
+                }
+            }
+            PGM_STAMP(13);
+
+            // ---- the NS row parts' images: publish this one (16-B sc1 stores, every wave drains, barrier,
+            // one lane stores the tagged flag {step, loss sum}); wait for the other parts' flags; sum the NS
+            // images in part order (identical in every part) into registers, squared norm fused in
+            constexpr int NV4 = IMG / 4, TAIL = IMG - 4 * NV4;
+            constexpr int NG4 = (NV4 + NT - 1) / NT;
+            f32x4 ag[NG4], am[NG4], av[NG4], ap[NG4];
+            float agt = 0.f, sq2 = 0.f;
+            float lsum_all = 0.f;
+            {
+                const unsigned tag = (unsigned)(nstep + 1);
+                const int par = nstep & 1;
+                auto slot_of = [&](int h) { return (((p * 2 + m) * NS + h) * 2 + par); };
+                const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(a.xb, 0, a.xbytes, 0x00020000);
+                constexpr int SC1 = 16;
+                const float* G0 = S.big.GA;
+                float lsum_wg = 0.f;
+#pragma unroll
+                for (int i = 0; i < W; ++i) lsum_wg += S.red[8 + i];
+                if constexpr (NS > 1) {
+                    const int off_mine = slot_of(hs) * a.xslot * 8;
+                    for (int i = t; i < NV4; i += NT) {
+                        const float4 v4 = *reinterpret_cast<const float4*>(&G0[4 * i]);
+                        const u32x4 v = {__float_as_uint(v4.x), __float_as_uint(v4.y), __float_as_uint(v4.z),
+                                         __float_as_uint(v4.w)};
+                        __builtin_amdgcn_raw_buffer_store_b128(v, xr, off_mine + 16 * i, 0, SC1);
+                    }
+                    if (t < TAIL)
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(G0[4 * NV4 + t]), xr,
+                                                              off_mine + 16 * NV4 + 4 * t, 0, SC1);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
+                    lds_sync_m();
+                    PGM_STAMP(10);
+                    if (t == 0) {
+                        unsigned long long* flag_mine = a.xb + (size_t)slot_of(hs) * a.xslot + a.xslot - 1;
+                        __hip_atomic_store(flag_mine, ((unsigned long long)tag << 32) | __float_as_uint(lsum_wg),
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        float lparts[NS];
+                        for (int h = 0; h < NS; ++h) {
+                            if (h == hs) {
+                                lparts[h] = lsum_wg;
+                                continue;
+                            }
+                            const unsigned long long* flag_h = a.xb + (size_t)slot_of(h) * a.xslot + a.xslot - 1;
+                            unsigned long long x = 0;
+                            for (unsigned spins = 0;; ++spins) {
+                                x = __hip_atomic_load(flag_h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                if ((unsigned)(x >> 32) == tag) break;
+                                if (spins > (1u << 26)) {  // a part never arrived: flag the launch as failed
+                                    __hip_atomic_store(a.ws + 2 * a.P, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                    x = 0;
+                                    break;
+                                }
+                                __builtin_amdgcn_s_sleep(1);
+                            }
+                            lparts[h] = __uint_as_float((unsigned)x);
+                        }
+                        float ls = 0.f;
+                        for (int h = 0; h < NS; ++h) ls += lparts[h];
+                        S.red[4] = ls;
+                    }
+                    lds_sync_m();
+                } else {
+                    if (t == 0) S.red[4] = lsum_wg;
+                    lds_sync_m();
+                }
+                lsum_all = S.red[4];
+#pragma unroll
+                for (int k = 0; k < NG4; ++k) {
+                    const int i = min(t + k * NT, NV4 - 1);
+                    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int h = 0; h < NS; ++h) {
+                        float4 v4;
+                        if (h == hs) {
+                            v4 = *reinterpret_cast<const float4*>(&G0[4 * i]);
+                        } else {
+                            const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(xr, slot_of(h) * a.xslot * 8 + 16 * i, 0, SC1);
+                            v4 = make_float4(__uint_as_float(u[0]), __uint_as_float(u[1]), __uint_as_float(u[2]),
+                                             __uint_as_float(u[3]));
+                        }
+                        if (h == 0) {
+                            acc = f32x4{v4.x, v4.y, v4.z, v4.w};
+                        } else {
+                            acc[0] += v4.x;
+                            acc[1] += v4.y;
+                            acc[2] += v4.z;
+                            acc[3] += v4.w;
+                        }
+                    }
+                    ag[k] = acc;
+                    if (t + k * NT < NV4)
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) sq2 = fmaf(acc[q], acc[q], sq2);
+                }
+                if (t < TAIL) {
+                    float acc = 0.f;
+#pragma unroll
+                    for (int h = 0; h < NS; ++h) {
+                        const float v = h == hs ? G0[4 * NV4 + t]
+                                                : __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                                                      xr, slot_of(h) * a.xslot * 8 + 16 * NV4 + 4 * t, 0, SC1));
+                        acc = h == 0 ? v : acc + v;
+                    }
+                    agt = acc;
+                    sq2 = fmaf(agt, agt, sq2);
+                }
+#pragma unroll
+                for (int k = 0; k < NG4; ++k) {
+                    const int i = min(t + k * NT, NV4 - 1);
+                    const float4 m4 = *reinterpret_cast<const float4*>(&S.MV[4 * i]);
+                    const float4 v4 = *reinterpret_cast<const float4*>(&S.MV[IMG + 4 * i]);
+                    const float4 p4 = *reinterpret_cast<const float4*>(&Pf[4 * i]);
+                    am[k] = f32x4{m4.x, m4.y, m4.z, m4.w};
+                    av[k] = f32x4{v4.x, v4.y, v4.z, v4.w};
+                    ap[k] = f32x4{p4.x, p4.y, p4.z, p4.w};
+                }
+            }
+            PGM_STAMP(11);
+            // ---- clip_grad_norm_: this tower's squared norm (waves summed in order), exchanged with the other
+            // tower's workgroup of the same row part as one tagged 8-byte granule
+            float sq = wave_sum64(sq2);
+            if (l == 0) S.red[w] = sq;
+            lds_sync_m();
+            float total = 0.f;
+#pragma unroll
+            for (int i = 0; i < W; ++i) total += S.red[i];
+            PGM_STAMP(8);
+            if (t == 0) {
+                const unsigned tag = (unsigned)(nstep + 1);
+                unsigned long long* gr = a.ws + ppo_norm_granule(a.P, p, 0, hs);
+                __hip_atomic_store(gr + m, ((unsigned long long)tag << 32) | __float_as_uint(total), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                unsigned long long x = 0;
+                const bool failed = __hip_atomic_load(a.ws + 2 * a.P, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                for (unsigned spins = 0; !failed; ++spins) {
+                    x = __hip_atomic_load(gr + (1 - m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if ((unsigned)(x >> 32) == tag) break;
+                    if (spins > (1u << 26)) {
+                        __hip_atomic_store(a.ws + 2 * a.P, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        x = 0;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                const float other = __uint_as_float((unsigned)x);
+                S.red[5] = m == 0 ? total + other : other + total;  // critic + actor in every workgroup
+            }
+            lds_sync_m();
+            total = S.red[5];
+            PGM_STAMP(9);
+            const float coef = fminf(a.hp.max_grad_norm / (sqrtf(total) + 1e-6f), 1.f);
+            if (t == 0) {
+                if (m == 0) st_v += 0.5f * lsum_all / (float)(mb * K);
+                else st_a += lsum_all / (float)mb;
+                st_e += ent;
+            }
+            // ---- Adam from registers (padding: g = m = v = 0 keeps p = 0)
+            ++nstep;
+            b1p *= (double)b1c;
+            b2p *= (double)b2c;
+            const double bc1 = 1.0 - b1p;
+            const double bc2 = 1.0 - b2p;
+            const float step_size = (float)(lr / bc1);
+            const float inv_bc2s = 1.f / (float)sqrt(bc2);
+            auto adam1 = [&](float gg, float& mm, float& vv, float& pp) {
+                const float gc = gg * coef;
+                mm = mm + (1.f - b1c) * (gc - mm);
+                vv = vv * b2c + (1.f - b2c) * (gc * gc);
+                const float den = __builtin_amdgcn_sqrtf(vv) * inv_bc2s + eps;
+                pp -= step_size * mm * __builtin_amdgcn_rcpf(den);
+            };
+#pragma unroll
+            for (int k = 0; k < NG4; ++k) {
+                const int i = t + k * NT;
+                if (i >= NV4) break;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    float mm = am[k][q], vv = av[k][q], pp = ap[k][q];
+                    adam1(ag[k][q], mm, vv, pp);
+                    am[k][q] = mm;
+                    av[k][q] = vv;
+                    ap[k][q] = pp;
+                    if (m == 1 && 4 * i + q >= oLs && 4 * i + q < oLs + A) S.aiv[4 * i + q - oLs] = expf(-2.f * pp);
+                }
+                *reinterpret_cast<float4*>(&S.MV[4 * i]) = make_float4(am[k][0], am[k][1], am[k][2], am[k][3]);
+                *reinterpret_cast<float4*>(&S.MV[IMG + 4 * i]) = make_float4(av[k][0], av[k][1], av[k][2], av[k][3]);
+                *reinterpret_cast<float4*>(&Pf[4 * i]) = make_float4(ap[k][0], ap[k][1], ap[k][2], ap[k][3]);
+            }
+            if (t < TAIL) {
+                const int i = 4 * NV4 + t;
+                float mm = S.MV[i], vv = S.MV[IMG + i], pp = Pf[i];
+                adam1(agt, mm, vv, pp);
+                S.MV[i] = mm;
+                S.MV[IMG + i] = vv;
+                Pf[i] = pp;
+                if (m == 1 && i >= oLs && i < oLs + A) S.aiv[i - oLs] = expf(-2.f * pp);
+            }
+            lds_sync_m();  // parameters updated before the next minibatch; GA region reused as scr
+            PGM_STAMP(3);
+        }  // minibatches
+    }      // epochs
+    PGM_STAMP_FLUSH;
+    if (hs != 0) return;  // the NS parts hold identical copies
+    for (int i = t; i < IMG; i += NT) {
+        const int f = img_to_flat<O, A, K>(i, m, L);
+        if (f < 0) continue;
+        P[f] = Pf[i];
+        Mo[f] = S.MV[i];
+        Vo[f] = S.MV[IMG + i];
+    }
+    if (t == 0) {
+        const float n = (float)(E * M);
+        if (m == 0) a.stats[p * 3 + 0] = st_v / n;
+        if (m == 1) {
+            a.step[p] = step0 + nstep;
+            a.stats[p * 3 + 1] = st_a / n;
+            a.stats[p * 3 + 2] = st_e / n;
+        }
+    }
+}
+
+template <int O, int A, int K, int NS, int W>
+int launch_t16(const pgm_dims* d, const MArgs& a, hipStream_t stream) {
+    using Sm = T16Smem<O, A, K, W>;
+    const size_t smem = sizeof(Sm);
+    if (smem > 160 * 1024) {
+        set_error("pgm_ppo_update: LDS image %zu bytes exceeds 160 KiB", smem);
+        return PGM_E_UNSUPPORTED;
+    }
+    static_assert(sizeof(Sm) > 80 * 1024, "residency argument (one workgroup per CU) needs > 80 KiB LDS");
+    auto kern = ppo_update_t16_kernel<O, A, K, NS, W>;
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update");
+    e = hipMemsetAsync(a.ws, 0, ppo_flag_bytes(d->P) + ppo_xbuf_bytes(d, NS), stream);
+    if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update (workspace reset)");
+    const int grid = 8 * NS * ((d->P + 3) / 4);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * W), smem, stream, a);
+    return launch_status("pgm_ppo_update");
+}
+
 static int device_cus() { return device_cu_count(); }
 
 template <int O, int A, int K, int MODE>
@@ -890,13 +1588,19 @@ int launch_ppo_update_mfma(const pgm_dims* d, const MArgs& a, const pgm_rollout_
     hipLaunchKernelGGL(pack, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, stream, pa);
     if (int rc = launch_status("pgm_ppo_update (pack rows)")) return rc;
     // every workgroup of a split launch must be resident at once: one per CU (LDS > 80 KiB, 512 registers
-    // per lane), so the grid must fit the CU count.  MODE 2 (4 CUs per task) while 16 * ceil(P / 4) <= CUs,
-    // MODE 1 (2 per task) while 2P <= CUs, else one workgroup per task.  PGM_UPDATE_SPLIT=0/1/2 caps it.
+    // per lane), so the grid must fit the CU count.  PGM_UPDATE_SPLIT selects: 4 = 16-row tiles on 4
+    // workgroups per tower (8 CUs per task, while 32 ceil(P / 4) <= CUs), 3 = 16-row tiles on 2 workgroups
+    // of 8 waves per tower, 2 = 32-row tiles on 2 workgroups per tower (4 CUs per task, while
+    // 16 ceil(P / 4) <= CUs), 1 = one workgroup per tower (2P <= CUs), 0 = one workgroup per task; each
+    // falls back to the next one down when its grid does not fit.
     static_assert(sizeof(MSmem<O, A, K, true>) > 80 * 1024, "split residency argument needs > 80 KiB LDS");
     const char* sel = getenv("PGM_UPDATE_SPLIT");
-    const int cap = sel && sel[0] >= '0' && sel[0] <= '2' ? sel[0] - '0' : 2;
+    const int cap = sel && sel[0] >= '0' && sel[0] <= '4' ? sel[0] - '0' : 2;
     const int cus = device_cus();
-    if (cap >= 2 && 16 * ((d->P + 3) / 4) <= cus) return launch_mode<O, A, K, 2>(d, a, stream);
+    const int groups = (d->P + 3) / 4;
+    if (cap >= 4 && 32 * groups <= cus) return launch_t16<O, A, K, 4, 4>(d, a, stream);
+    if (cap >= 3 && 16 * groups <= cus) return launch_t16<O, A, K, 2, 8>(d, a, stream);
+    if (cap >= 2 && 16 * groups <= cus) return launch_mode<O, A, K, 2>(d, a, stream);
     if (cap >= 1 && 2 * d->P <= cus) return launch_mode<O, A, K, 1>(d, a, stream);
     return launch_mode<O, A, K, 0>(d, a, stream);
 }

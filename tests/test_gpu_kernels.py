@@ -167,15 +167,17 @@ def _update_setup(env, P, T, N, E, M, seed):
     return args, spec, tb, pols, (obs, actions, logp, values, returns, adv), perms
 
 
-@pytest.mark.parametrize('kernel', ['mfma', 'mfma-tower', 'mfma-joint', 'valu'])
+@pytest.mark.parametrize('kernel', ['t16x4', 't16x2', 'mfma', 'mfma-tower', 'mfma-joint', 'valu'])
 @pytest.mark.parametrize('env,T,N,E,M', [('MO-Hopper-v2', 64, 4, 2, 4), ('MO-Walker2d-v2', 128, 4, 2, 2),
                                          ('MO-Hopper-v3', 50, 3, 1, 3), ('MO-Swimmer-v2', 64, 1, 1, 1),
                                          ('MO-Ant-v2', 160, 4, 1, 2), ('MO-Walker2d-v2', 2048, 4, 1, 32)])
 def test_ppo_update(gpu, env, T, N, E, M, kernel, monkeypatch):
-    # mfma: each tower on two workgroups, half the minibatch rows each (default at small P); mfma-tower: one
-    # workgroup per tower; mfma-joint: one workgroup per task
-    monkeypatch.setenv('PGM_UPDATE_KERNEL', kernel.split('-')[0])
-    monkeypatch.setenv('PGM_UPDATE_SPLIT', {'mfma': '2', 'mfma-tower': '1', 'mfma-joint': '0'}.get(kernel, '2'))
+    # t16x4 / t16x2: 16-row tiles, each tower on 4 workgroups of 4 waves / 2 workgroups of 8 waves; mfma: 32-row
+    # tiles, each tower on two workgroups, half the minibatch rows each; mfma-tower: one workgroup per tower;
+    # mfma-joint: one workgroup per task
+    monkeypatch.setenv('PGM_UPDATE_KERNEL', 'valu' if kernel == 'valu' else 'mfma')
+    monkeypatch.setenv('PGM_UPDATE_SPLIT', {'t16x4': '4', 't16x2': '3', 'mfma': '2', 'mfma-tower': '1',
+                                            'mfma-joint': '0'}.get(kernel, '2'))
     P, lr = 2, 3e-4
     args, spec, tb, pols, data, perms = _update_setup(env, P, T, N, E, M, seed=11)
     obs, actions, logp, values, returns, adv = data

@@ -9,18 +9,47 @@ Semantics follow the reference exactly (bit-exact EP membership and order):
   * OptGraph.insert                                                    -- morl/opt_graph.py:8-27
   * hypervolume w.r.t. the origin (maximisation), rounded to 4 dp      -- morl/hypervolume.py:41-74
   * sparsity                                                           -- morl/utils.py:87-100
-The dominance test is vectorised (one [n, n] comparison) instead of the reference's per-point loop.
+The dominance test is an O(n log n) sort-and-sweep for two objectives (exact: the same boolean predicate)
+and chunked [n, chunk] comparisons for more, instead of the reference's per-point O(n^2) loop.
 """
 import numpy as np
+
+
+def _dominated_2d(objs):
+    """Exact dominance flags of 2-D points in O(n log n): sorted by x descending (y descending inside equal x),
+    point i is dominated iff some point with a strictly larger x has y >= y_i, or some point with an equal x
+    has a strictly larger y (the same predicate as the pairwise >= all & > any test)."""
+    x, y = objs[:, 0], objs[:, 1]
+    order = np.lexsort((-y, -x))
+    xs, ys = x[order], y[order]
+    n = len(xs)
+    start = np.ones(n, dtype=bool)
+    start[1:] = xs[1:] != xs[:-1]
+    gstart = np.maximum.accumulate(np.where(start, np.arange(n), 0))  # first index of each point's x group
+    pm = np.maximum.accumulate(ys)
+    before = np.where(gstart > 0, pm[np.maximum(gstart - 1, 0)], -np.inf)  # max y over strictly larger x
+    dom_sorted = (before >= ys) | (ys[gstart] > ys)
+    dom = np.empty(n, dtype=bool)
+    dom[order] = dom_sorted
+    return dom
+
+
+def _dominated_nd(objs, chunk=512):
+    n = len(objs)
+    dom = np.zeros(n, dtype=bool)
+    for i0 in range(0, n, chunk):  # [n, chunk] comparisons at a time (bounded memory)
+        blk = objs[i0:i0 + chunk]
+        ge = (objs[:, None, :] >= blk[None, :, :]).all(-1)  # ge[j, i]: j >= i everywhere
+        gt = (objs[:, None, :] > blk[None, :, :]).any(-1)
+        dom[i0:i0 + chunk] = (ge & gt).any(0)
+    return dom
 
 
 def get_ep_indices(obj_batch_input):
     if len(obj_batch_input) == 0:
         return np.array([])
     objs = np.asarray(obj_batch_input, dtype=np.float64)
-    ge = (objs[:, None, :] >= objs[None, :, :]).all(-1)  # ge[j, i]: j >= i everywhere
-    gt = (objs[:, None, :] > objs[None, :, :]).any(-1)
-    dominated = (ge & gt).any(0)
+    dominated = _dominated_2d(objs) if objs.shape[1] == 2 and not np.isnan(objs).any() else _dominated_nd(objs)
     keep = (objs >= 0).all(1) & ~dominated
     order = np.argsort(objs.T[0])
     return [int(i) for i in order if keep[i]]

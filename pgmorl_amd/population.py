@@ -13,11 +13,19 @@ Semantics kept: candidate construction and order, duplicate-direction filters, t
 argmax of HV - alpha * sparsity with first-max tie breaking, virtual-EP updates, the global
 ``np.random`` draws of ``random_selection`` and of the 3-D candidate shuffle.
 
+Generation-boundary speed, results unchanged:
+  * the hyperbolic fits of all population members run over a spawn pool of CPU-only workers
+    (PGM_FIT_WORKERS, default min(15, CPUs - 1)), each the same least_squares call;
+  * 2-D greedy steps screen every candidate with one vectorised pass and re-score exactly (the
+    reference's own computation, strict > in index order) only those within a rounding bound of the
+    best, so the pick and its tie-breaking are the reference's;
+  * 3-D greedy steps score candidate chunks on the same pool (the reference forks one process per
+    candidate, population_3d.py:216-237).
+
 Deliberate differences (documented in DESIGN.md):
-  * The 3-D greedy step evaluates candidates in-process with vectorised numpy (update_ep,
-    prefix-area hypervolume) instead of one forked process per candidate
-    (population_3d.py:216-237); results are the same, the order of float summation inside the
-    hypervolume differs (it is rounded to 4 dp like hypervolume.py:74).
+  * The 3-D candidate evaluation uses vectorised numpy (update_ep, prefix-area hypervolume); the
+    order of float summation inside the hypervolume differs from InnerHyperVolume's (it is rounded
+    to 4 dp like hypervolume.py:74).
   * The 2-D neighbourhood search (population_2d.py:37-54) has no exit when fewer than four
     distinct weights are reachable and spins forever; here it stops once a larger threshold
     cannot add any node.  When no node is reachable at all (the reference raises inside
@@ -133,6 +141,127 @@ def predict_hyperbolic(args, opt_graph, optgraph_id, test_weights, bounded_searc
     return {'sample_index': optgraph_id, 'predictions': [original + deltas[i] for i in range(len(test_weights))]}
 
 
+def _predict_chunk(payload):
+    """Pool worker: predict_hyperbolic for a chunk of (node, test weights) jobs on a snapshot of the graph."""
+    args_d, graph, jobs, bounded = payload
+    import argparse
+    args = argparse.Namespace(**args_d)
+    og = _GraphView(*graph)
+    objs_arr = np.asarray(og.objs, dtype=np.float64)
+    return [predict_hyperbolic(args, og, node, tw, bounded_search=bounded, objs_arr=objs_arr) for node, tw in jobs]
+
+
+class _GraphView:
+    """The fields of an OptGraph that predict_hyperbolic reads (picklable snapshot for the fit workers)."""
+
+    def __init__(self, weights, objs, delta_objs, succ):
+        self.weights, self.objs, self.delta_objs, self.succ = weights, objs, delta_objs, succ
+
+
+_POOL = None
+
+
+def _fit_pool():
+    """Lazily started spawn pool for the hyperbolic fits (CPU-only workers: numpy / scipy, no GPU runtime).
+    Size: PGM_FIT_WORKERS, default min(15, usable CPUs - 1); 0 or 1 disables it."""
+    global _POOL
+    import os
+    n = int(os.environ.get('PGM_FIT_WORKERS', min(15, max(1, len(os.sched_getaffinity(0)) - 1))))
+    if n <= 1:
+        return None
+    if _POOL is None:
+        import multiprocessing as mp
+        import sys
+        import types
+        # workers start from a bare __main__ (not the caller's script, which may import torch and open the
+        # GPU) with no device visible: CPU-only processes
+        saved_main = sys.modules['__main__']
+        saved_env = {k: os.environ.get(k) for k in ('HIP_VISIBLE_DEVICES', 'ROCR_VISIBLE_DEVICES')}
+        sys.modules['__main__'] = types.ModuleType('__main__')
+        os.environ['HIP_VISIBLE_DEVICES'] = os.environ['ROCR_VISIBLE_DEVICES'] = ''
+        try:
+            _POOL = mp.get_context('spawn').Pool(n)
+        finally:
+            sys.modules['__main__'] = saved_main
+            for k, v in saved_env.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+    return _POOL
+
+
+def predict_all(args, opt_graph, jobs, bounded_search, min_parallel=16):
+    """predict_hyperbolic for every (node, test_weights) job, in order: in-process for few jobs, else chunked
+    over the fit pool (each chunk carries one snapshot of the graph)."""
+    pool = _fit_pool() if len(jobs) >= min_parallel else None
+    if pool is None:
+        objs_arr = np.asarray(opt_graph.objs, dtype=np.float64)
+        return [predict_hyperbolic(args, opt_graph, node, tw, bounded_search=bounded_search, objs_arr=objs_arr)
+                for node, tw in jobs]
+    graph = (list(opt_graph.weights), list(opt_graph.objs), list(opt_graph.delta_objs), [list(x) for x in opt_graph.succ])
+    args_d = {'obj_num': args.obj_num}
+    nch = min(len(jobs), 4 * pool._processes)
+    chunks = [jobs[i::nch] for i in range(nch)]  # strided chunks balance cheap and expensive fits
+    outs = pool.map(_predict_chunk, [(args_d, graph, ch, bounded_search) for ch in chunks])
+    res = [None] * len(jobs)
+    for i, out in enumerate(outs):
+        res[i::nch] = out
+    return res
+
+
+def _screen_2d(ep, preds, alpha):
+    """Vectorised HV - alpha * sparsity of (virtual EP + candidate) for every candidate (2 objectives), in a
+    float order of its own (screening only: see Population2d._best_candidate).  Returns (scores, magnitude
+    of the summed terms) for the rounding bound."""
+    C, n = len(preds), len(ep)
+    x0, x1 = preds[:, 0], preds[:, 1]
+    if n:
+        q0, q1 = ep[:, 0], ep[:, 1]
+        dom_by_x = (x0[:, None] >= q0[None]) & (x1[:, None] >= q1[None]) & \
+                   ((x0[:, None] > q0[None]) | (x1[:, None] > q1[None]))       # [C, n] EP point dropped
+        x_dom = ((q0[None] >= x0[:, None]) & (q1[None] >= x1[:, None]) &
+                 ((q0[None] > x0[:, None]) | (q1[None] > x1[:, None]))).any(1)  # candidate dropped
+    else:
+        dom_by_x = np.zeros((C, 0), dtype=bool)
+        x_dom = np.zeros(C, dtype=bool)
+    x_keep = ~x_dom & (x0 >= 0) & (x1 >= 0)
+    # merged sequence per candidate: EP points (already obj0-ascending) with the candidate at its slot
+    pos = np.searchsorted(ep[:, 0], x0, side='left') if n else np.zeros(C, dtype=int)
+    j = np.arange(n + 1)[None, :]
+    src = np.where(j < pos[:, None], j, j - 1)
+    is_x = j == pos[:, None]
+    src_c = np.clip(src, 0, max(n - 1, 0))
+    p0 = np.where(is_x, x0[:, None], ep[src_c, 0] if n else 0.0)
+    p1 = np.where(is_x, x1[:, None], ep[src_c, 1] if n else 0.0)
+    keep = np.where(is_x, x_keep[:, None], ~np.take_along_axis(np.pad(dom_by_x, ((0, 0), (0, 1))), src_c, 1)
+                    if n else False)
+    # staircase HV: (x_i - x_prev) * y_i over kept points, x_prev the previous kept x (ascending)
+    kx = np.where(keep, np.maximum(p0, 0.0), 0.0)
+    prev = np.concatenate([np.zeros((C, 1)), np.maximum.accumulate(kx, axis=1)[:, :-1]], 1)
+    terms = np.where(keep, (kx - prev) * np.maximum(p1, 0.0), 0.0)
+    hv = terms.sum(1)
+    # EP-order sparsity: squared steps between consecutive kept points
+    big = np.where(keep, p0, np.nan)
+    last0 = _ffill(big)
+    last1 = _ffill(np.where(keep, p1, np.nan))
+    d0 = p0 - np.concatenate([np.full((C, 1), np.nan), last0[:, :-1]], 1)
+    d1 = p1 - np.concatenate([np.full((C, 1), np.nan), last1[:, :-1]], 1)
+    step = np.where(keep & ~np.isnan(d0), d0 * d0 + d1 * d1, 0.0)
+    cnt = keep.sum(1)
+    sp = np.where(cnt >= 2, step.sum(1) / np.maximum(cnt - 1, 1), 0.0)
+    mag = np.abs(terms).sum(1) + alpha * np.abs(step).sum(1) / np.maximum(cnt - 1, 1)
+    return hv - alpha * sp, mag
+
+
+def _ffill(a):
+    """Forward-fill NaNs along axis 1."""
+    idx = np.where(~np.isnan(a), np.arange(a.shape[1])[None, :], 0)
+    np.maximum.accumulate(idx, axis=1, out=idx)
+    out = np.take_along_axis(a, idx, 1)
+    return out
+
+
 # --------------------------------------------------------------------------- virtual EP metrics
 
 
@@ -205,6 +334,19 @@ def _sparsity_ep_order(ep_objs):
     return float(np.sum(np.square(np.diff(ep_objs, axis=0)))) / (len(ep_objs) - 1)
 
 
+def _evaluate_3d(virtual_ep, pred):
+    """population_3d.py:216-237 per candidate: update_ep, then hypervolume and sparsity of the new front."""
+    e = update_ep(virtual_ep, pred)
+    if len(e) == 0:
+        return 0.0, 0.0
+    return hypervolume_nd(e), _sparsity_sorted(e)
+
+
+def _score_chunk_3d(payload):
+    virtual_ep, preds = payload
+    return np.array([_evaluate_3d(virtual_ep, x) for x in preds], dtype=np.float64).reshape(-1, 2)
+
+
 # --------------------------------------------------------------------------- populations
 
 
@@ -268,26 +410,26 @@ class _PopulationBase:
     # the greedy knapsack over predicted offspring (population_2d.py:262-304, population_3d.py:296-333)
     def prediction_guided_selection(self, args, iteration, ep, opt_graph, scalarization_template):
         candidates = []
-        objs_arr = np.asarray(opt_graph.objs, dtype=np.float64)
+        jobs = []
         for sample in self.sample_batch:
             test_weights = self._test_weights(args, opt_graph, sample.optgraph_id)
             if len(test_weights) > 0:
-                res = predict_hyperbolic(args, opt_graph, sample.optgraph_id, test_weights,
-                                         bounded_search=self.bounded_search, objs_arr=objs_arr)
-                for w, pred in zip(test_weights, res['predictions']):
-                    candidates.append({'sample': sample, 'weight': w, 'prediction': pred})
+                jobs.append((sample, test_weights))
+        # the hyperbolic fits of every population member: independent small least-squares problems, fanned
+        # out over a process pool when there are many (the reference forks per candidate in 3-D,
+        # population_3d.py:216-237); results are the same function's, in job order
+        preds = predict_all(args, opt_graph, [(s.optgraph_id, tw) for s, tw in jobs], self.bounded_search)
+        for (sample, test_weights), res in zip(jobs, preds):
+            for w, pred in zip(test_weights, res['predictions']):
+                candidates.append({'sample': sample, 'weight': w, 'prediction': pred})
 
         virtual_ep = np.array([np.asarray(s.objs, dtype=np.float64) for s in ep.sample_batch]).reshape(-1, args.obj_num)
         mask = np.ones(len(candidates), dtype=bool)
         predicted_offspring_objs, elite_batch, scalarization_batch = [], [], []
         alpha = args.sparsity
+        pred_arr = np.array([c['prediction'] for c in candidates], dtype=np.float64).reshape(-1, args.obj_num)
         for _ in range(args.num_tasks):
-            best_id, best = -1, -np.inf
-            for i in range(len(candidates)):
-                if mask[i]:
-                    hv, sp = self._evaluate(virtual_ep, candidates[i]['prediction'])
-                    if hv - alpha * sp > best:
-                        best, best_id = hv - alpha * sp, i
+            best_id = self._best_candidate(virtual_ep, pred_arr, mask, alpha)
             if best_id == -1:
                 print('Too few candidates')
                 break
@@ -300,6 +442,16 @@ class _PopulationBase:
             virtual_ep = self._virtual_insert(virtual_ep, c['prediction'])
             predicted_offspring_objs.append(np.array(c['prediction'], dtype=np.float64))
         return elite_batch, scalarization_batch, predicted_offspring_objs
+
+    def _best_candidate(self, virtual_ep, preds, mask, alpha):
+        """First index of the maximum of HV - alpha * sparsity over the unmasked candidates (strict > scan in
+        index order, population_2d.py:276-292), or -1."""
+        best_id, best = -1, -np.inf
+        for i in np.nonzero(mask)[0]:
+            hv, sp = self._evaluate(virtual_ep, preds[i])
+            if hv - alpha * sp > best:
+                best, best_id = hv - alpha * sp, int(i)
+        return best_id
 
 
 class Population2d(_PopulationBase):
@@ -350,6 +502,24 @@ class Population2d(_PopulationBase):
         new = np.vstack([virtual_ep, np.asarray(pred, dtype=np.float64)[None]])
         e = new[get_ep_indices(new)]
         return _hv_2d_staircase(e), _sparsity_ep_order(e)
+
+    def _best_candidate(self, virtual_ep, preds, mask, alpha):
+        """Same result as the exact scan, fast: every candidate's score is first computed vectorised (the new
+        front = virtual EP minus the points the candidate dominates, plus the candidate, in obj0 order) with a
+        different float summation order; only the candidates within a rounding bound of the best screened
+        score are then re-scored with the exact reference computation, scanned in index order with the strict
+        > of the reference.  A candidate outside the bound scores below the best exactly, so the pick and
+        its first-max tie-breaking are the reference's."""
+        idx = np.nonzero(mask)[0]
+        if len(idx) == 0:
+            return -1
+        score, mag = _screen_2d(virtual_ep, preds[idx], alpha)
+        if np.isnan(score).all():  # every score NaN: no strict > ever holds (population_2d.py:286)
+            return -1
+        top = np.nanmax(score)
+        tol = 1e-9 * (np.max(mag) + 1.0)
+        near = idx[score >= top - 2.0 * tol]
+        return _PopulationBase._best_candidate(self, virtual_ep, preds, np.isin(np.arange(len(preds)), near), alpha)
 
     def _virtual_insert(self, virtual_ep, pred):
         new = np.vstack([virtual_ep, np.asarray(pred, dtype=np.float64)[None]])
@@ -402,10 +572,28 @@ class Population3d(_PopulationBase):
         return out
 
     def _evaluate(self, virtual_ep, pred):
-        e = update_ep(virtual_ep, pred)
-        if len(e) == 0:
-            return 0.0, 0.0
-        return hypervolume_nd(e), _sparsity_sorted(e)
+        return _evaluate_3d(virtual_ep, pred)
+
+    def _best_candidate(self, virtual_ep, preds, mask, alpha):
+        """The exact per-candidate scores, computed over the fit pool in chunks when there are many (the
+        reference forks one process per candidate, population_3d.py:216-237); the strict > scan in index order
+        then runs here on the returned (identical) values."""
+        idx = np.nonzero(mask)[0]
+        pool = _fit_pool() if len(idx) >= 64 else None
+        if pool is None:
+            return _PopulationBase._best_candidate(self, virtual_ep, preds, mask, alpha)
+        nch = min(len(idx), 4 * pool._processes)
+        chunks = [idx[i::nch] for i in range(nch)]
+        outs = pool.map(_score_chunk_3d, [(virtual_ep, preds[ch]) for ch in chunks])
+        hv = np.empty(len(preds))
+        sp = np.empty(len(preds))
+        for ch, out in zip(chunks, outs):
+            hv[ch], sp[ch] = out[:, 0], out[:, 1]
+        best_id, best = -1, -np.inf
+        for i in idx:
+            if hv[i] - alpha * sp[i] > best:
+                best, best_id = hv[i] - alpha * sp[i], int(i)
+        return best_id
 
     def _virtual_insert(self, virtual_ep, pred):
         return update_ep(virtual_ep, pred)

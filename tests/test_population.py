@@ -207,3 +207,67 @@ def test_random_selection_uses_the_global_stream():
     assert [id(e) for e in e1] == [id(pop.sample_batch[i]) for i, _ in want]
     for sc, (_, w) in zip(s1, want):
         np.testing.assert_array_equal(sc.weights.numpy(), w)
+
+
+# ---------------------------------------------------------------- fast generation-boundary paths == exact ones
+
+
+def _exact_pick(pop, virtual_ep, preds, mask, alpha):
+    return population._PopulationBase._best_candidate(pop, virtual_ep, preds, mask, alpha)
+
+
+@pytest.mark.parametrize('seed', range(8))
+def test_screened_2d_pick_equals_exact_scan(seed):
+    """Population2d._best_candidate (vectorised screen + exact re-score of the near-best) picks exactly what
+    the reference's strict-> scan picks, including exact ties (duplicated candidates: first index wins),
+    candidates dominated by the EP, candidates with negative coordinates and candidates that dominate EP
+    points."""
+    rng = np.random.RandomState(seed)
+    pop = population.Population2d(_args(2))
+    K = 2
+    ep = rng.rand(rng.randint(0, 40), K) * 100
+    ep = ep[pareto.get_ep_indices(ep)] if len(ep) else ep.reshape(0, K)
+    preds = rng.rand(300, K) * 110 - 5
+    preds[::7] = preds[3]                                   # exact ties
+    if len(ep):
+        preds[5::11] = ep[rng.randint(len(ep), size=len(preds[5::11]))]  # duplicates of EP points
+    for alpha in (0.0, 1.0, 30.0):
+        mask = rng.rand(len(preds)) < 0.9
+        for _ in range(6):
+            a = pop._best_candidate(ep, preds, mask, alpha)
+            b = _exact_pick(pop, ep, preds, mask, alpha)
+            assert a == b
+            if a < 0:
+                break
+            mask[a] = False
+            ep = pop._virtual_insert(ep, preds[a])
+
+
+def test_pooled_fits_equal_sequential(monkeypatch):
+    og, offspring = _history(2, 5, gens=3)
+    args = _args(2)
+    pop = population.Population2d(args)
+    jobs = [(s.optgraph_id, pop._test_weights(args, og, s.optgraph_id)) for s in offspring]
+    jobs = [j for j in jobs if len(j[1])]
+    monkeypatch.setenv('PGM_FIT_WORKERS', '3')
+    pooled = population.predict_all(args, og, jobs, False, min_parallel=1)
+    seq = [population.predict_hyperbolic(args, og, n, tw) for n, tw in jobs]
+    for a, b in zip(pooled, seq):
+        assert a['sample_index'] == b['sample_index']
+        np.testing.assert_array_equal(np.array(a['predictions']), np.array(b['predictions']))
+
+
+def test_pooled_3d_pick_equals_exact_scan(monkeypatch):
+    monkeypatch.setenv('PGM_FIT_WORKERS', '3')
+    rng = np.random.RandomState(3)
+    pop = population.Population3d(_args(3, pbuffer_num=6))
+    ep = rng.rand(30, 3) * 50
+    ep = ep[pareto.get_ep_indices(ep)]
+    preds = rng.rand(200, 3) * 55
+    preds[::9] = preds[1]
+    mask = np.ones(len(preds), dtype=bool)
+    for _ in range(4):
+        a = pop._best_candidate(ep, preds, mask, 0.5)
+        assert a == _exact_pick(pop, ep, preds, mask, 0.5)
+        mask[a] = False
+        ep = pop._virtual_insert(ep, preds[a])

@@ -53,11 +53,13 @@ def initialize_warm_up_batch(args, runtime):
     return samples, scal
 
 
-def run(args, device='cuda', rng='device', log=print):
+def run(args, device='cuda', rng='device', log=print, runtime=None):
+    """The generation loop.  ``runtime`` (default: MOPGPopulation on ``device``) is the MOPG back end: any
+    object with MOPGPopulation's run / evaluate_samples / materialize / _batch(P).layout / device."""
     np.random.seed(args.seed)
     torch.manual_seed(args.seed)
     t_start = time.perf_counter()
-    runtime = MOPGPopulation(args, device=device, rng=rng)
+    runtime = MOPGPopulation(args, device=device, rng=rng) if runtime is None else runtime
     template = WeightedSumScalarization(num_objs=args.obj_num, weights=np.ones(args.obj_num) / args.obj_num)
     total_num_updates = int(args.num_env_steps) // args.num_steps // args.num_processes
     start_time = time.time()

@@ -55,6 +55,24 @@ def parse():
     return ap.parse_args()
 
 
+def update_kernel_name(obs_dim, P):
+    """The pgm_ppo_update variant the launcher selects (pgm_ppo_mfma.hip launch_ppo_update_mfma and
+    pgm_ppo_wide.hip): 16-row tiles on 8 CUs per task while 32 ceil(P/4) <= CUs, else MODE 2 (4 CUs per task)
+    while 16 ceil(P/4) <= CUs; PGM_UPDATE_SPLIT caps it."""
+    if obs_dim > 32:
+        return 'ppo_update_wide_kernel'
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    cap = os.environ.get('PGM_UPDATE_SPLIT', '4')[:1]
+    cap = int(cap) if cap.isdigit() and int(cap) <= 4 else 4
+    groups = (P + 3) // 4
+    if cap >= 4 and 32 * groups <= cus:
+        return 'ppo_update_t16_kernel (NS=4, W=4)'
+    if cap == 3 and 16 * groups <= cus:
+        return 'ppo_update_t16_kernel (NS=2, W=8)'
+    mode = 2 if cap >= 2 and 16 * groups <= cus else 1 if cap >= 1 and 2 * P <= cus else 0
+    return f'ppo_update_mfma_kernel (MODE {mode})'
+
+
 def mflops_per_row(O, A, K, H=64):
     """M_f = 2(O*H + H^2) + H*A + H*K multiply-adds per row forward."""
     return 2 * (O * H + H * H) + H * A + H * K
@@ -273,7 +291,7 @@ def main():
                                f'N={N}, T={T}, ppo_epoch={E}, num_mini_batch={M}, eval_num=1, perf-mode device RNG',
                    'env': args.env_name, 'tasks_per_gpu': P, 'global_tasks': G, 'num_processes': N,
                    'num_steps': T, 'ppo_epoch': E, 'num_mini_batch': M, 'parallelism': f'task-sharded x{world}'},
-        'roofline': {'bound': 'mfma', 'kernel': 'ppo_update_mfma_kernel' if spec['obs_dim'] <= 32 else 'ppo_update_wide_kernel', 'achieved': achieved,
+        'roofline': {'bound': 'mfma', 'kernel': update_kernel_name(spec['obs_dim'], P), 'achieved': achieved,
                      'peak': PEAK_FP32_TFLOPS, 'unit': 'TFLOP/s', 'frac': achieved / PEAK_FP32_TFLOPS,
                      'traffic': traffic, 'avg_launch_ms': upd_ms, 'flop_per_launch': upd_flop,
                      'algorithmic_bytes_per_launch': P * T * N * E * 4 * (spec['obs_dim'] + spec['act_dim'] +

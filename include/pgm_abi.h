@@ -174,11 +174,12 @@ int pgm_adv_normalize(const pgm_dims* d, const pgm_rollout_buf* rb, const double
  * incremented per step, lr [P].  stats [P][3] = mean (value_loss, action_loss, dist_entropy).
  * workspace: caller-owned device bytes (pgm_ppo_update_workspace_bytes), required (PGM_E_INVALID_ARG
  * when NULL), reset inside the call on `stream`.  The critic and actor towers of a task run on separate
- * CUs that exchange the squared gradient norm per minibatch step; each tower is further split over two
- * CUs (half the minibatch rows each, gradient images added through the workspace) while
- * 16 * ceil(P/4) <= CU count.  obs_dim <= 32: tower images LDS-resident (falls back to 2 CUs per task,
- * then 1, as P grows); obs_dim > 32 (Humanoid): layer 1 streamed from L2, needs 2P <= CU count
- * (PGM_E_UNSUPPORTED otherwise: shard the tasks over more GPUs).  PGM_UPDATE_SPLIT=0/1/2 caps the split.
+ * CUs that exchange the squared gradient norm per minibatch step; each tower is further split over four
+ * CUs (a quarter of the minibatch rows each, gradient images added through the workspace) while
+ * 32 * ceil(P/4) <= CU count, else over two CUs while 16 * ceil(P/4) <= CU count.  obs_dim <= 32: tower
+ * images LDS-resident (falls back to 2 CUs per task, then 1, as P grows); obs_dim > 32 (Humanoid): layer
+ * 1 streamed from L2, needs 2P <= CU count (PGM_E_UNSUPPORTED otherwise: shard the tasks over more
+ * GPUs).  PGM_UPDATE_SPLIT=0/1/2/3/4 caps the split (3 = an A/B-only variant, selected only explicitly).
  * After the call, the 8-byte word at index 2P of the workspace is nonzero iff an exchange timed out
  * (the workgroups were not co-resident); the results of such a call are invalid. */
 int pgm_ppo_update(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params, float* adam_m,

@@ -903,9 +903,10 @@ struct T16SmemT {
     float dout[W][T16][DQS];                // per-wave dL/d(head output), transposed for dH2
     float aiv[A];                           // actor 1 / std^2
     float red[32];
+    static constexpr int NIMG = W == 4 ? 2 : 1;  // W = 4: wave pairs (0,1) and (2,3) fill one image each
     union Big {
         float scr[W][T16][S16];             // transpose tiles during the passes
-        float GA[IMG];                      // the workgroup's gradient image after them
+        float GA[NIMG][IMG];                // the workgroup's gradient image(s) after them
     } big;
 };
 template <int O, int A, int K, int W>
@@ -1244,71 +1245,80 @@ __global__ __launch_bounds__(64 * W) void ppo_update_t16_kernel(MArgs a) {
             if (l == 0) S.red[8 + w] = lsum;
             PGM_STAMP(12);
 
-            // ---- the W waves' register partials -> ONE image, W rounds: in round j wave w owns slice
-            // (w + j) mod W (blocks b with b mod W == slice; round 0 stores, later rounds add), so every
-            // element is summed in a fixed wave order.  Blocks: 0-15 dW2, 16-16+4 K1B dW1, then dWh, then the
-            // vectors (b1, b2, head bias, logstd).
+            // ---- the W waves' register partials -> the workgroup's image.  W = 4: the wave pairs (0,1), (2,3) fill
+            // images A, B in two rounds (round 0: wave 2i+h stores its half h of the blocks, round 1: it adds its
+            // other half), and the publish sums A + B -- every element is (w0 + w1) + (w2 + w3).  Otherwise W
+            // rounds on one image: in round j wave w owns slice (w + j) mod W (fixed wave order per element).
+            // Blocks: 0-15 dW2, 16-16+4 K1B dW1, then dWh, then the vectors (b1, b2, head bias, logstd).  The slice
+            // is a compile-time parameter of the round body (a uniform branch picks it), so every (index, value)
+            // pair is a register and a round's reads all issue before its writes.
             {
-                float* Gt = S.big.GA;
-                constexpr int BW1 = 16, BWH = 16 + 4 * K1B, BV = BWH + 4, NBLK = BV + 1;
-                for (int j = 0; j < W; ++j) {
-                    const int sl = (w + j) % W;
-                    const bool add = j > 0;
-                    auto put = [&](int idx, float v) { Gt[idx] = add ? Gt[idx] + v : v; };
+                constexpr int BW1 = 16, BWH = 16 + 4 * K1B, BV = BWH + 4;
+                constexpr int NSL = Sm::NIMG == 2 ? 2 : W;  // slices = rounds
+                float* Gt = S.big.GA[Sm::NIMG == 2 ? (w >> 1) : 0];
+                auto round = [&](auto slc, bool add) {
+                    constexpr int SL = decltype(slc)::value;
+                    // one 4-register block at a time: its reads, then its writes (the previous block's writes
+                    // overlap this block's read latency)
                     auto put4 = [&](auto idx, const f32x4& v) {
                         if (add) {
                             float tmp[4];
 #pragma unroll
-                            for (int r = 0; r < 4; ++r) tmp[r] = Gt[idx(r)];
+                            for (int r = 0; r < 4; ++r) tmp[r] = idx(r) >= 0 ? Gt[idx(r)] : 0.f;
 #pragma unroll
-                            for (int r = 0; r < 4; ++r) Gt[idx(r)] = tmp[r] + v[r];
+                            for (int r = 0; r < 4; ++r)
+                                if (idx(r) >= 0) Gt[idx(r)] = tmp[r] + v[r];
                         } else {
 #pragma unroll
-                            for (int r = 0; r < 4; ++r) Gt[idx(r)] = v[r];
+                            for (int r = 0; r < 4; ++r)
+                                if (idx(r) >= 0) Gt[idx(r)] = v[r];
                         }
                     };
 #pragma unroll
                     for (int ib = 0; ib < 4; ++ib)
 #pragma unroll
                         for (int ob = 0; ob < 4; ++ob)
-                            if ((ib * 4 + ob) % W == sl)
+                            if ((ib * 4 + ob) % NSL == SL)
                                 put4([&](int r) { return oW2 + (ib * T16 + 4 * g + r) * SCR + ob * T16 + c; }, gW2[ib][ob]);
 #pragma unroll
                     for (int kb = 0; kb < K1B; ++kb)
 #pragma unroll
                         for (int hb = 0; hb < 4; ++hb)
-                            if ((BW1 + kb * 4 + hb) % W == sl) {
-                                // rows k >= O are exactly zero (A operand 0): they land in distinct W2 padding
-                                // slots (column H of row k), which the vector block zeroes afterwards... so
-                                // write them only to the in-range rows
-                                const int kr = kb * T16 + 4 * g;
-                                if (kr + 3 < O) {
-                                    put4([&](int r) { return (kr + r) * H + hb * T16 + c; }, gW1[kb][hb]);
-                                } else {
-#pragma unroll
-                                    for (int r = 0; r < 4; ++r)
-                                        if (kr + r < O) put((kr + r) * H + hb * T16 + c, gW1[kb][hb][r]);
-                                }
-                            }
+                            if ((BW1 + kb * 4 + hb) % NSL == SL)  // rows k >= O are exactly zero and not in the image
+                                put4([&](int r) { const int k = kb * T16 + 4 * g + r; return k < O ? k * H + hb * T16 + c : -1; },
+                                     gW1[kb][hb]);
 #pragma unroll
                     for (int ub = 0; ub < 4; ++ub)
-                        if ((BWH + ub) % W == sl && c < Q)
-                            put4([&](int r) { return oWh + c * H + ub * T16 + 4 * g + r; }, gWh[ub]);
-                    if (BV % W == sl && g == 0) {
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) {
-                            put(oB1 + i * T16 + c, gB1[i]);
-                            put(oB2 + i * T16 + c, gB2[i]);
-                        }
-                        if (c < Q) put(oBh + c, c < NQ ? gbh : 0.f);
-                        if (c < A) {  // -entropy_coef * d(mean entropy)/d logstd enters once (ppo.py:98)
-                            const float ec = add ? 0.f : a.hp.entropy_coef;
-                            put(oLs + c, m == 1 ? gls - ec : 0.f);
-                        }
-                        if (!add) Gt[oW2 + c * SCR + H] = 0.f;  // W2 padding column (rows 0..15 here,
+                        if ((BWH + ub) % NSL == SL)
+                            put4([&](int r) { return c < Q ? oWh + c * H + ub * T16 + 4 * g + r : -1; }, gWh[ub]);
+                    if constexpr (BV % NSL == SL) {  // vectors: lanes of group 0 (every group holds the sums)
+                        // -entropy_coef * d(mean entropy)/d logstd enters once (ppo.py:98)
+                        const float lsv = m == 1 ? gls - (add ? 0.f : a.hp.entropy_coef) : 0.f;
+                        put4([&](int r) { return g == 0 ? oB1 + r * T16 + c : -1; }, f32x4{gB1[0], gB1[1], gB1[2], gB1[3]});
+                        put4([&](int r) { return g == 0 ? oB2 + r * T16 + c : -1; }, f32x4{gB2[0], gB2[1], gB2[2], gB2[3]});
+                        put4([&](int r) { return g == 0 && r == 0 && c < Q ? oBh + c : g == 0 && r == 1 && c < A ? oLs + c : -1; },
+                             f32x4{c < NQ ? gbh : 0.f, lsv, 0.f, 0.f});
+                        if (!add) Gt[oW2 + (g * T16 + c) * SCR + H] = 0.f;  // W2 padding column, rows 0..63
                     }
-                    if (BV % W == sl && g != 0 && !add) Gt[oW2 + (g * T16 + c) * SCR + H] = 0.f;  // rows 16..63)
-                    (void)NBLK;
+                };
+                for (int j = 0; j < NSL; ++j) {
+                    const int sl = Sm::NIMG == 2 ? ((w & 1) ^ j) : (w + j) % W;
+                    const bool add = j > 0;
+                    if constexpr (NSL == 2) {
+                        if (sl == 0) round(ic<0>{}, add);
+                        else round(ic<1>{}, add);
+                    } else {
+                        switch (sl) {
+                            case 0: round(ic<0>{}, add); break;
+                            case 1: round(ic<1 % NSL>{}, add); break;
+                            case 2: round(ic<2 % NSL>{}, add); break;
+                            case 3: round(ic<3 % NSL>{}, add); break;
+                            case 4: round(ic<4 % NSL>{}, add); break;
+                            case 5: round(ic<5 % NSL>{}, add); break;
+                            case 6: round(ic<6 % NSL>{}, add); break;
+                            default: round(ic<7 % NSL>{}, add); break;
+                        }
+                    }
                     lds_sync_m();
                 }
             }
@@ -1328,21 +1338,31 @@ __global__ __launch_bounds__(64 * W) void ppo_update_t16_kernel(MArgs a) {
                 auto slot_of = [&](int h) { return (((p * 2 + m) * NS + h) * 2 + par); };
                 const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(a.xb, 0, a.xbytes, 0x00020000);
                 constexpr int SC1 = 16;
-                const float* G0 = S.big.GA;
+                float* G0 = S.big.GA[0];
                 float lsum_wg = 0.f;
 #pragma unroll
                 for (int i = 0; i < W; ++i) lsum_wg += S.red[8 + i];
                 if constexpr (NS > 1) {
                     const int off_mine = slot_of(hs) * a.xslot * 8;
                     for (int i = t; i < NV4; i += NT) {
-                        const float4 v4 = *reinterpret_cast<const float4*>(&G0[4 * i]);
+                        float4 v4 = *reinterpret_cast<const float4*>(&G0[4 * i]);
+                        if constexpr (Sm::NIMG == 2) {  // A + B, kept in A for this part's own gather
+                            const float4 b4 = *reinterpret_cast<const float4*>(&S.big.GA[1][4 * i]);
+                            v4 = make_float4(v4.x + b4.x, v4.y + b4.y, v4.z + b4.z, v4.w + b4.w);
+                            *reinterpret_cast<float4*>(&G0[4 * i]) = v4;
+                        }
                         const u32x4 v = {__float_as_uint(v4.x), __float_as_uint(v4.y), __float_as_uint(v4.z),
                                          __float_as_uint(v4.w)};
                         __builtin_amdgcn_raw_buffer_store_b128(v, xr, off_mine + 16 * i, 0, SC1);
                     }
-                    if (t < TAIL)
-                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(G0[4 * NV4 + t]), xr,
-                                                              off_mine + 16 * NV4 + 4 * t, 0, SC1);
+                    if (t < TAIL) {
+                        float v = G0[4 * NV4 + t];
+                        if constexpr (Sm::NIMG == 2) {
+                            v += S.big.GA[1][4 * NV4 + t];
+                            G0[4 * NV4 + t] = v;
+                        }
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), xr, off_mine + 16 * NV4 + 4 * t, 0, SC1);
+                    }
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
                     lds_sync_m();
                     PGM_STAMP(10);
@@ -1380,33 +1400,38 @@ __global__ __launch_bounds__(64 * W) void ppo_update_t16_kernel(MArgs a) {
                     lds_sync_m();
                 }
                 lsum_all = S.red[4];
+                // partner loads in flight KC groups at a time (registers), then the sums in part order
+                constexpr int KC = 2;
 #pragma unroll
-                for (int k = 0; k < NG4; ++k) {
-                    const int i = min(t + k * NT, NV4 - 1);
-                    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+                for (int k0 = 0; k0 < NG4; k0 += KC) {
+                    u32x4 pl[KC][NS];
 #pragma unroll
-                    for (int h = 0; h < NS; ++h) {
-                        float4 v4;
-                        if (h == hs) {
-                            v4 = *reinterpret_cast<const float4*>(&G0[4 * i]);
-                        } else {
-                            const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(xr, slot_of(h) * a.xslot * 8 + 16 * i, 0, SC1);
-                            v4 = make_float4(__uint_as_float(u[0]), __uint_as_float(u[1]), __uint_as_float(u[2]),
-                                             __uint_as_float(u[3]));
-                        }
-                        if (h == 0) {
-                            acc = f32x4{v4.x, v4.y, v4.z, v4.w};
-                        } else {
-                            acc[0] += v4.x;
-                            acc[1] += v4.y;
-                            acc[2] += v4.z;
-                            acc[3] += v4.w;
-                        }
+                    for (int kk = 0; kk < KC; ++kk) {
+                        const int i = min(t + (k0 + kk) * NT, NV4 - 1);
+#pragma unroll
+                        for (int h = 0; h < NS; ++h)
+                            if (k0 + kk < NG4 && h != hs)
+                                pl[kk][h] = __builtin_amdgcn_raw_buffer_load_b128(xr, slot_of(h) * a.xslot * 8 + 16 * i, 0, SC1);
                     }
-                    ag[k] = acc;
-                    if (t + k * NT < NV4)
 #pragma unroll
-                        for (int q = 0; q < 4; ++q) sq2 = fmaf(acc[q], acc[q], sq2);
+                    for (int kk = 0; kk < KC; ++kk) {
+                        const int k = k0 + kk;
+                        if (k >= NG4) break;
+                        const int i = min(t + k * NT, NV4 - 1);
+                        const float4 own = *reinterpret_cast<const float4*>(&G0[4 * i]);
+                        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                        for (int h = 0; h < NS; ++h) {
+                            const f32x4 v = h == hs ? f32x4{own.x, own.y, own.z, own.w}
+                                                    : f32x4{__uint_as_float(pl[kk][h][0]), __uint_as_float(pl[kk][h][1]),
+                                                            __uint_as_float(pl[kk][h][2]), __uint_as_float(pl[kk][h][3])};
+                            acc = h == 0 ? v : acc + v;
+                        }
+                        ag[k] = acc;
+                        if (t + k * NT < NV4)
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) sq2 = fmaf(acc[q], acc[q], sq2);
+                    }
                 }
                 if (t < TAIL) {
                     float acc = 0.f;
@@ -1588,18 +1613,19 @@ int launch_ppo_update_mfma(const pgm_dims* d, const MArgs& a, const pgm_rollout_
     hipLaunchKernelGGL(pack, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, stream, pa);
     if (int rc = launch_status("pgm_ppo_update (pack rows)")) return rc;
     // every workgroup of a split launch must be resident at once: one per CU (LDS > 80 KiB, 512 registers
-    // per lane), so the grid must fit the CU count.  PGM_UPDATE_SPLIT selects: 4 = 16-row tiles on 4
-    // workgroups per tower (8 CUs per task, while 32 ceil(P / 4) <= CUs), 3 = 16-row tiles on 2 workgroups
-    // of 8 waves per tower, 2 = 32-row tiles on 2 workgroups per tower (4 CUs per task, while
-    // 16 ceil(P / 4) <= CUs), 1 = one workgroup per tower (2P <= CUs), 0 = one workgroup per task; each
-    // falls back to the next one down when its grid does not fit.
+    // per lane), so the grid must fit the CU count.  PGM_UPDATE_SPLIT selects: 4 (default) = 16-row tiles
+    // on 4 workgroups per tower (8 CUs per task, while 32 ceil(P / 4) <= CUs; Walker P = 20: 6.4 ms vs
+    // MODE 2's 7.1 ms), 3 = 16-row tiles on 2 workgroups of 8 waves per tower (A/B only: it spills and is
+    // slower than MODE 2, so only an explicit 3 selects it), 2 = 32-row tiles on 2 workgroups per tower
+    // (4 CUs per task, while 16 ceil(P / 4) <= CUs), 1 = one workgroup per tower (2P <= CUs), 0 = one
+    // workgroup per task; each falls back to the next one down when its grid does not fit.
     static_assert(sizeof(MSmem<O, A, K, true>) > 80 * 1024, "split residency argument needs > 80 KiB LDS");
     const char* sel = getenv("PGM_UPDATE_SPLIT");
-    const int cap = sel && sel[0] >= '0' && sel[0] <= '4' ? sel[0] - '0' : 2;
+    const int cap = sel && sel[0] >= '0' && sel[0] <= '4' ? sel[0] - '0' : 4;
     const int cus = device_cus();
     const int groups = (d->P + 3) / 4;
     if (cap >= 4 && 32 * groups <= cus) return launch_t16<O, A, K, 4, 4>(d, a, stream);
-    if (cap >= 3 && 16 * groups <= cus) return launch_t16<O, A, K, 2, 8>(d, a, stream);
+    if (cap == 3 && 16 * groups <= cus) return launch_t16<O, A, K, 2, 8>(d, a, stream);
     if (cap >= 2 && 16 * groups <= cus) return launch_mode<O, A, K, 2>(d, a, stream);
     if (cap >= 1 && 2 * d->P <= cus) return launch_mode<O, A, K, 1>(d, a, stream);
     return launch_mode<O, A, K, 0>(d, a, stream);

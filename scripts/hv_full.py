@@ -6,7 +6,9 @@ prediction-guided selection, text dumps) from the same fp32-rounded reference-or
 the reference's RNG draws (torch.manual_seed(j) -> T x normal([N, A]), E x randperm(T N), morl/mopg.py:96);
 only the MOPG back end differs: MOPGPopulation on the GPU (rng='host') or OracleMOPG, which trains every
 task with the fp64 oracle MOPG_worker restatement in a process pool (one process per task, like
-morl/morl.py:84-88).  Each side picks its own elites from its own offspring, so the comparison is on the
+morl/morl.py:84-88).  Side 'oracle32' is the noise floor: the same fp64 oracle with each offspring's
+parameters and Adam moments rounded to fp32 at the generation boundary (the device's storage precision),
+compared against the plain oracle with --ref like the device side.  Each side picks its own elites from its own offspring, so the comparison is on the
 budget-level quantities (HV of the final EP vs the origin, EP size, train env-steps), as
 scripts/plot/ep_batch_visualize_2d.py:23-45 reports them.
 
@@ -115,8 +117,8 @@ def _env_params(ep):
 class OracleMOPG:
     """MOPGPopulation's interface over the fp64 oracle (CPU, one process per task)."""
 
-    def __init__(self, args, procs):
-        self.args, self.procs = args, procs
+    def __init__(self, args, procs, round32=False):
+        self.args, self.procs, self.round32 = args, procs, round32
         self.device = torch.device('cpu')
         spec = envspec.make_spec(args.env_name)
         self.spec, self._layout = spec, ParamLayout(spec['obs_dim'], spec['act_dim'], spec['obj_num'])
@@ -164,6 +166,8 @@ class OracleMOPG:
         for task_res in res:
             offs = []
             for objs, flat, m, v, step, ep in task_res:
+                if self.round32:  # the device's storage precision at the generation boundary (noise floor)
+                    flat, m, v = (x.astype(np.float32).astype(np.float64) for x in (flat, m, v))
                 snap = DeviceSnapshot(self._layout, torch.from_numpy(flat), torch.from_numpy(m), torch.from_numpy(v), step)
                 offs.append(Sample.from_snapshot(snap, _env_params(ep), objs))
             offspring.append(offs)
@@ -174,7 +178,7 @@ def run_side(side, env, seed, procs):
     from pgmorl_amd.morl import run
     with tempfile.TemporaryDirectory() as d:
         args = make_args(env, seed, d)
-        runtime = OracleMOPG(args, procs) if side == 'oracle' else None
+        runtime = OracleMOPG(args, procs, round32=side == 'oracle32') if side != 'device' else None
         t0 = time.time()
         ep = run(args, device='cuda' if side == 'device' else 'cpu', rng='host', log=lambda *m: None, runtime=runtime)
         dt = time.time() - t0
@@ -186,24 +190,24 @@ def run_side(side, env, seed, procs):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument('side', choices=['oracle', 'device'])
+    ap.add_argument('side', choices=['oracle', 'oracle32', 'device'])
     ap.add_argument('--env', default='MO-Hopper-v2', choices=sorted(CONFIGS))
     ap.add_argument('--seeds', type=int, nargs='+', default=[0])
     ap.add_argument('--procs', type=int, default=7)
     ap.add_argument('--ref', help='oracle JSON (device side)')
     ap.add_argument('--out', required=True)
     a = ap.parse_args()
-    if a.side == 'device':
+    if a.ref:
         ref = json.load(open(a.ref))
         env, seeds = ref['env'], [r['seed'] for r in ref['runs']]
     else:
         env, seeds = a.env, a.seeds
     runs = [run_side(a.side, env, s, a.procs) for s in seeds]
     out = {'side': a.side, 'env': env, 'config': CONFIGS[env], 'runs': runs}
-    if a.side == 'device':
+    if a.ref:
         cmp = []
         for r, o in zip(runs, ref['runs']):
-            cmp.append({'seed': r['seed'], 'hv_device': r['hv'], 'hv_oracle': o['hv'],
+            cmp.append({'seed': r['seed'], 'side': a.side, 'hv_device': r['hv'], 'hv_oracle': o['hv'],
                         'hv_rel_diff': (r['hv'] - o['hv']) / max(abs(o['hv']), 1e-12),
                         'ep_size_device': r['ep_size'], 'ep_size_oracle': o['ep_size'],
                         'env_steps_device': r['train_env_steps'], 'env_steps_oracle': o['train_env_steps'],

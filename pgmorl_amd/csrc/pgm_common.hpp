@@ -45,12 +45,15 @@ inline size_t ppo_xbuf_bytes(const pgm_dims* d, int ns = PGM_NS_MAX) {
     return d->O <= 32 ? (size_t)d->P * 2 * ns * 2 * ppo_xslot(d->O, d->A, d->K) * 8 : 0;
 }
 int wide_xslot_words(int O, int A, int K);  // pgm_ppo_wide.hip: small image + dW1 + flag granule, 8-B words
-// obs_dim > 32 (wide kernel): flags, exchange slots [P][2 towers][2 halves][2 parities], half 1's private
-// [P][3][L] parameter / moment copies
+inline size_t wide_xbuf_bytes(const pgm_dims* d) {
+    return (size_t)d->P * 2 * PGM_NS_MAX * 2 * wide_xslot_words(d->O, d->A, d->K) * 8;
+}
+// obs_dim > 32 (wide kernel): flags, exchange slots [P][2 towers][NS parts][2 parities], parts 1..NS-1's
+// private [P][NS-1][L] parameter copies (sized for PGM_NS_MAX parts)
 inline size_t ppo_workspace_bytes(const pgm_dims* d) {
     if (d->O > 32)
-        return ppo_flag_bytes(d->P) + (size_t)d->P * 8 * wide_xslot_words(d->O, d->A, d->K) * 8 +
-               (size_t)d->P * 3 * make_layout(d->O, d->A, d->K, d->H).total * sizeof(float);
+        return ppo_flag_bytes(d->P) + wide_xbuf_bytes(d) +
+               (size_t)d->P * (PGM_NS_MAX - 1) * make_layout(d->O, d->A, d->K, d->H).total * sizeof(float);
     return ppo_flag_bytes(d->P) + ppo_xbuf_bytes(d) +
            (size_t)d->P * d->T * d->N * ppo_row_stride(d->O, d->A, d->K) * sizeof(float);
 }

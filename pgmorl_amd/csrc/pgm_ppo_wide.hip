@@ -2,11 +2,12 @@
 // cores.  Same semantics as pgm_ppo_mfma.hip (a2c_ppo_acktr/algo/ppo.py:58-115, storage.py:118-154,
 // model.py:75-82, distributions.py:29-40; torch min/max/clamp tie rules), different data placement:
 //
-//   * each tower (critic / actor) on NS workgroups (NS = 2 while the grid fits the CUs): each takes 1/NS of
-//     every minibatch's rows, in passes of 128 rows (one 32-row MFMA tile per wave); the NS gradient images
-//     are added through a 16-B sc1 publish + tagged flag hand-off (cdna_hip_programming.md G16 R1), both
-//     halves add them in the same order, so their Adam steps stay bitwise identical; the two towers exchange
-//     the squared gradient norm through one tagged granule per step (the narrow kernel's MODE 2 protocol);
+//   * each tower (critic / actor) on NS workgroups (NS = 4 while 32 ceil(P/4) <= CUs, else 2 while
+//     16 ceil(P/4) <= CUs, else 1): each takes 1/NS of every minibatch's rows, in passes of 128 rows (one
+//     32-row MFMA tile per wave); the NS gradient images (small image + dW1) are added through a 16-B sc1
+//     publish + tagged flag hand-off (cdna_hip_programming.md G16 R1), every part sums them in part order
+//     0..NS-1, so the NS Adam steps stay bitwise identical; the two towers exchange the squared gradient
+//     norm through one tagged granule per (step, row part) (the narrow kernel's protocol);
 //   * layer 1 (O x 64 = 96 KB) does not fit LDS next to the rest: the forward streams W1 through L1 (the
 //     four waves read the same rows; the L1 is invalidated after each layer-1 Adam step) and the observation
 //     rows straight from the rollout buffer (float4 per lane), both three 4-k-step groups ahead of the MFMAs.  Layer-1 k-steps pair features (h*KH + ks) of the two lane halves: any
@@ -19,8 +20,10 @@
 //   * everything but layer 1 (W2, heads, biases, logstd) is an LDS "small image" with LDS-resident Adam
 //     moments, reduced / clipped / updated like the narrow kernel's tower images; the head-weight gradient
 //     is an MFMA with the per-sample head gradients transposed through LDS.
-// Half 1 of a tower updates a private copy of its task's parameters / moments (workspace), so neither half
-// ever reads layer-1 weights the other is rewriting; half 0 works on the caller's arrays.
+// Layer 1 (the bulk of the parameters) is sharded over the NS parts for the clip / Adam step: every part
+// sums, clips and updates only its slice of dW1 and hands the new weights to the others, which write them
+// into their own parameter copy (parts 1..NS-1 keep private parameter rows in the workspace, so no part
+// reads layer-1 weights another is rewriting; part 0 works on the caller's row).
 #include <stdlib.h>
 
 #include "pgm_dispatch.hpp"
@@ -95,14 +98,14 @@ struct WArgs {
     Layout L;
     pgm_ppo_hparams hp;
     float *params, *m, *v;  // caller's arrays (half 0)
-    float* copies;          // NS = 2: half 1's private [P][3][L] params | exp_avg | exp_avg_sq
+    float* copies;          // NS > 1: parts 1..NS-1's private parameter rows [P][NS-1][L]
     int32_t* step;
     const float* lr;
     const int32_t* perms;
     const float *obs, *actions, *logp, *adv, *values, *returns;
     float* stats;
     unsigned long long* ws;  // tagged norm granules + timeout flag (word 2P), zeroed before the launch
-    unsigned long long* xb;  // NS = 2: gradient exchange slots [P][2 towers][2 halves][2 parities][xslot]
+    unsigned long long* xb;  // NS > 1: gradient exchange slots [P][2 towers][NS parts][2 parities][xslot]
     int xslot;               // 8-byte words per exchange slot (image | dW1 | flag granule)
     int xbytes;
 };
@@ -114,7 +117,9 @@ int wide_xslot_words(int O, int A, int K) {
     const int Q = A > K ? A : K;
     const int img = H * (H + 1) + Q * H + 2 * H + Q + A;
     const int nkt = (O + 31) / 32;
-    return ((img + nkt * 32 * H + 2) / 2 + 31) / 32 * 32;  // floats -> 8-byte words, 256-B aligned slots
+    const int nkw = (nkt + 3) / 4;
+    // small image | dW1 image | new-W1 slice [2 nkw 16/NS][256 threads] (NS >= 2) | 2 flag granules
+    return ((img + nkt * 32 * H + nkw * 16 * 256 + 1) / 2 + 2 + 31) / 32 * 32;  // 8-byte words, 256-B aligned
 }
 
 namespace {
@@ -135,11 +140,13 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
     constexpr int NKW = (NKT + 3) / 4;      // tiles owned per wave: kt = w + 4j
     constexpr int oWh = H * SCR, oB1 = oWh + Q * H, oB2 = oB1 + H, oBh = oB2 + H, oLs = oBh + Q;
     const int t = threadIdx.x, w = t >> 6, l = t & 63, h = l >> 5, c = l & 31;
-    // block map (NS = 2): in each group of 16 blocks, block r holds half r >> 3 of tower r & 1 of task
-    // 4g + ((r & 7) >> 1): the two halves of a tower are blocks b and b + 8 (speed only)
+    // block map (NS > 1): in each group of 8 NS blocks, block r holds part r >> 3 of tower r & 1 of task
+    // 4g + ((r & 7) >> 1): the parts of a tower are blocks b, b + 8, ... (one XCD under round-robin
+    // dispatch: speed only)
     const int bx = (int)blockIdx.x;
-    const int p = NS == 2 ? 4 * (bx >> 4) + ((bx & 7) >> 1) : (bx >> 1);
-    const int hs = NS == 2 ? (bx >> 3) & 1 : 0;
+    const int r8 = bx % (8 * NS);
+    const int p = NS > 1 ? 4 * (bx / (8 * NS)) + ((r8 & 7) >> 1) : (bx >> 1);
+    const int hs = NS > 1 ? r8 >> 3 : 0;
     if (p >= a.P) return;
     const int m = bx & 1;
     const int NQ = m == 0 ? K : A;
@@ -150,9 +157,12 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
     const int npass = (mbs + 4 * TS - 1) / (4 * TS);
     const float clip = a.hp.clip_param;
     const Layout& L = a.L;
-    float* __restrict__ P = hs == 0 ? a.params + (size_t)p * L.total : a.copies + ((size_t)p * 3 + 0) * L.total;
-    float* __restrict__ Mo = hs == 0 ? a.m + (size_t)p * L.total : a.copies + ((size_t)p * 3 + 1) * L.total;
-    float* __restrict__ Vo = hs == 0 ? a.v + (size_t)p * L.total : a.copies + ((size_t)p * 3 + 2) * L.total;
+    // parameters: part 0 the caller's row, parts 1..NS-1 private copies; Adam moments: the caller's rows for
+    // every part (layer-1 elements are owned by one part each; the small image is written back by part 0 only)
+    float* __restrict__ P = hs == 0 ? a.params + (size_t)p * L.total
+                                    : a.copies + ((size_t)p * (NS - 1) + (hs - 1)) * L.total;
+    float* __restrict__ Mo = a.m + (size_t)p * L.total;
+    float* __restrict__ Vo = a.v + (size_t)p * L.total;
     const int offW1 = L.off[m ? PGM_P_ACTOR_W1 : PGM_P_CRITIC_W1];
     const float* obs = a.obs + (size_t)p * (T + 1) * N * O;
     const float* acts = a.actions + (size_t)p * B * A;
@@ -539,20 +549,57 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
             const float* G1 = S.big.GA[1];
             const float lsum_wg = (S.red[8] + S.red[9]) + (S.red[10] + S.red[11]);
             float lsum_task = lsum_wg;
-            if constexpr (NS == 2) {
-                // ---- add the other half's gradients (small image + this wave's dW1 registers): 16-B sc1 stores
-                // of G0 + G1 and 4-B sc1 stores of the dW1 registers, every wave drains, barrier, one lane stores
-                // the tagged flag granule {step, loss sum}; then one lane polls the partner's flag, barrier, sc1
-                // loads.  Both halves add half0 + half1 in that order (bitwise identical Adam steps).  Slots are
-                // double-buffered by step parity.
-                const unsigned tag = (unsigned)(nstep + 1);
-                const int par = nstep & 1;
-                const int slot_mine = ((p * 2 + m) * 2 + hs) * 2 + par;
-                const int slot_other = ((p * 2 + m) * 2 + (1 - hs)) * 2 + par;
-                const int off_mine = slot_mine * a.xslot * 8, off_other = slot_other * a.xslot * 8;
-                const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(a.xb, 0, a.xbytes, 0x00020000);
+            // Layer 1 is SHARDED over the NS row parts: part hs owns values r in [RS hs, RS hs + RS) of every
+            // 16-value dW1 register block of every lane (rows 8 (r >> 2) + (r & 3) + 4 h of the block's feature
+            // tile), sums only those over the parts, clips / Adam-updates only them (moments straight in the
+            // caller's arrays: the parts' elements are disjoint) and hands the new weights to the other parts.
+            constexpr int RS = 16 / NS;  // values per block this part owns
+            constexpr int NB = NKW * 2;  // dW1 register blocks per lane
+            const int rbase = RS * hs;
+            float gs[NB][RS];  // this part's slice of the task's summed dW1
+            const int kb = opaque(w * TS + 4 * h);           // lane's first layer-1 row (feature)
+            const int fb = opaque(offW1 + kb * H + c);       // ... its flat parameter index
+            auto krow = [&](int j, int r) { return 4 * j * TS + (r & 3) + 8 * (r >> 2); };  // row - kb of value r
+            const unsigned tag = (unsigned)(nstep + 1);
+            const int par = nstep & 1;
+            auto slot_of = [&](int hh) { return ((p * 2 + m) * NS + hh) * 2 + par; };
+            const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(a.xb, 0, a.xbytes, 0x00020000);
+            constexpr int DW = IMG * 4;                        // byte offset of the dW1 block inside a slot
+            constexpr int DS = DW + NKT * TS * H * 4;          // byte offset of the new-W1-slice block
+            auto spin = [&](const unsigned long long* fl, unsigned want) {  // one lane; bounded
+                unsigned long long x = 0;
+                for (unsigned spins = 0;; ++spins) {
+                    x = __hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if ((unsigned)(x >> 32) == want) break;
+                    if (spins > (1u << 26)) {  // a partner never arrived: flag the launch as failed
+                        __hip_atomic_store(a.ws + 2 * a.P, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        return 0ull;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                return x;
+            };
+            // this part's own partial of its slice (a select among NS candidates per value)
+#pragma unroll
+            for (int j = 0; j < NKW; ++j)
+#pragma unroll
+                for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+                    for (int ri = 0; ri < RS; ++ri) {
+                        float v = dW1[j][ib][ri];
+#pragma unroll
+                        for (int hh = 1; hh < NS; ++hh)
+                            if (hs == hh) v = dW1[j][ib][RS * hh + ri];
+                        gs[j * 2 + ib][ri] = v;
+                    }
+            if constexpr (NS > 1) {
+                // ---- the parts' gradients: 16-B sc1 stores of the small image G0 + G1 and 4-B sc1 stores of the
+                // dW1 registers, every wave drains, barrier, one lane stores the tagged flag granule {step, loss
+                // sum} and polls the other parts' flags, barrier, sc1 loads of the other parts' small images and
+                // of THIS part's dW1 slice.  Sums in part order 0..NS-1 (the small-image Adam steps of the parts
+                // stay bitwise identical).  Slots are double-buffered by step parity.
+                const int off_mine = slot_of(hs) * a.xslot * 8;
                 constexpr int NV4 = IMG / 4, TAIL = IMG - 4 * NV4;
-                constexpr int DW = IMG * 4;  // byte offset of the dW1 block inside a slot
                 for (int i = t; i < NV4; i += MT) {
                     u32x4 v;
 #pragma unroll
@@ -574,64 +621,81 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
 #pragma unroll
                     for (int ib = 0; ib < 2; ++ib)
 #pragma unroll
-                        for (int r = 0; r < 16; ++r) {
-                            const int cidx = (4 * j * TS + (r & 3) + 8 * (r >> 2)) * H + ib * TS;
+                        for (int r = 0; r < 16; ++r)
                             __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dW1[j][ib][r]), xr, dwb,
-                                                                  off_mine + DW + 4 * cidx, WSPLIT);
-                        }
+                                                                  off_mine + DW + 4 * (krow(j, r) * H + ib * TS), WSPLIT);
                 __builtin_amdgcn_sched_barrier(0);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 lds_sync_m();
                 if (t == 0) {
-                    unsigned long long* flag_mine = a.xb + (size_t)slot_mine * a.xslot + a.xslot - 1;
-                    const unsigned long long* flag_other = a.xb + (size_t)slot_other * a.xslot + a.xslot - 1;
+                    unsigned long long* flag_mine = a.xb + (size_t)slot_of(hs) * a.xslot + a.xslot - 1;
                     __hip_atomic_store(flag_mine, ((unsigned long long)tag << 32) | __float_as_uint(lsum_wg),
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    unsigned long long x = 0;
-                    for (unsigned spins = 0;; ++spins) {
-                        x = __hip_atomic_load(flag_other, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        if ((unsigned)(x >> 32) == tag) break;
-                        if (spins > (1u << 26)) {  // partner never arrived: flag the launch as failed
-                            __hip_atomic_store(a.ws + 2 * a.P, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                            x = 0;
-                            break;
-                        }
-                        __builtin_amdgcn_s_sleep(1);
+                    float ls = 0.f;
+                    for (int hh = 0; hh < NS; ++hh) {  // loss sums in part order
+                        const float v = hh == hs ? lsum_wg
+                                                 : __uint_as_float((unsigned)spin(a.xb + (size_t)slot_of(hh) * a.xslot + a.xslot - 1, tag));
+                        ls = hh == 0 ? v : ls + v;
                     }
-                    const float lo = __uint_as_float((unsigned)x);
-                    S.red[12] = hs == 0 ? lsum_wg + lo : lo + lsum_wg;
+                    S.red[12] = ls;
                 }
                 PGM_STAMP(8);
-                lds_sync_m();  // the polling lane matched: every wave may load the partner's gradients
+                lds_sync_m();  // the polling lane matched: every wave may load the other parts' gradients
+                {  // this part's dW1 slice from every other part: all loads in flight, then the part-order sums
+                    float ov[NS > 1 ? NS - 1 : 1][NB][RS];
+#pragma unroll
+                    for (int q = 0; q < NS - 1; ++q) {
+                        const int hh = q < hs ? q : q + 1;
+#pragma unroll
+                        for (int j = 0; j < NKW; ++j)
+#pragma unroll
+                            for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+                                for (int ri = 0; ri < RS; ++ri)
+                                    ov[q][j * 2 + ib][ri] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                                        xr, dwb, slot_of(hh) * a.xslot * 8 + DW + 4 * (krow(j, rbase + ri) * H + ib * TS),
+                                        WSPLIT));
+                    }
+#pragma unroll
+                    for (int b = 0; b < NB; ++b)
+#pragma unroll
+                        for (int ri = 0; ri < RS; ++ri) {
+                            float acc = 0.f;
+#pragma unroll
+                            for (int hh = 0; hh < NS; ++hh) {
+                                const float v = hh == hs ? gs[b][ri] : ov[hh < hs ? hh : hh - 1][b][ri];
+                                acc = hh == 0 ? v : acc + v;
+                            }
+                            gs[b][ri] = acc;
+                        }
+                }
                 for (int i = t; i < NV4; i += MT) {
-                    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(xr, off_other + 16 * i, 0, WSPLIT);
+                    u32x4 pv[NS];
+#pragma unroll
+                    for (int hh = 0; hh < NS; ++hh)
+                        if (hh != hs) pv[hh] = __builtin_amdgcn_raw_buffer_load_b128(xr, slot_of(hh) * a.xslot * 8 + 16 * i, 0, WSPLIT);
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
-                        const float ov = __uint_as_float(v[q]);
-                        G0[4 * i + q] = hs == 0 ? G0[4 * i + q] + ov : ov + G0[4 * i + q];
+                        float acc = 0.f;
+#pragma unroll
+                        for (int hh = 0; hh < NS; ++hh) {
+                            const float v = hh == hs ? G0[4 * i + q] : __uint_as_float(pv[hh][q]);
+                            acc = hh == 0 ? v : acc + v;
+                        }
+                        G0[4 * i + q] = acc;
                     }
                 }
                 if (t < TAIL) {
-                    const float ov = __uint_as_float(
-                        __builtin_amdgcn_raw_buffer_load_b32(xr, off_other + 16 * NV4 + 4 * t, 0, WSPLIT));
-                    G0[4 * NV4 + t] = hs == 0 ? G0[4 * NV4 + t] + ov : ov + G0[4 * NV4 + t];
-                }
-                const int dwo = opaque(4 * ((w * TS + 4 * h) * H + c));
+                    float acc = 0.f;
 #pragma unroll
-                for (int j = 0; j < NKW; ++j)
-#pragma unroll
-                    for (int ib = 0; ib < 2; ++ib) {
-                        float ov[16];
-#pragma unroll
-                        for (int r = 0; r < 16; ++r) {
-                            const int cidx = (4 * j * TS + (r & 3) + 8 * (r >> 2)) * H + ib * TS;
-                            ov[r] = __uint_as_float(
-                                __builtin_amdgcn_raw_buffer_load_b32(xr, dwo, off_other + DW + 4 * cidx, WSPLIT));
-                        }
-#pragma unroll
-                        for (int r = 0; r < 16; ++r) dW1[j][ib][r] = hs == 0 ? dW1[j][ib][r] + ov[r] : ov[r] + dW1[j][ib][r];
-                        __builtin_amdgcn_sched_barrier(0);  // one 16-load block in flight at a time
+                    for (int hh = 0; hh < NS; ++hh) {
+                        const float v = hh == hs ? G0[4 * NV4 + t]
+                                                 : __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                                                       xr, slot_of(hh) * a.xslot * 8 + 16 * NV4 + 4 * t, 0, WSPLIT));
+                        acc = hh == 0 ? v : acc + v;
                     }
+                    G0[4 * NV4 + t] = acc;
+                }
                 lds_sync_m();
                 lsum_task = S.red[12];
             } else {
@@ -639,38 +703,33 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
                 lds_sync_m();
             }
             PGM_STAMP(9);
-            // ---- clip_grad_norm_: small image + this wave's dW1 registers (rows k >= O hold zeros)
+            // ---- clip_grad_norm_: part 0 counts the small image, every part its dW1 slice (rows k >= O hold
+            // zeros); the 2 NS partial sums of the task meet through tagged granules, summed in (tower, part)
+            // order in every workgroup
             float sq = 0.f;
-            for (int i = t; i < IMG; i += MT) sq = fmaf(G0[i], G0[i], sq);
+            if (hs == 0)
+                for (int i = t; i < IMG; i += MT) sq = fmaf(G0[i], G0[i], sq);
 #pragma unroll
-            for (int j = 0; j < NKW; ++j)
+            for (int b = 0; b < NB; ++b)
 #pragma unroll
-                for (int ib = 0; ib < 2; ++ib)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) sq = fmaf(dW1[j][ib][r], dW1[j][ib][r], sq);
+                for (int ri = 0; ri < RS; ++ri) sq = fmaf(gs[b][ri], gs[b][ri], sq);
             sq = wave_sum64(sq);
             if (l == 0) S.red[w] = sq;
             lds_sync_m();
             float total = (S.red[0] + S.red[1]) + (S.red[2] + S.red[3]);
-            if (t == 0) {  // tagged 8-byte granule hand-off with the other tower's workgroup (same half)
-                const unsigned tag = (unsigned)(nstep + 1);
-                unsigned long long* ws = a.ws + (hs == 0 ? 2 * p : 2 * a.P + 1 + 2 * p);
-                __hip_atomic_store(ws + m, ((unsigned long long)tag << 32) | __float_as_uint(total), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-                unsigned long long x = 0;
+            if (t == 0) {
+                __hip_atomic_store(a.ws + ppo_norm_granule(a.P, p, m, hs), ((unsigned long long)tag << 32) | __float_as_uint(total),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const bool failed = __hip_atomic_load(a.ws + 2 * a.P, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                for (unsigned spins = 0; !failed; ++spins) {
-                    x = __hip_atomic_load(ws + (1 - m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if ((unsigned)(x >> 32) == tag) break;
-                    if (spins > (1u << 26)) {
-                        __hip_atomic_store(a.ws + 2 * a.P, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        x = 0;
-                        break;
+                float tot = 0.f;
+                for (int mm = 0; mm < 2; ++mm)
+                    for (int hh = 0; hh < NS; ++hh) {
+                        float v = total;
+                        if (mm != m || hh != hs)
+                            v = failed ? 0.f : __uint_as_float((unsigned)spin(a.ws + ppo_norm_granule(a.P, p, mm, hh), tag));
+                        tot = mm == 0 && hh == 0 ? v : tot + v;
                     }
-                    __builtin_amdgcn_s_sleep(1);
-                }
-                const float other = __uint_as_float((unsigned)x);
-                S.red[4] = m == 0 ? total + other : other + total;
+                S.red[4] = tot;
             }
             lds_sync_m();
             total = S.red[4];
@@ -681,7 +740,8 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
                 st_e += ent;
             }
             PGM_STAMP(10);
-            // ---- Adam: the small image in LDS, layer 1 from the owning wave's registers (moments in HBM)
+            // ---- Adam: layer 1 first (this part's slice; moments in HBM), its new weights handed to the other
+            // parts while the small image (LDS) updates, then the other parts' slices into this part's copy
             ++nstep;
             b1p *= (double)b1c;
             b2p *= (double)b2c;
@@ -694,6 +754,49 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
                 const float den = __builtin_amdgcn_sqrtf(vv) * inv_bc2s + eps;
                 pp -= step_size * mm * __builtin_amdgcn_rcpf(den);
             };
+            auto live = [&](int j, int r) { return w + 4 * j < NKT && kb + krow(j, r) < O; };
+            {
+                // loads of CB blocks in flight at a time (all of them at NS = 4)
+                constexpr int CB = RS >= 16 ? 1 : RS >= 8 ? 3 : NB;
+#pragma unroll
+                for (int b0 = 0; b0 < NB; b0 += CB) {
+                    float bm[CB][RS], bv[CB][RS], bp[CB][RS];
+#pragma unroll
+                    for (int bb = 0; bb < CB; ++bb)
+#pragma unroll
+                        for (int ri = 0; ri < RS; ++ri) {
+                            const int b = b0 + bb, j = b >> 1, ib = b & 1, r = rbase + ri;
+                            const int f = b < NB && live(j, r) ? fb + krow(j, r) * H + ib * TS : offW1;
+                            bm[bb][ri] = Mo[f];
+                            bv[bb][ri] = Vo[f];
+                            bp[bb][ri] = P[f];
+                        }
+#pragma unroll
+                    for (int bb = 0; bb < CB; ++bb)
+#pragma unroll
+                        for (int ri = 0; ri < RS; ++ri) {
+                            const int b = b0 + bb, j = b >> 1, ib = b & 1, r = rbase + ri;
+                            if (b >= NB) continue;
+                            adam(gs[b][ri], bm[bb][ri], bv[bb][ri], bp[bb][ri]);
+                            gs[b][ri] = bp[bb][ri];
+                            if (!live(j, r)) continue;
+                            const int f = fb + krow(j, r) * H + ib * TS;
+                            Mo[f] = bm[bb][ri];
+                            Vo[f] = bv[bb][ri];
+                            P[f] = bp[bb][ri];
+                        }
+                }
+            }
+            if constexpr (NS > 1) {  // publish the new slice (4-B sc1 stores, [value][thread]), drain, flag
+#pragma unroll
+                for (int b = 0; b < NB; ++b)
+#pragma unroll
+                    for (int ri = 0; ri < RS; ++ri)
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(gs[b][ri]), xr,
+                                                              slot_of(hs) * a.xslot * 8 + DS + 4 * ((b * RS + ri) * MT + t), 0,
+                                                              WSPLIT);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
             for (int i = t; i < IMG; i += MT) {
                 float mm = S.MV[i], vv = S.MV[IMG + i], pp = Pf[i];
                 adam(G0[i], mm, vv, pp);
@@ -702,41 +805,33 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
                 Pf[i] = pp;
                 if (m == 1 && i >= oLs && i < oLs + A) S.aiv[i - oLs] = expf(-2.f * pp);
             }
-            {
-                // layer 1 rows k = (w + 4j)*32 + rowof(r, h) of this lane (column ib*32 + c): lane base + constant;
-                // the moments / weights of block b + 1 are loaded while block b updates
-                const int kb = opaque(w * TS + 4 * h);
-                const int fb = opaque(offW1 + kb * H + c);
-                constexpr int NBK = NKW * 2;
-                float bm[2][16], bv[2][16], bp[2][16];
-                auto load_blk = [&](int bk, float (&mm)[16], float (&vv)[16], float (&pp)[16]) {
-                    const int j = bk >> 1, ib = bk & 1;
+            if constexpr (NS > 1) {
+                lds_sync_m();  // every wave's slice stores drained
+                if (t == 0) {
+                    __hip_atomic_store(a.xb + (size_t)slot_of(hs) * a.xslot + a.xslot - 2, (unsigned long long)tag << 32,
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    for (int hh = 0; hh < NS; ++hh)
+                        if (hh != hs) spin(a.xb + (size_t)slot_of(hh) * a.xslot + a.xslot - 2, tag);
+                }
+                lds_sync_m();
+                // the other parts' new slices -> this part's layer-1 copy
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const int kr = 4 * j * TS + (r & 3) + 8 * (r >> 2);  // k - kb
-                        const int f = w + 4 * j < NKT && kb + kr < O ? fb + kr * H + ib * TS : offW1;
-                        mm[r] = Mo[f];
-                        vv[r] = Vo[f];
-                        pp[r] = P[f];
-                    }
-                };
-                load_blk(0, bm[0], bv[0], bp[0]);
+                for (int q = 0; q < NS - 1; ++q) {
+                    const int hh = q < hs ? q : q + 1;
+                    float nv[NB][RS];
 #pragma unroll
-                for (int bk = 0; bk < NBK; ++bk) {
-                    const int j = bk >> 1, ib = bk & 1, cur = bk & 1;
-                    if (bk + 1 < NBK) load_blk(bk + 1, bm[cur ^ 1], bv[cur ^ 1], bp[cur ^ 1]);
-                    if (w + 4 * j < NKT) {
+                    for (int b = 0; b < NB; ++b)
 #pragma unroll
-                        for (int r = 0; r < 16; ++r) {
-                            const int kr = 4 * j * TS + (r & 3) + 8 * (r >> 2);
-                            if (kb + kr >= O) continue;
-                            const int f = fb + kr * H + ib * TS;
-                            adam(dW1[j][ib][r], bm[cur][r], bv[cur][r], bp[cur][r]);
-                            Mo[f] = bm[cur][r];
-                            Vo[f] = bv[cur][r];
-                            P[f] = bp[cur][r];
+                        for (int ri = 0; ri < RS; ++ri)
+                            nv[b][ri] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                                xr, slot_of(hh) * a.xslot * 8 + DS + 4 * ((b * RS + ri) * MT + t), 0, WSPLIT));
+#pragma unroll
+                    for (int b = 0; b < NB; ++b)
+#pragma unroll
+                        for (int ri = 0; ri < RS; ++ri) {
+                            const int j = b >> 1, ib = b & 1, r = RS * hh + ri;
+                            if (live(j, r)) P[fb + krow(j, r) * H + ib * TS] = nv[b][ri];
                         }
-                    }
                 }
             }
             // layer-1 stores land in L2, then this CU's L1 is invalidated: the next step's W1 stream (plain
@@ -748,7 +843,7 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
         }  // minibatches
     }      // epochs
     PGM_STAMP_FLUSH;
-    if (hs != 0) return;  // half 1 worked on copies
+    if (hs != 0) return;  // parts 1..NS-1 worked on copies
     // ---- write back the small image (layer 1 was updated in place)
     for (int i = t; i < IMG; i += MT) {
         const int f = simg_to_flat<A, K>(i, m, L);
@@ -777,11 +872,13 @@ int ppo_update_wide(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params,
         set_error("pgm_ppo_update: the wide update needs the workspace (pgm_ppo_update_workspace_bytes)");
         return PGM_E_INVALID_ARG;
     }
-    // NS = 2 (each tower on two CUs) while the 16-block groups fit the CU count; PGM_UPDATE_SPLIT=1 caps it
+    // NS = 4 (each tower on four CUs) while the 32-block groups fit the CU count, else NS = 2 while the
+    // 16-block groups do, else 1; PGM_UPDATE_SPLIT caps it (0/1: one workgroup per tower, 2: at most two)
     const char* sel = getenv("PGM_UPDATE_SPLIT");
-    const int cap = sel && sel[0] >= '0' && sel[0] <= '2' ? sel[0] - '0' : 2;
+    const int cap = sel && sel[0] >= '0' && sel[0] <= '4' ? sel[0] - '0' : 4;
     const int cus = device_cu_count();
-    const int ns = cap >= 2 && 16 * ((d->P + 3) / 4) <= cus ? 2 : 1;
+    const int groups = (d->P + 3) / 4;
+    const int ns = cap >= 4 && 32 * groups <= cus ? 4 : cap >= 2 && 16 * groups <= cus ? 2 : 1;
     if (ns == 1 && 2 * d->P > cus) {
         set_error("pgm_ppo_update: the wide update needs 2P <= CUs (P=%d); shard the tasks over more GPUs", d->P);
         return PGM_E_UNSUPPORTED;
@@ -790,21 +887,19 @@ int ppo_update_wide(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params,
     char* ws = (char*)workspace;
     const size_t flags = ppo_flag_bytes(d->P);
     const int xslot = wide_xslot_words(d->O, d->A, d->K);
-    const size_t xbytes = (size_t)d->P * 8 * xslot * 8;
-    float* copies = (float*)(ws + flags + xbytes);
+    const size_t xcap = wide_xbuf_bytes(d);  // sized for PGM_NS_MAX parts
+    const size_t xbytes = (size_t)d->P * 2 * ns * 2 * xslot * 8;
+    float* copies = (float*)(ws + flags + xcap);
     WArgs a{d->N, d->T, d->P, L, *hp, params, adam_m, adam_v, copies, adam_step, lr, perms,
             rb->obs, rb->actions, rb->logp, rb->adv, rb->values, rb->returns, stats, (unsigned long long*)ws,
             (unsigned long long*)(ws + flags), xslot, (int)xbytes};
-    hipError_t e = hipMemsetAsync(workspace, 0, flags + (ns == 2 ? xbytes : 0), stream);
+    hipError_t e = hipMemsetAsync(workspace, 0, flags + (ns > 1 ? xbytes : 0), stream);
     if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update (workspace reset)");
-    if (ns == 2) {  // half 1's private copies of every task's parameters / moments
-        const size_t row = (size_t)L.total * sizeof(float);
-        for (int k = 0; k < 3; ++k) {
-            const float* src = k == 0 ? params : k == 1 ? adam_m : adam_v;
-            e = hipMemcpy2DAsync(copies + (size_t)k * L.total, 3 * row, src, row, row, d->P, hipMemcpyDeviceToDevice,
-                                 stream);
-            if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update (half copies)");
-        }
+    const size_t row = (size_t)L.total * sizeof(float);
+    for (int hh = 1; hh < ns; ++hh) {  // parts 1..ns-1: private copies of every task's parameters
+        e = hipMemcpy2DAsync(copies + (size_t)(hh - 1) * L.total, (size_t)(ns - 1) * row, params, row, row, d->P,
+                             hipMemcpyDeviceToDevice, stream);
+        if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update (part copies)");
     }
     return dispatch_dims(d->O, d->A, d->K, "pgm_ppo_update", [&](auto o, auto aa, auto k) -> int {
         constexpr int O = decltype(o)::value, A = decltype(aa)::value, K = decltype(k)::value;
@@ -825,7 +920,8 @@ int ppo_update_wide(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params,
                 hipLaunchKernelGGL(kern, dim3(grid), dim3(MT), smem, stream, a);
                 return launch_status("pgm_ppo_update");
             };
-            if (ns == 2) return launch(ppo_update_wide_kernel<O, A, K, 2>, 16 * ((d->P + 3) / 4));
+            if (ns == 4) return launch(ppo_update_wide_kernel<O, A, K, 4>, 32 * groups);
+            if (ns == 2) return launch(ppo_update_wide_kernel<O, A, K, 2>, 16 * groups);
             return launch(ppo_update_wide_kernel<O, A, K, 1>, 2 * d->P);
         }
     });

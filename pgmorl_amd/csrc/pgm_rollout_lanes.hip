@@ -172,6 +172,9 @@ struct LaneSmem {
     alignas(16) float x[NN][opad<O>()];  // normalised fp32 obs row of env n (written / read by its wave)
     alignas(16) float h1[4][H];          // per-wave layer-1 exchange row
     double sr[2][NN][64];                // statistics rows, double-buffered by step parity
+    double sn[2][NN][64];                // pre-reset next state of env n (feature lanes), by step parity
+    double e2[2][NN];                    // |clip(a)|^2 of env n, by step parity
+    int dn[2][NN];                       // done of env n, by step parity
     alignas(16) float eps[2][NN][NCH * A];  // action noise of env n for NCH steps, double-buffered
 };
 
@@ -191,66 +194,37 @@ __device__ __forceinline__ double clipd_s(double x, double lo, double hi) {
     return r;
 }
 
+// Two wave roles per env slot (2 NW waves, NW = min(N, 4); two waves per SIMD):
+//  * CHAIN waves (w < NW) run the observation chain: policy -> Gaussian draw -> fp64 dynamics -> time
+//    limit / auto-reset -> ob_rms merge -> next normalised input, and store obs / actions / log-probs / masks;
+//  * OBJECTIVE waves (w >= NW, env slots of wave w - NW) run everything the chain does not need: the raw
+//    objectives (fp64 wave sums of V . s'), the discounted objective / ret accumulators, the obj_rms / ret_rms
+//    merges and the rewards, reading s', |a|^2 and done from parity-buffered LDS rows after each step's
+//    barrier.  They run one step behind (step t's objective side after barrier t, its accumulators merged
+//    after barrier t + 1), so they only fill the chain waves' stall slots on the shared SIMDs.
+// Both roles execute the same barriers (one per step plus one drain).
 template <int O, int A, int K, int NN>
-__global__ __launch_bounds__(256) void rollout_lane_kernel(RolloutArgs a) {
+__global__ __launch_bounds__(512) void rollout_lane_kernel(RolloutArgs a) {
     static_assert(lanes_fit<O, K>(), "lane roles need O + K + 1 <= 64");
-    constexpr int NE = (NN + 3) / 4;  // env slots per wave
+    constexpr int NW = NN < 4 ? NN : 4;  // waves per role
+    constexpr int NE = (NN + 3) / 4;     // env slots per wave
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     auto& S = *reinterpret_cast<LaneSmem<O, A, NN>*>(smem_raw);
     const int p = blockIdx.x, l = threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const bool chain = wv < NW;
+    const int w = chain ? wv : wv - NW;  // env slot base of this wave
     const int T = a.T;
     const NormCfg nc = norm_cfg(a.ns);
     const Layout& L = a.L;
-    const float* prm = a.params + (size_t)p * L.total;
     float* obs = a.rb.obs + (size_t)p * (T + 1) * NN * O;
-    float* act = a.rb.actions + (size_t)p * T * NN * A;
-    float* logp = a.rb.logp + (size_t)p * T * NN;
-    float* rew = a.rb.rewards + (size_t)p * T * NN * K;
     float* masks = a.rb.masks + (size_t)p * (T + 1) * NN;
     float* bad = a.rb.bad_masks + (size_t)p * (T + 1) * NN;
-    const int maxs = a.spec.max_episode_steps;
-    // per-task output ranges as buffer resources (branch-free masked stores)
-    const auto r_obs = out_rsrc(obs, (size_t)(T + 1) * NN * O * 4);
-    const auto r_act = out_rsrc(act, (size_t)T * NN * A * 4);
-    const auto r_logp = out_rsrc(logp, (size_t)T * NN * 4);
-    const auto r_rew = out_rsrc(rew, (size_t)T * NN * K * 4);
-    const auto r_msk = out_rsrc(masks, (size_t)(T + 1) * NN * 4);
-    const auto r_bad = out_rsrc(bad, (size_t)(T + 1) * NN * 4);
-
-    ActorLane<O, A> pol;
-    pol.load(prm, L, l);
-    EnvLane<O, A, K> env;
-    env.load(a.spec, l);
-
-    // ---- env state of this wave's envs (feature l), VecNormalize accumulators (wave-uniform)
     const bool fl = l < O;
     const int lo = fl ? l : 0;
-    double s_o[NE], s0_o[NE], sn_e[NE], e2_e[NE], objacc[NE][K], ret[NE], objraw[NE][K];
-    int elapsed[NE], dprev[NE], dcur[NE];  // done of step t - 1 (consumed after step t's barrier) and of step t
-#pragma unroll
-    for (int e = 0; e < NE; ++e) {
-        const int n = min(w + 4 * e, NN - 1);
-        s_o[e] = a.st.s[((size_t)p * NN + n) * O + lo];
-        s0_o[e] = a.st.s0[(size_t)n * O + lo];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            objacc[e][k] = a.st.obj_acc[((size_t)p * NN + n) * K + k];
-            objraw[e][k] = 0.0;
-        }
-        ret[e] = a.st.ret[p * NN + n];
-        elapsed[e] = a.st.elapsed[p * NN + n];
-        dprev[e] = dcur[e] = 0;
-        sn_e[e] = e2_e[e] = 0.0;
-    }
-    int obj_valid = a.st.obj_acc_valid[p];
 
     // ---- running statistics, one lane per statistic (role 0: ob feature l, 1: objective l - O, 2: ret),
-    // replicated in every wave.  The objective / ret statistics (roles 1, 2) run ONE STEP BEHIND the
-    // observation statistics: step t's objective sums, accumulators and reward are formed after step t's
-    // barrier, merged after step t + 1's (the row of step t + 1 carries them) and the reward of step t is
-    // emitted then -- so nothing but the observation chain (policy -> dynamics -> ob_rms -> next input) sits
-    // between two barriers.  A drain step after the loop merges the last step.
+    // replicated in every wave (the chain waves use role 0, the objective waves roles 1 and 2)
     const int role = l < O ? 0 : l < O + K ? 1 : l == O + K ? 2 : 3;
     const int ko = role == 1 ? l - O : 0;
     double mean = 0.0, var = 1.0, cnt = 1.0;
@@ -269,70 +243,6 @@ __global__ __launch_bounds__(256) void rollout_lane_kernel(RolloutArgs a) {
     }
     const bool upd = role == 0 ? nc.use_ob != 0 : role == 1 ? nc.use_obj != 0 : role == 2;
     double inv = 1.0;
-    const double clip_lo = role == 0 ? -nc.clipob : -nc.cliprew, clip_hi = role == 0 ? nc.clipob : nc.cliprew;
-    const bool scale_out = role == 0 ? nc.use_ob != 0 : nc.use_obj != 0;
-
-    // ---- slot 0: after_update() carry (storage.py:71-75) and the first policy input
-#pragma unroll
-    for (int e = 0; e < NE; ++e) {
-        const int n = w + 4 * e;
-        if (n >= NN) break;
-        if (fl) {
-            float v = obs[(size_t)(a.carry ? T : 0) * NN * O + n * O + l];
-            if (a.carry) obs[n * O + l] = v;
-            S.x[n][l] = v;
-        }
-        if (a.carry && l == 0) {
-            masks[n] = masks[(size_t)T * NN + n];
-            bad[n] = bad[(size_t)T * NN + n];
-        }
-    }
-    // action noise, staged per wave in LDS chunks of NCH steps: the next chunk is loaded into registers a
-    // whole chunk ahead and written to LDS at the chunk boundary, so its vmcnt wait (which also drains the
-    // wave's rollout-storage stores) is paid once per NCH steps.  NULL noise: the perf-mode counter stream.
-    constexpr int CA = NCH * A, CR = (CA + 63) / 64;
-    float nreg[NE][CR];
-    auto load_eps = [&](int c) {
-        size_t idx[NE][CR];
-#pragma unroll
-        for (int e = 0; e < NE; ++e) {
-            const int n = min(w + 4 * e, NN - 1);
-#pragma unroll
-            for (int r = 0; r < CR; ++r) {
-                const int i = min(64 * r + l, CA - 1);
-                const int st = min(c * NCH + i / A, T - 1), j = i % A;
-                idx[e][r] = ((size_t)st * NN + n) * A + j;
-            }
-        }
-        if (a.noise) {  // uniform branch: plain loads, consumed a chunk later
-#pragma unroll
-            for (int e = 0; e < NE; ++e)
-#pragma unroll
-                for (int r = 0; r < CR; ++r) nreg[e][r] = a.noise[idx[e][r]];
-        } else {
-#pragma unroll
-            for (int e = 0; e < NE; ++e)
-#pragma unroll
-                for (int r = 0; r < CR; ++r) nreg[e][r] = counter_normal(a.seed, idx[e][r]);
-        }
-    };
-    auto store_eps = [&](int cb) {
-#pragma unroll
-        for (int e = 0; e < NE; ++e) {
-            const int n = w + 4 * e;
-            if (n >= NN) break;
-#pragma unroll
-            for (int r = 0; r < CR; ++r)
-                if (64 * r + l < CA) S.eps[cb][n][64 * r + l] = nreg[e][r];
-        }
-    };
-    load_eps(0);
-    store_eps(0);
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): preamble loads retired where the compiler sees it
-    if (NCH < T) load_eps(1);
-    wave_lds_fence_r();
-    PGM_STAMP_DECL
-
     // statistics merge of this lane's role (counts from before the merge; numpy's mean / var divide by N,
     // exact for N a power of two)
     auto merge = [&](int buf, bool active) {
@@ -359,158 +269,295 @@ __global__ __launch_bounds__(256) void rollout_lane_kernel(RolloutArgs a) {
             inv = rsqrt_d(var + nc.eps);
         }
     };
-    // objective side of step t for env slot e (after step t's barrier): reset by done_{t-1}, raw objectives
-    // (wave sums), discounted accumulators (vec_normalize.py:32-45), kept for the next step's row
-    auto objective_side = [&](int e) {
-        if (dprev[e]) {
-#pragma unroll
-            for (int k = 0; k < K; ++k) objacc[e][k] = 0.0;
-            ret[e] = 0.0;
-        }
-        double ob[K];
-        env.objectives(sn_e[e], e2_e[e], ob);
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            objraw[e][k] = ob[k];
-            objacc[e][k] = obj_valid ? objacc[e][k] * nc.gamma + ob[k] : ob[k];
-        }
-        ret[e] = ret[e] * nc.gamma + 0.0;  // SynthMO's scalar reward is 0 (vec_normalize.py:32)
-    };
-    // reward of step ts (role-1 lanes, after the merge of its accumulators): clip(obj / sqrt(var + eps))
-    auto emit_reward = [&](int e, int n, int ts) {
-        double r = sel_lane_d(objraw[e], ko);
-        if (scale_out) r = clipd_s(r * inv, clip_lo, clip_hi);
-        store_lane(r_rew, role == 1 ? (uint32_t)((((size_t)ts * NN + n) * K + ko) * 4) : OOB_OFF, (float)r);
-    };
+    PGM_STAMP_DECL
 
-    for (int step = 0; step < T; ++step) {
-        const int buf = step & 1;
-        const int cs = step % NCH, cb = (step / NCH) & 1;
-        if (cs == 0 && step > 0) {  // chunk step / NCH (loaded a chunk ago) into LDS; load the next one
-            store_eps(cb);
-            if (step + NCH < T) load_eps(step / NCH + 1);
-            wave_lds_fence_r();
-        }
-        PGM_STAMP(0);
-#pragma unroll
-        for (int e = 0; e < NE; ++e) {
-            const int n = w + 4 * e;
-            if (n >= NN) break;
-            float ej[A];  // this step's noise, read before the forward so its LDS latency hides there
-#pragma unroll
-            for (int j = 0; j < A; ++j) ej[j] = S.eps[cb][n][cs * A + j];
-            float mu[A];
-            pol.forward(S.x[n], S.h1[w], l, mu);
-            PGM_STAMP(1);
-            // Gaussian draw (torch.normal(mean, std) = eps * std + mean), log-prob and clipped action, all
-            // wave-uniform; lanes 0..A-1 store the action row, lane 0 its log-prob
-            float lpt[A], avs[A];
-            double ac[A], sq[A];
+    if (chain) {
+        // =========================================================== chain waves
+        const float* prm = a.params + (size_t)p * L.total;
+        float* act = a.rb.actions + (size_t)p * T * NN * A;
+        float* logp = a.rb.logp + (size_t)p * T * NN;
+        const int maxs = a.spec.max_episode_steps;
+        const auto r_obs = out_rsrc(obs, (size_t)(T + 1) * NN * O * 4);
+        const auto r_act = out_rsrc(act, (size_t)T * NN * A * 4);
+        const auto r_logp = out_rsrc(logp, (size_t)T * NN * 4);
+        const auto r_msk = out_rsrc(masks, (size_t)(T + 1) * NN * 4);
+        const auto r_bad = out_rsrc(bad, (size_t)(T + 1) * NN * 4);
+        ActorLane<O, A> pol;
+        pol.load(prm, L, l);
+        // per-lane SynthMO constants of feature l (the dynamics; the objective constants live in the
+        // objective waves)
+        double U[A], dd, cc, alo[A], ahi[A];
+        {
+            const pgm_env_spec& g = a.spec;
 #pragma unroll
             for (int j = 0; j < A; ++j) {
-                const float av = fmaf(ej[j], pol.sd[j], mu[j]);
-                const float dz = (av - mu[j]) * pol.rsd[j];
-                lpt[j] = -0.5f * dz * dz - pol.ls[j] - LOG_SQRT_2PI;
-                avs[j] = av;
-                ac[j] = clipd_s((double)av, env.lo[j], env.hi[j]);
-                sq[j] = ac[j] * ac[j];
+                U[j] = fl ? g.U[lo * A + j] : 0.0;
+                alo[j] = g.act_lo[j];
+                ahi[j] = g.act_hi[j];
+                asm volatile("" : "+v"(alo[j]));  // wave-uniform constants in VGPRs (see ActorLane::load)
+                asm volatile("" : "+v"(ahi[j]));
             }
-            const float lp = tree_sum(lpt);
-            e2_e[e] = tree_sum(sq);
-            store_lane(r_act, l < A ? (uint32_t)(((size_t)step * NN + n) * A + l) * 4 : OOB_OFF, sel_lane(avs, l));
-            store_lane(r_logp, l == 0 ? (uint32_t)((size_t)step * NN + n) * 4 : OOB_OFF, lp);
-            PGM_STAMP(6);
-            // dynamics (fp64, lane = feature), time limit, auto-reset
-            sn_e[e] = env.next_state(s_o[e], ac);
-            PGM_STAMP(7);
-            const int el = elapsed[e] + 1;
-            const int dn = el >= maxs;
-            const int bf = dn && el == maxs;
-            elapsed[e] = dn ? 0 : el;
-            dcur[e] = dn;
-            s_o[e] = dn ? s0_o[e] : sn_e[e];
-            // statistics row: the observation now, the objective / ret accumulators of the previous step
-            const double rv = role == 0 ? s_o[e] : role == 1 ? sel_lane_d(objacc[e], ko) : role == 2 ? ret[e] : 0.0;
-            S.sr[buf][n][l] = rv;
-            // masks of step + 1 (lane 0: masks, lane 1: bad_masks)
-            const uint32_t moff = (uint32_t)((size_t)(step + 1) * NN + n) * 4;
-            store_lane(r_msk, l == 0 ? moff : OOB_OFF, dn ? 0.f : 1.f);
-            store_lane(r_bad, l == 0 ? moff : OOB_OFF, bf ? 0.f : 1.f);
-            if (e == 0) PGM_STAMP(2);
+            dd = fl ? g.d[lo] : 0.0;
+            cc = fl ? g.c[lo] : 0.0;
         }
-        lds_sync();
-        PGM_STAMP(3);
-        merge(buf, role == 0 || step > 0);
-        PGM_STAMP(4);
-        // ---- emit: normalised fp32 obs (next input); then the objective side, off the observation chain
+        double s_o[NE], s0_o[NE];
+        int elapsed[NE];
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+            const int n = min(w + 4 * e, NN - 1);
+            s_o[e] = a.st.s[((size_t)p * NN + n) * O + lo];
+            s0_o[e] = a.st.s0[(size_t)n * O + lo];
+            elapsed[e] = a.st.elapsed[p * NN + n];
+        }
+        const bool upd0 = role == 0 && nc.use_ob;
+
+        // ---- slot 0: after_update() carry (storage.py:71-75) and the first policy input
 #pragma unroll
         for (int e = 0; e < NE; ++e) {
             const int n = w + 4 * e;
             if (n >= NN) break;
-            {
+            if (fl) {
+                float v = obs[(size_t)(a.carry ? T : 0) * NN * O + n * O + l];
+                if (a.carry) obs[n * O + l] = v;
+                S.x[n][l] = v;
+            }
+            if (a.carry && l == 0) {
+                masks[n] = masks[(size_t)T * NN + n];
+                bad[n] = bad[(size_t)T * NN + n];
+            }
+        }
+        // action noise, staged per wave in LDS chunks of NCH steps: the next chunk is loaded into registers a
+        // whole chunk ahead and written to LDS at the chunk boundary, so its vmcnt wait (which also drains the
+        // wave's rollout-storage stores) is paid once per NCH steps.  NULL noise: the perf-mode counter stream.
+        constexpr int CA = NCH * A, CR = (CA + 63) / 64;
+        float nreg[NE][CR];
+        auto load_eps = [&](int c) {
+            size_t idx[NE][CR];
+#pragma unroll
+            for (int e = 0; e < NE; ++e) {
+                const int n = min(w + 4 * e, NN - 1);
+#pragma unroll
+                for (int r = 0; r < CR; ++r) {
+                    const int i = min(64 * r + l, CA - 1);
+                    const int st = min(c * NCH + i / A, T - 1), j = i % A;
+                    idx[e][r] = ((size_t)st * NN + n) * A + j;
+                }
+            }
+            if (a.noise) {  // uniform branch: plain loads, consumed a chunk later
+#pragma unroll
+                for (int e = 0; e < NE; ++e)
+#pragma unroll
+                    for (int r = 0; r < CR; ++r) nreg[e][r] = a.noise[idx[e][r]];
+            } else {
+#pragma unroll
+                for (int e = 0; e < NE; ++e)
+#pragma unroll
+                    for (int r = 0; r < CR; ++r) nreg[e][r] = counter_normal(a.seed, idx[e][r]);
+            }
+        };
+        auto store_eps = [&](int cb) {
+#pragma unroll
+            for (int e = 0; e < NE; ++e) {
+                const int n = w + 4 * e;
+                if (n >= NN) break;
+#pragma unroll
+                for (int r = 0; r < CR; ++r)
+                    if (64 * r + l < CA) S.eps[cb][n][64 * r + l] = nreg[e][r];
+            }
+        };
+        load_eps(0);
+        store_eps(0);
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): preamble loads retired where the compiler sees it
+        if (NCH < T) load_eps(1);
+        wave_lds_fence_r();
+
+        for (int step = 0; step < T; ++step) {
+            const int buf = step & 1;
+            const int cs = step % NCH, cb = (step / NCH) & 1;
+            if (cs == 0 && step > 0) {  // chunk step / NCH (loaded a chunk ago) into LDS; load the next one
+                store_eps(cb);
+                if (step + NCH < T) load_eps(step / NCH + 1);
+                wave_lds_fence_r();
+            }
+            PGM_STAMP(0);
+#pragma unroll
+            for (int e = 0; e < NE; ++e) {
+                const int n = w + 4 * e;
+                if (n >= NN) break;
+                float ej[A];  // this step's noise, read before the forward so its LDS latency hides there
+#pragma unroll
+                for (int j = 0; j < A; ++j) ej[j] = S.eps[cb][n][cs * A + j];
+                float mu[A];
+                pol.forward(S.x[n], S.h1[w], l, mu);
+                PGM_STAMP(1);
+                // Gaussian draw (torch.normal(mean, std) = eps * std + mean), log-prob and clipped action, all
+                // wave-uniform; lanes 0..A-1 store the action row, lane 0 its log-prob
+                float lpt[A], avs[A];
+                double ac[A], sq[A], pu[A];
+#pragma unroll
+                for (int j = 0; j < A; ++j) {
+                    const float av = fmaf(ej[j], pol.sd[j], mu[j]);
+                    const float dz = (av - mu[j]) * pol.rsd[j];
+                    lpt[j] = -0.5f * dz * dz - pol.ls[j] - LOG_SQRT_2PI;
+                    avs[j] = av;
+                    ac[j] = clipd_s((double)av, alo[j], ahi[j]);
+                    sq[j] = ac[j] * ac[j];
+                    pu[j] = U[j] * ac[j];
+                }
+                // dynamics (fp64, lane = feature): s' = tanh(d s + U clip(a) + c)
+                const double sn = tanh_d2(dd * s_o[e] + tree_sum(pu) + cc);
+                const float lp = tree_sum(lpt);
+                store_lane(r_act, l < A ? (uint32_t)(((size_t)step * NN + n) * A + l) * 4 : OOB_OFF, sel_lane(avs, l));
+                store_lane(r_logp, l == 0 ? (uint32_t)((size_t)step * NN + n) * 4 : OOB_OFF, lp);
+                PGM_STAMP(6);
+                // time limit, auto-reset; the objective side's inputs (s', |a|^2, done) to the parity rows
+                const int el = elapsed[e] + 1;
+                const int dn = el >= maxs;
+                const int bf = dn && el == maxs;
+                elapsed[e] = dn ? 0 : el;
+                s_o[e] = dn ? s0_o[e] : sn;
+                if (role == 0) S.sr[buf][n][l] = s_o[e];  // lanes O.. of the row belong to the objective waves
+                S.sn[buf][n][l] = sn;
+                if (l == 0) {
+                    S.e2[buf][n] = tree_sum(sq);
+                    S.dn[buf][n] = dn;
+                }
+                const uint32_t moff = (uint32_t)((size_t)(step + 1) * NN + n) * 4;
+                store_lane(r_msk, l == 0 ? moff : OOB_OFF, dn ? 0.f : 1.f);
+                store_lane(r_bad, l == 0 ? moff : OOB_OFF, bf ? 0.f : 1.f);
+                if (e == 0) PGM_STAMP(2);
+            }
+            lds_sync();
+            PGM_STAMP(3);
+            merge(buf, upd0);
+            PGM_STAMP(4);
+            // ---- normalised fp32 obs: the next input and the rollout buffer
+#pragma unroll
+            for (int e = 0; e < NE; ++e) {
+                const int n = w + 4 * e;
+                if (n >= NN) break;
                 double v = s_o[e];
                 if (nc.use_ob) v = clipd_s((v - mean) * inv, -nc.clipob, nc.clipob);
                 const float f = (float)v;  // VecPyTorch .float() (envs.py:192)
                 if (role == 0) S.x[n][l] = f;
                 store_lane(r_obs, role == 0 ? (uint32_t)(((size_t)(step + 1) * NN + n) * O + l) * 4 : OOB_OFF, f);
             }
-            if (step > 0) emit_reward(e, n, step - 1);
-            objective_side(e);  // resets by done_{t-1} first
-            dprev[e] = dcur[e];
+            wave_lds_fence_r();
+            PGM_STAMP(5);
         }
-        obj_valid = 1;
-        wave_lds_fence_r();
-        PGM_STAMP(5);
-    }
-
-    // ---- drain: merge the last step's objective / ret accumulators, its reward, the done reset
+        lds_sync();  // the objective waves' drain merge
+        // ---- env state and observation statistics back to HBM
 #pragma unroll
-    for (int e = 0; e < NE; ++e) {
-        const int n = w + 4 * e;
-        if (n >= NN) break;
-        const double rv = role == 1 ? sel_lane_d(objacc[e], ko) : role == 2 ? ret[e] : 0.0;
-        S.sr[T & 1][n][l] = rv;
-    }
-    lds_sync();
-    merge(T & 1, role == 1 || role == 2);
-#pragma unroll
-    for (int e = 0; e < NE; ++e) {
-        const int n = w + 4 * e;
-        if (n >= NN) break;
-        emit_reward(e, n, T - 1);
-        if (dprev[e]) {
-#pragma unroll
-            for (int k = 0; k < K; ++k) objacc[e][k] = 0.0;
-            ret[e] = 0.0;
+        for (int e = 0; e < NE; ++e) {
+            const int n = w + 4 * e;
+            if (n >= NN) break;
+            if (fl) a.st.s[((size_t)p * NN + n) * O + l] = s_o[e];
+            if (l == 0) a.st.elapsed[p * NN + n] = elapsed[e];
         }
-    }
-
-    // ---- env state and statistics back to HBM
-#pragma unroll
-    for (int e = 0; e < NE; ++e) {
-        const int n = w + 4 * e;
-        if (n >= NN) break;
-        if (fl) a.st.s[((size_t)p * NN + n) * O + l] = s_o[e];
-        if (l < K) a.st.obj_acc[((size_t)p * NN + n) * K + l] = sel_lane_d(objacc[e], l);
-        if (l == 0) {
-            a.st.ret[p * NN + n] = ret[e];
-            a.st.elapsed[p * NN + n] = elapsed[e];
-        }
-    }
-    if (w == 0) {
-        if (role == 0) {
+        if (w == 0 && role == 0) {
             a.ns.ob_mean[(size_t)p * O + l] = mean;
             a.ns.ob_var[(size_t)p * O + l] = var;
             if (l == 0) a.ns.ob_count[p] = cnt;
-        } else if (role == 1) {
-            a.ns.obj_mean[p * K + ko] = mean;
-            a.ns.obj_var[p * K + ko] = var;
-            if (ko == 0) a.ns.obj_count[p] = cnt;
-        } else if (role == 2) {
-            a.ns.ret_mean[p] = mean;
-            a.ns.ret_var[p] = var;
-            a.ns.ret_count[p] = cnt;
-            a.st.obj_acc_valid[p] = obj_valid;
+        }
+    } else {
+        // =========================================================== objective waves
+        float* rew = a.rb.rewards + (size_t)p * T * NN * K;
+        const auto r_rew = out_rsrc(rew, (size_t)T * NN * K * 4);
+        double V[K], ebase[K], ecoef[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            V[k] = fl ? a.spec.V[k * O + lo] : 0.0;
+            ebase[k] = a.spec.ebase[k];
+            ecoef[k] = a.spec.ecoef[k];
+            asm volatile("" : "+v"(ebase[k]));
+            asm volatile("" : "+v"(ecoef[k]));
+        }
+        double objacc[NE][K], ret[NE], objraw[NE][K];
+        int dprev[NE];
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+            const int n = min(w + 4 * e, NN - 1);
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                objacc[e][k] = a.st.obj_acc[((size_t)p * NN + n) * K + k];
+                objraw[e][k] = 0.0;
+            }
+            ret[e] = a.st.ret[p * NN + n];
+            dprev[e] = 0;
+        }
+        int obj_valid = a.st.obj_acc_valid[p];
+        const double clip_lo = -nc.cliprew, clip_hi = nc.cliprew;
+        const bool scale_out = nc.use_obj != 0;
+        // reward of step ts (role-1 lanes, after the merge of its accumulators): clip(obj / sqrt(var + eps))
+        auto emit_reward = [&](int e, int n, int ts) {
+            double r = sel_lane_d(objraw[e], ko);
+            if (scale_out) r = clipd_s(r * inv, clip_lo, clip_hi);
+            store_lane(r_rew, role == 1 ? (uint32_t)((((size_t)ts * NN + n) * K + ko) * 4) : OOB_OFF, (float)r);
+        };
+        // the statistics row lanes of roles 1 / 2 for the merge after barrier t + 1 (step t's accumulators);
+        // the first row (step 0's barrier) carries nothing for them (merge inactive at step 0)
+        for (int step = 0; step < T; ++step) {
+            const int buf = step & 1;
+            lds_sync();
+            merge(buf, (role == 1 || role == 2) && step > 0);
+#pragma unroll
+            for (int e = 0; e < NE; ++e) {
+                const int n = w + 4 * e;
+                if (n >= NN) break;
+                if (step > 0) emit_reward(e, n, step - 1);
+                // objective side of step t: reset by done_{t-1}, raw objectives (wave sums), discounted
+                // accumulators (vec_normalize.py:32-45), the row of step t + 1
+                if (dprev[e]) {
+#pragma unroll
+                    for (int k = 0; k < K; ++k) objacc[e][k] = 0.0;
+                    ret[e] = 0.0;
+                }
+                const double sn = S.sn[buf][n][l];
+                const double e2 = S.e2[buf][n];
+                dprev[e] = S.dn[buf][n];
+                double ob[K];
+#pragma unroll
+                for (int k = 0; k < K; ++k) ob[k] = V[k] * sn;
+                wave_sum64_d_multi<K>(ob, ob);
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    ob[k] += ebase[k] - ecoef[k] * e2;
+                    objraw[e][k] = ob[k];
+                    objacc[e][k] = obj_valid ? objacc[e][k] * nc.gamma + ob[k] : ob[k];
+                }
+                ret[e] = ret[e] * nc.gamma + 0.0;  // SynthMO's scalar reward is 0 (vec_normalize.py:32)
+                const double rv = role == 1 ? sel_lane_d(objacc[e], ko) : role == 2 ? ret[e] : 0.0;
+                if (role == 1 || role == 2) S.sr[buf ^ 1][n][l] = rv;
+            }
+            obj_valid = 1;
+        }
+        // ---- drain: merge the last step's objective / ret accumulators, its reward, the done reset
+        lds_sync();
+        merge(T & 1, role == 1 || role == 2);
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+            const int n = w + 4 * e;
+            if (n >= NN) break;
+            emit_reward(e, n, T - 1);
+            if (dprev[e]) {
+#pragma unroll
+                for (int k = 0; k < K; ++k) objacc[e][k] = 0.0;
+                ret[e] = 0.0;
+            }
+            if (l < K) a.st.obj_acc[((size_t)p * NN + n) * K + l] = sel_lane_d(objacc[e], l);
+            if (l == 0) a.st.ret[p * NN + n] = ret[e];
+        }
+        if (w == 0) {
+            if (role == 1) {
+                a.ns.obj_mean[p * K + ko] = mean;
+                a.ns.obj_var[p * K + ko] = var;
+                if (ko == 0) a.ns.obj_count[p] = cnt;
+            } else if (role == 2) {
+                a.ns.ret_mean[p] = mean;
+                a.ns.ret_var[p] = var;
+                a.ns.ret_count[p] = cnt;
+                a.st.obj_acc_valid[p] = obj_valid;
+            }
         }
     }
     PGM_STAMP_FLUSH;
@@ -688,7 +735,7 @@ bool eval_waves_supported(const pgm_dims* d, int eval_num) {
 
 template <int O, int A, int K, int NN>
 static int launch_rollout_n(const pgm_dims* d, const RolloutArgs& a, hipStream_t s) {
-    if (int rc = launch_k(rollout_lane_kernel<O, A, K, NN>, dim3(d->P), dim3(64 * (NN < 4 ? NN : 4)),
+    if (int rc = launch_k(rollout_lane_kernel<O, A, K, NN>, dim3(d->P), dim3(2 * 64 * (NN < 4 ? NN : 4)),
                           sizeof(LaneSmem<O, A, NN>), s, a, "pgm_rollout"))
         return rc;
     return launch_critic_values(d, a, s);

@@ -95,6 +95,26 @@ __device__ __forceinline__ double tanh_d2(double y) {
     return copysign(fma(-2.0, r, 1.0), y);
 }
 
+// fp64 tanh with a table-driven exp: exp(x) = 2^m 2^(j/32) p(r), x = (32 m + j) ln2/32 + r, |r| <= ln2/64,
+// p = the degree-6 Taylor polynomial (error < 4e-18) in Estrin form (4 dependent steps); t2[j] = 2^(j/32)
+// from LDS.  Max |error| vs the IEEE tanh ~3e-16 (host-checked over [-25, 25]); about half the dependent
+// fp64 chain of tanh_d2.
+__device__ __forceinline__ double tanh_d3(double y, const double* t2) {
+    const double x = 2.0 * fmin(fabs(y), 20.0);
+    const double kf = __builtin_rint(x * 46.16624130844683);  // 32 / ln 2
+    const int k = (int)kf;
+    double r = fma(-kf, 0.021660849392496573, x);  // ln2/32, high 42 bits (k ln2/32 exact)
+    r = fma(-kf, 1.718100943346366e-15, r);        // ... low part
+    const double tj = t2[k & 31];
+    const double r2 = r * r;
+    const double p = (1.0 + r) + r2 * (fma(r, 1.0 / 6.0, 0.5) + r2 * (fma(r, 1.0 / 120.0, 1.0 / 24.0) + r2 * (1.0 / 720.0)));
+    const double e = __builtin_ldexp(tj * p, k >> 5) + 1.0;
+    double q = __builtin_amdgcn_rcp(e);
+    q = fma(q, fma(-e, q, 1.0), q);
+    q = fma(q, fma(-e, q, 1.0), q);
+    return copysign(fma(-2.0, q, 1.0), y);
+}
+
 // fp64 lane-half / row folds of the transposing multi-value sum (pgm_common.hpp has the fp32 forms)
 __device__ __forceinline__ double pl32_fold_d(double a, double b) {
     const auto lo = __builtin_amdgcn_permlane32_swap(__double2loint(a), __double2loint(b), false, false);

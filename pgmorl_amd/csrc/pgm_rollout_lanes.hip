@@ -175,6 +175,7 @@ struct LaneSmem {
     double sn[2][NN][64];                // pre-reset next state of env n (feature lanes), by step parity
     double e2[2][NN];                    // |clip(a)|^2 of env n, by step parity
     int dn[2][NN];                       // done of env n, by step parity
+    double t2[32];                       // 2^(j/32): tanh_d3's exp table
     alignas(16) float eps[2][NN][NCH * A];  // action noise of env n for NCH steps, double-buffered
 };
 
@@ -243,13 +244,17 @@ __global__ __launch_bounds__(512) void rollout_lane_kernel(RolloutArgs a) {
     }
     const bool upd = role == 0 ? nc.use_ob != 0 : role == 1 ? nc.use_obj != 0 : role == 2;
     double inv = 1.0;
-    // statistics merge of this lane's role (counts from before the merge; numpy's mean / var divide by N,
-    // exact for N a power of two)
-    auto merge = [&](int buf, bool active) {
-        const double tot = cnt + (double)NN;  // 1 / (count + N): hardware reciprocal + two Newton steps
+    // 1 / (count + N) for the next merge: hardware reciprocal + two Newton steps, formed before the barrier
+    double itot = 0.0;
+    auto prep_merge = [&]() {
+        const double tot = cnt + (double)NN;
         double r = __builtin_amdgcn_rcp(tot);
         r = fma(r, fma(-tot, r, 1.0), r);
-        const double itot = fma(r, fma(-tot, r, 1.0), r);
+        itot = fma(r, fma(-tot, r, 1.0), r);
+    };
+    // statistics merge of this lane's role (counts from before the merge; numpy's mean / var divide by N,
+    // exact for N a power of two); prep_merge() ran since the last merge
+    auto merge = [&](int buf, bool active) {
         double v[NN], sum = 0.0;
 #pragma unroll
         for (int n = 0; n < NN; ++n) {
@@ -269,6 +274,8 @@ __global__ __launch_bounds__(512) void rollout_lane_kernel(RolloutArgs a) {
             inv = rsqrt_d(var + nc.eps);
         }
     };
+    if (threadIdx.x < 32) S.t2[threadIdx.x] = exp2((double)threadIdx.x / 32.0);
+    lds_sync();  // (every wave: the two roles execute the same barriers)
     PGM_STAMP_DECL
 
     if (chain) {
@@ -405,7 +412,7 @@ __global__ __launch_bounds__(512) void rollout_lane_kernel(RolloutArgs a) {
                     pu[j] = U[j] * ac[j];
                 }
                 // dynamics (fp64, lane = feature): s' = tanh(d s + U clip(a) + c)
-                const double sn = tanh_d2(dd * s_o[e] + tree_sum(pu) + cc);
+                const double sn = tanh_d3(dd * s_o[e] + tree_sum(pu) + cc, S.t2);
                 const float lp = tree_sum(lpt);
                 store_lane(r_act, l < A ? (uint32_t)(((size_t)step * NN + n) * A + l) * 4 : OOB_OFF, sel_lane(avs, l));
                 store_lane(r_logp, l == 0 ? (uint32_t)((size_t)step * NN + n) * 4 : OOB_OFF, lp);
@@ -427,6 +434,7 @@ __global__ __launch_bounds__(512) void rollout_lane_kernel(RolloutArgs a) {
                 store_lane(r_bad, l == 0 ? moff : OOB_OFF, bf ? 0.f : 1.f);
                 if (e == 0) PGM_STAMP(2);
             }
+            prep_merge();
             lds_sync();
             PGM_STAMP(3);
             merge(buf, upd0);
@@ -498,6 +506,7 @@ __global__ __launch_bounds__(512) void rollout_lane_kernel(RolloutArgs a) {
         // the first row (step 0's barrier) carries nothing for them (merge inactive at step 0)
         for (int step = 0; step < T; ++step) {
             const int buf = step & 1;
+            prep_merge();
             lds_sync();
             merge(buf, (role == 1 || role == 2) && step > 0);
 #pragma unroll
@@ -532,6 +541,7 @@ __global__ __launch_bounds__(512) void rollout_lane_kernel(RolloutArgs a) {
             obj_valid = 1;
         }
         // ---- drain: merge the last step's objective / ret accumulators, its reward, the done reset
+        prep_merge();
         lds_sync();
         merge(T & 1, role == 1 || role == 2);
 #pragma unroll

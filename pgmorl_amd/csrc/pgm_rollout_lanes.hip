@@ -36,6 +36,10 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 template <int O, int K>
 constexpr bool lanes_fit() { return O <= 48 && O + K + 1 <= 64; }
 
+#ifndef PGM_ROLL_L2_LDS
+#define PGM_ROLL_L2_LDS 0  // 1: layer-2 inputs through the per-wave LDS row (A/B)
+#endif
+
 // per-lane actor tower: unit l of both layers, every head row of unit l (weights constant in a launch)
 template <int O, int A>
 struct ActorLane {
@@ -79,13 +83,25 @@ struct ActorLane {
             if (k + 2 < O) z0 = fmaf(v.z, w1[k + 2], z0);
             if (k + 3 < O) z1 = fmaf(v.w, w1[k + 3], z1);
         }
-        h1[l] = tanh_fast(z0 + z1);
+        const float hl = tanh_fast(z0 + z1);
+#if PGM_ROLL_L2_LDS
+        h1[l] = hl;
         wave_lds_fence_r();
-        // packed fp32 FMAs over unit pairs (v_pk_fma_f32: two MACs per instruction), two chains of 16
+#endif
+        // packed fp32 FMAs over unit pairs (v_pk_fma_f32: two MACs per instruction), two chains of 16; unit k's
+        // activation reaches every lane by v_readlane (no LDS round trip on the chain)
         f2 a01 = f2{b2, 0.f}, a23 = f2{0.f, 0.f};
 #pragma unroll
         for (int k = 0; k < H; k += 4) {
+#if PGM_ROLL_L2_LDS
             const float4 h = *reinterpret_cast<const float4*>(h1 + k);
+#else
+            const int hi = __float_as_int(hl);
+            const float4 h = make_float4(__int_as_float(__builtin_amdgcn_readlane(hi, k)),
+                                         __int_as_float(__builtin_amdgcn_readlane(hi, k + 1)),
+                                         __int_as_float(__builtin_amdgcn_readlane(hi, k + 2)),
+                                         __int_as_float(__builtin_amdgcn_readlane(hi, k + 3)));
+#endif
             a01 = __builtin_elementwise_fma(f2{h.x, h.y}, f2{w2[k], w2[k + 1]}, a01);
             a23 = __builtin_elementwise_fma(f2{h.z, h.w}, f2{w2[k + 2], w2[k + 3]}, a23);
         }
@@ -96,7 +112,9 @@ struct ActorLane {
         wave_sum64_multi<A>(pr, mu);
 #pragma unroll
         for (int j = 0; j < A; ++j) mu[j] += bm[j];
+#if PGM_ROLL_L2_LDS
         wave_lds_fence_r();  // every lane's h1 reads done before the row is rewritten
+#endif
     }
 };
 

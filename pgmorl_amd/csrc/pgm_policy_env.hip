@@ -782,6 +782,7 @@ int pgm_eval(const pgm_dims* d, const float* params, const pgm_env_spec* spec, c
                eval_num, use_ob_rms, raw, gamma, objs_out};
     const char* sel = getenv("PGM_EVAL_KERNEL");  // "block": the workgroup-per-step kernel (A/B, tests)
     if (!(sel && sel[0] == 'b') && eval_waves_supported(d, eval_num)) return launch_eval_waves(d, a, (hipStream_t)stream);
+    if (!(sel && sel[0] == 'b') && eval_wide_supported(d, eval_num)) return launch_eval_wide(d, a, (hipStream_t)stream);
     return dispatch_dims(d->O, d->A, d->K, "pgm_eval", [&](auto o, auto aa, auto k) {
         constexpr int O = decltype(o)::value, A = decltype(aa)::value, K = decltype(k)::value;
         return launch_smem(eval_kernel<O, A, K>, d->P, sizeof(StepSmem<O, A, K>), (hipStream_t)stream, a,

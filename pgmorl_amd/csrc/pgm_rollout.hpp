@@ -199,5 +199,8 @@ int launch_critic_values(const pgm_dims* d, const RolloutArgs& a, hipStream_t st
 // wide-observation rollout (pgm_rollout_wide.hip): 48 < obs_dim <= 448, N in {1, 2, 4, 8}, N*K <= 16
 bool rollout_wide_supported(const pgm_dims* d);
 int launch_rollout_wide(const pgm_dims* d, const RolloutArgs& a, hipStream_t stream);
+// wide-observation evaluation (pgm_rollout_wide.hip): 48 < obs_dim <= 512, eval_num <= 8, eval_num*K <= 16
+bool eval_wide_supported(const pgm_dims* d, int eval_num);
+int launch_eval_wide(const pgm_dims* d, const EvalArgs& a, hipStream_t stream);
 
 }  // namespace pgm

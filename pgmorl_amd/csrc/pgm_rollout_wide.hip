@@ -493,7 +493,258 @@ __global__ __launch_bounds__(WTH) void rollout_wide_kernel(RolloutArgs a) {
     }
 }
 
+// evaluation() (morl/mopg.py:25-46) for WIDE observations: the eval_num deterministic episodes of a task
+// run as the envs of one workgroup with the rollout's step structure (layer 1 on the f32 MFMA over the four
+// waves' k-slices, env n's layer 2 / mean head on wave n % 4, feature-slot fp64 dynamics), actions = the
+// clipped means, observations normalised in fp64 by the snapshot ob_rms (eps 1e-8, clip 10) and rounded to
+// fp32 as the policy input, raw objective sums discounted unless --raw; episodes end at the time limit.
+// Objective partial sums of step t are finished during step t + 1 by the statistics wave (lane n*K + k).
+template <int O, int A, int K, int NE>
+struct WideEvalSmem {
+    alignas(16) float x[NE][wrow<O>() + 4];
+    alignas(16) float zp[WW][NE][H];
+    alignas(16) float h1[NE][H];
+    float mu[NE][32];
+    double ac[NE][A];
+    double e2[2][NE];
+    double objp[2][WW][16];
+    double U[A][2 * WTH];
+    double acc[16];
+};
+
+template <int O, int A, int K, int NE>
+__global__ __launch_bounds__(WTH) void eval_wide_kernel(EvalArgs a) {
+    static_assert(O > 48 && O <= 2 * WTH && NE * K <= 16, "wide eval envelope");
+    constexpr int KW = wkw<O>(), OR = wrow<O>();
+    constexpr int FPL = (O + WTH - 1) / WTH;
+    constexpr int EPW = (NE + WW - 1) / WW;
+    constexpr int SW = WW - 1;
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    auto& S = *reinterpret_cast<WideEvalSmem<O, A, K, NE>*>(smem_raw);
+    const int p = blockIdx.x, t = threadIdx.x, l = t & 63;
+    const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+    const Layout& L = a.L;
+    const float* prm = a.params + (size_t)p * L.total;
+    const int maxs = a.spec.max_episode_steps;
+    const int ne = a.eval_num;  // live episodes (rows >= ne run a copy of episode 0 and are not counted)
+
+    constexpr int KQ = KW / 4;
+    const int lj = l & 15, lg = l >> 4;
+    float wb[KQ][4];
+#pragma unroll
+    for (int kk = 0; kk < KQ; ++kk) {
+        const int k = w * KW + lg * KQ + kk;
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb) wb[kk][jb] = k < O ? prm[L.off[PGM_P_ACTOR_W1] + k * H + 16 * jb + lj] : 0.f;
+    }
+    float w2[H], wm[A];
+#pragma unroll
+    for (int k = 0; k < H; ++k) w2[k] = prm[L.off[PGM_P_ACTOR_W2] + k * H + l];
+#pragma unroll
+    for (int j = 0; j < A; ++j) wm[j] = prm[L.off[PGM_P_MEAN_W] + l * A + j];
+    const float b1 = prm[L.off[PGM_P_ACTOR_B1] + l], b2 = prm[L.off[PGM_P_ACTOR_B2] + l];
+    const int la = l < A ? l : 0;
+    const float bm_l = prm[L.off[PGM_P_MEAN_B] + la];
+    const double lo_l = a.spec.act_lo[la], hi_l = a.spec.act_hi[la];
+
+    bool fv[FPL];
+    int fo[FPL];
+    double V[FPL][K], dd[FPL], cc[FPL], s[FPL][NE], mean[FPL], inv[FPL];
+#pragma unroll
+    for (int j = 0; j < FPL; ++j) {
+        fv[j] = t + WTH * j < O;
+        fo[j] = fv[j] ? t + WTH * j : 0;
+        const int o = fo[j];
+#pragma unroll
+        for (int k = 0; k < K; ++k) V[j][k] = fv[j] ? a.spec.V[k * O + o] : 0.0;
+        dd[j] = fv[j] ? a.spec.d[o] : 0.0;
+        cc[j] = fv[j] ? a.spec.c[o] : 0.0;
+#pragma unroll
+        for (int n = 0; n < NE; ++n) s[j][n] = fv[j] ? a.s0_eval[(size_t)(n < ne ? n : 0) * O + o] : 0.0;
+        // mopg.py:37-38: fp64 normalisation with the snapshot ob_rms, fixed eps 1e-8
+        mean[j] = a.use_ob && fv[j] ? a.ob_mean[(size_t)p * O + o] : 0.0;
+        inv[j] = a.use_ob && fv[j] ? 1.0 / sqrt(a.ob_var[(size_t)p * O + o] + 1e-8) : 1.0;
+    }
+    for (int i = t; i < A * O; i += WTH) {
+        const int q = i / O, f = i - q * O;
+        S.U[q][f] = a.spec.U[f * A + q];
+    }
+    auto norm_x = [&]() {  // normalised fp32 policy inputs of every episode (row padding stays zero)
+#pragma unroll
+        for (int j = 0; j < FPL; ++j) {
+            if (!fv[j]) continue;
+#pragma unroll
+            for (int n = 0; n < NE; ++n) {
+                double v = s[j][n];
+                if (a.use_ob) v = clipd((v - mean[j]) * inv[j], -10.0, 10.0);
+                S.x[n][fo[j]] = (float)v;
+            }
+        }
+    };
+    for (int i = t; i < NE * OR; i += WTH) (&S.x[0][0])[(i / OR) * (OR + 4) + i % OR] = 0.f;
+    __syncthreads();
+    norm_x();
+    // statistics wave: lane n*K + k accumulates episode n's objective k
+    const bool olane = w == SW && l < NE * K;
+    const int on = olane ? l / K : 0, ok = olane ? l % K : 0;
+    const double ebase = a.spec.ebase[ok], ecoef = a.spec.ecoef[ok];
+    double acc = 0.0, g = 1.0;
+    auto finish_step = [&](int par) {
+        if (olane) {
+            double sum = 0.0;
+#pragma unroll
+            for (int ww = 0; ww < WW; ++ww) sum += S.objp[par][ww][l];
+            const double raw = sum + ebase - ecoef * S.e2[par][on];
+            acc += g * raw;
+            if (!a.raw) g *= a.gamma;
+        }
+    };
+    __syncthreads();
+
+    for (int step = 0; step < maxs; ++step) {
+        const int par = step & 1;
+        {  // 1. layer-1 partial sums of this wave's k-slice (envs on MFMA rows)
+            f32x4 z4[4];
+#pragma unroll
+            for (int jb = 0; jb < 4; ++jb) z4[jb] = f32x4{0.f, 0.f, 0.f, 0.f};
+            const bool arow = lj < NE;
+            const float* xrow = &S.x[arow ? lj : 0][w * KW + lg * KQ];
+#pragma unroll
+            for (int q = 0; q < KQ; q += 4) {
+                float4 xv = *reinterpret_cast<const float4*>(xrow + q);
+                if (!arow) xv = make_float4(0.f, 0.f, 0.f, 0.f);
+                const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+#pragma unroll
+                    for (int jb = 0; jb < 4; ++jb)
+                        z4[jb] = __builtin_amdgcn_mfma_f32_16x16x4f32(xs[e], wb[q + e][jb], z4[jb], 0, 0, 0);
+            }
+            if (4 * lg < NE) {
+#pragma unroll
+                for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (4 * lg + r < NE) S.zp[w][4 * lg + r][16 * jb + lj] = z4[jb][r];
+            }
+        }
+        lds_sync();  // A
+        // 2. this wave's episodes: layer 1 sum + tanh, layer 2, mean head, clipped deterministic action
+#pragma unroll
+        for (int e = 0; e < EPW; ++e) {
+            const int n = w + WW * e;
+            if (n >= NE) break;
+            float z = b1;
+#pragma unroll
+            for (int ww = 0; ww < WW; ++ww) z += S.zp[ww][n][l];
+            S.h1[n][l] = tanh_fast(z);
+        }
+        wave_lds_fence_r();
+#pragma unroll
+        for (int e = 0; e < EPW; ++e) {
+            const int n = w + WW * e;
+            if (n >= NE) break;
+            f2 a01 = f2{b2, 0.f}, a23 = f2{0.f, 0.f};
+#pragma unroll
+            for (int k = 0; k < H; k += 4) {
+                const float4 hv = *reinterpret_cast<const float4*>(&S.h1[n][k]);
+                a01 = __builtin_elementwise_fma(f2{hv.x, hv.y}, f2{w2[k], w2[k + 1]}, a01);
+                a23 = __builtin_elementwise_fma(f2{hv.z, hv.w}, f2{w2[k + 2], w2[k + 3]}, a23);
+            }
+            const float h2 = tanh_fast((a01.x + a01.y) + (a23.x + a23.y));
+            float pr[A], mu[A];
+#pragma unroll
+            for (int j = 0; j < A; ++j) pr[j] = h2 * wm[j];
+            head_sums<A>(pr, mu);
+            if (l == 0) {
+#pragma unroll
+                for (int j = 0; j < A; ++j) S.mu[n][j] = mu[j];
+            }
+        }
+        wave_lds_fence_r();
+#pragma unroll
+        for (int e = 0; e < EPW; ++e) {
+            const int n = w + WW * e;
+            if (n >= NE) break;
+            const bool al = l < A;
+            const double acd = clipd_hw((double)(S.mu[n][la] + bm_l), lo_l, hi_l);
+            const double e2 = wave_sum64_d(al ? acd * acd : 0.0);
+            if (al) S.ac[n][l] = acd;
+            if (l == 0) S.e2[par][n] = e2;
+        }
+        lds_sync();  // C
+        // 3. fp64 dynamics of every episode per feature slot, objective partial sums, next inputs
+        {
+            double vk[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) vk[i] = 0.0;
+#pragma unroll
+            for (int j = 0; j < FPL; ++j) {
+                if (j > 0 && !fv[j]) continue;
+                double u[A];
+#pragma unroll
+                for (int q = 0; q < A; ++q) u[q] = S.U[q][fo[j]];
+#pragma unroll
+                for (int n = 0; n < NE; ++n) {
+                    asm volatile("" ::: "memory");
+                    double pu[A];
+#pragma unroll
+                    for (int q = 0; q < A; ++q) pu[q] = u[q] * S.ac[n][q];
+                    const double sn = tanh_d2(dd[j] * s[j][n] + tree_sum(pu) + cc[j]);
+#pragma unroll
+                    for (int k = 0; k < K; ++k) vk[n * K + k] = fma(V[j][k], sn, vk[n * K + k]);
+                    s[j][n] = sn;
+                }
+            }
+            wave_sum16_d(vk, &S.objp[par][w][0]);
+        }
+        norm_x();
+        if (w == SW && step > 0) finish_step(par ^ 1);
+        lds_sync();  // D
+    }
+    if (w == SW) finish_step((maxs - 1) & 1);
+    if (olane) S.acc[l] = acc;
+    __syncthreads();
+    if (t < K) {  // objs /= eval_num, episodes summed in order
+        double sum = 0.0;
+        for (int n = 0; n < ne; ++n) sum += S.acc[n * K + t];
+        a.objs[(size_t)p * K + t] = sum / (double)ne;
+    }
+}
+
 }  // namespace
+
+bool eval_wide_supported(const pgm_dims* d, int eval_num) {
+    return d->O > 48 && d->O <= 2 * WTH && eval_num >= 1 && eval_num <= 8 && eval_num * d->K <= 16 && d->A <= 32;
+}
+
+int launch_eval_wide(const pgm_dims* d, const EvalArgs& a, hipStream_t stream) {
+    return dispatch_dims(d->O, d->A, d->K, "pgm_eval", [&](auto o, auto aa, auto k) -> int {
+        constexpr int O = decltype(o)::value, A = decltype(aa)::value, K = decltype(k)::value;
+        if constexpr (O <= 48 || O > 2 * WTH || A > 32) {
+            set_error("pgm_eval: obs_dim %d outside the wide eval kernel", O);
+            return PGM_E_UNSUPPORTED;
+        } else {
+            auto go = [&](auto kern, size_t smem) -> int {
+                if (smem > 160 * 1024) {
+                    set_error("pgm_eval: LDS image %zu bytes exceeds 160 KiB", smem);
+                    return PGM_E_UNSUPPORTED;
+                }
+                hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+                if (e != hipSuccess) return hip_fail(e, "pgm_eval");
+                hipLaunchKernelGGL(kern, dim3(d->P), dim3(WTH), smem, stream, a);
+                return launch_status("pgm_eval");
+            };
+            const int en = a.eval_num;
+            if (en <= 1) return go(eval_wide_kernel<O, A, K, 1>, sizeof(WideEvalSmem<O, A, K, 1>));
+            if (en <= 2) return go(eval_wide_kernel<O, A, K, 2>, sizeof(WideEvalSmem<O, A, K, 2>));
+            if (en <= 4) return go(eval_wide_kernel<O, A, K, 4>, sizeof(WideEvalSmem<O, A, K, 4>));
+            if constexpr (8 * K <= 16) return go(eval_wide_kernel<O, A, K, 8>, sizeof(WideEvalSmem<O, A, K, 8>));
+            set_error("pgm_eval: eval_num %d outside the wide eval kernel", en);
+            return PGM_E_UNSUPPORTED;
+        }
+    });
+}
 
 bool rollout_wide_supported(const pgm_dims* d) {
     return d->O > 48 && d->O <= 2 * WTH && (d->N == 1 || d->N == 2 || d->N == 4 || d->N == 8) &&

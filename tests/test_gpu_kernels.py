@@ -357,6 +357,34 @@ def test_eval(gpu, env, eval_num, raw, kernel, monkeypatch):
         _close(objs[p], ref, 1e-4, 1e-5, 'evaluation objs')
 
 
+@pytest.mark.parametrize('kernel', ['wide', 'block'])
+@pytest.mark.parametrize('eval_num,raw,steps', [(6, False, 12), (1, True, 20), (3, False, 7), (8, True, 5)])
+def test_eval_wide(gpu, eval_num, raw, steps, kernel, monkeypatch):
+    """Humanoid evaluation (obs_dim 376): the wide eval kernel (eval_num episodes as the envs of one workgroup,
+    layer 1 on the f32 MFMA) and the block kernel vs the oracle.  Episodes are cut to a few steps on both sides
+    (the time limit is a spec field): SynthMO-Humanoid under a 376-input policy amplifies fp32 rounding ~2x every
+    3 steps (see test_rollout), so full 1000-step episodes are not comparable; tolerance 1e-3 + 2e-4 |ref| as
+    test_gpu_production."""
+    monkeypatch.setenv('PGM_EVAL_KERNEL', kernel)
+    env, P = 'MO-Humanoid-v2', 3
+    spec, tb, pols = _batch_with_policies(env, P, 8, 8, seed=5, scale=0.1, eval_num=eval_num, raw=raw)
+    spec = dict(spec, max_episode_steps=steps)
+    tb.spec = spec
+    tb.c_spec.max_episode_steps = steps
+    args = small_args(env, eval_num=eval_num, raw=raw)
+    rng = np.random.RandomState(2)
+    rms = []
+    for p in range(P):
+        r = RunningMeanStd(shape=(spec['obs_dim'],))
+        r.update(rng.randn(50, spec['obs_dim']) * 0.3 + 0.1)
+        rms.append(r)
+        tb.set_env_params(p, {'ob_rms': r})
+    objs = tb.evaluate().cpu().numpy()
+    s0_eval = envspec.reset_table(spec['obs_dim'], 0, eval_num)
+    for p in range(P):
+        _close(objs[p], oracle_evaluation(args, spec, s0_eval, pols[p], rms[p]), 1e-3, 2e-4, f'{kernel} task {p}')
+
+
 def _noise_fn(T, N, A, E, B):
     def fn(j):
         torch.manual_seed(j)

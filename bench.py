@@ -12,6 +12,7 @@ like the reference's FPS print, morl/mopg.py:159).
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 """
 import argparse
+import glob
 import json
 import os
 import platform
@@ -51,7 +52,9 @@ def parse():
                          'bench process itself (the box allows 16 processes with the GPU open)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-overlap-eval', action='store_true', help='evaluate on the main stream (A/B)')
-    ap.add_argument('--traffic-file', default=os.path.join(ROOT, 'profiles', 'r01_ppo_update_pmc.json'))
+    ap.add_argument('--traffic-file', default=None,
+                    help='PMC summary (scripts/pmc_summary.py) to quote as roofline.traffic; default: the newest '
+                         'profiles/r0*_pmc_*.json whose workload matches this run')
     return ap.parse_args()
 
 
@@ -276,13 +279,17 @@ def main():
     upd_flop = P * T * N * E * 6 * mf          # fwd (2 M_f) + bwd (4 M_f) per row per epoch, one launch
     achieved = upd_flop / (upd_ms * 1e-3) / 1e12
     traffic = None
-    if os.path.exists(args.traffic_file):
+    wl = f'{args.env_name}/P{P}/N{N}/T{T}/E{E}/M{M}'
+    cands = [args.traffic_file] if args.traffic_file else sorted(glob.glob(os.path.join(ROOT, 'profiles', 'r0*_pmc_*.json')) +
+                                                               [os.path.join(ROOT, 'profiles', 'r01_ppo_update_pmc.json')], reverse=True)
+    for f in cands:
         try:
-            tr = json.load(open(args.traffic_file))
-            if tr.get('workload') == f'{args.env_name}/P{P}/N{N}/T{T}/E{E}/M{M}':
-                traffic = tr.get('hbm_bytes_per_launch')
+            tr = json.load(open(f))
         except Exception:
-            traffic = None
+            continue
+        if tr.get('workload') == wl and tr.get('hbm_bytes_per_launch'):
+            traffic = tr['hbm_bytes_per_launch']
+            break
     out = {
         'metric': METRIC, 'value': value, 'unit': 'env steps/sec', 'n_gpus': world, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': dt / args.steps * 1e3, 'higher_is_better': True, 'scaling': args.scaling,

@@ -51,6 +51,7 @@ struct WideSmem {
     double objp[2][WW][16];              // per-wave sums of V_k . s'[n] (index n*K + k), by step parity
     alignas(16) float eps[2][NN][WNCH * A];
     double U[A][2 * WTH];                // SynthMO U^T, feature-contiguous (conflict-free per-thread reads)
+    double t2[32];                       // 2^(j/32): tanh_d3's exp table
 };
 
 // 16 simultaneous fp64 64-lane sums: after the folds, row R of y[j] holds value j + 4R; lane 16R writes it
@@ -163,6 +164,7 @@ __global__ __launch_bounds__(WTH) void rollout_wide_kernel(RolloutArgs a) {
         const int q = i / O, f = i - q * O;
         S.U[q][f] = a.spec.U[f * A + q];
     }
+    if (t < 32) S.t2[t] = exp2((double)t / 32.0);
     double cnt = a.ns.ob_count[p];
     int elapsed[NN];
 #pragma unroll
@@ -412,7 +414,7 @@ __global__ __launch_bounds__(WTH) void rollout_wide_kernel(RolloutArgs a) {
                     double pu[A];
 #pragma unroll
                     for (int q = 0; q < A; ++q) pu[q] = u[q] * S.ac[n][q];
-                    const double sn = tanh_d2(dd[j] * s[j][n] + tree_sum(pu) + cc[j]);
+                    const double sn = tanh_d3(dd[j] * s[j][n] + tree_sum(pu) + cc[j], S.t2);
 #pragma unroll
                     for (int k = 0; k < K; ++k) vk[n * K + k] = fma(V[j][k], sn, vk[n * K + k]);
                     s[j][n] = sn;
@@ -510,6 +512,7 @@ struct WideEvalSmem {
     double objp[2][WW][16];
     double U[A][2 * WTH];
     double acc[16];
+    double t2[32];
 };
 
 template <int O, int A, int K, int NE>
@@ -569,6 +572,7 @@ __global__ __launch_bounds__(WTH) void eval_wide_kernel(EvalArgs a) {
         const int q = i / O, f = i - q * O;
         S.U[q][f] = a.spec.U[f * A + q];
     }
+    if (t < 32) S.t2[t] = exp2((double)t / 32.0);
     auto norm_x = [&]() {  // normalised fp32 policy inputs of every episode (row padding stays zero)
 #pragma unroll
         for (int j = 0; j < FPL; ++j) {
@@ -690,7 +694,7 @@ __global__ __launch_bounds__(WTH) void eval_wide_kernel(EvalArgs a) {
                     double pu[A];
 #pragma unroll
                     for (int q = 0; q < A; ++q) pu[q] = u[q] * S.ac[n][q];
-                    const double sn = tanh_d2(dd[j] * s[j][n] + tree_sum(pu) + cc[j]);
+                    const double sn = tanh_d3(dd[j] * s[j][n] + tree_sum(pu) + cc[j], S.t2);
 #pragma unroll
                     for (int k = 0; k < K; ++k) vk[n * K + k] = fma(V[j][k], sn, vk[n * K + k]);
                     s[j][n] = sn;

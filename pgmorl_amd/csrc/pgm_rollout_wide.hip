@@ -142,20 +142,36 @@ __global__ __launch_bounds__(WTH) void rollout_wide_kernel(RolloutArgs a) {
     const double lo_l = a.spec.act_lo[la], hi_l = a.spec.act_hi[la];
 
     // ---- feature slots j: feature o = t + WTH*j (< O): env constants, every env's state, ob_rms of o
+    // SPL (O - WTH <= 128, e.g. Humanoid's 376 = 256 + 120): the features beyond WTH are split by env halves
+    // over lane pairs (l, l + 32) of wave w (feature WTH + 32 w + (l & 31), envs NH (l >> 5) .. + NH - 1), so every
+    // thread steps 8 + 4 (feature, env) pairs instead of 16 on half the threads and 8 on the rest; the pair's
+    // ob_rms batch moments meet through one lane swap
+    constexpr bool SPL = FPL == 2 && O - WTH <= WTH / 2 && NN >= 2;
+    constexpr int NH = SPL ? NN / 2 : NN;
+    const int hb = l >> 5;
     bool fv[FPL];
     int fo[FPL];
     double V[FPL][K], dd[FPL], cc[FPL], s[FPL][NN], mean[FPL], var[FPL], inv[FPL];
 #pragma unroll
     for (int j = 0; j < FPL; ++j) {
-        fv[j] = t + WTH * j < O;
-        fo[j] = fv[j] ? t + WTH * j : 0;
+        if (SPL && j == 1) {
+            const int i1 = w * 32 + (l & 31);
+            fv[j] = i1 < O - WTH;
+            fo[j] = fv[j] ? WTH + i1 : 0;
+        } else {
+            fv[j] = t + WTH * j < O;
+            fo[j] = fv[j] ? t + WTH * j : 0;
+        }
         const int o = fo[j];
 #pragma unroll
         for (int k = 0; k < K; ++k) V[j][k] = fv[j] ? a.spec.V[k * O + o] : 0.0;
         dd[j] = fv[j] ? a.spec.d[o] : 0.0;
         cc[j] = fv[j] ? a.spec.c[o] : 0.0;
 #pragma unroll
-        for (int n = 0; n < NN; ++n) s[j][n] = fv[j] ? a.st.s[((size_t)p * NN + n) * O + o] : 0.0;
+        for (int n = 0; n < NN; ++n) {
+            const int ne = SPL && j == 1 ? hb * NH + n : n;
+            s[j][n] = fv[j] && (!(SPL && j == 1) || n < NH) ? a.st.s[((size_t)p * NN + ne) * O + o] : 0.0;
+        }
         mean[j] = fv[j] ? a.ns.ob_mean[(size_t)p * O + o] : 0.0;
         var[j] = fv[j] ? a.ns.ob_var[(size_t)p * O + o] : 1.0;
         inv[j] = 1.0;
@@ -402,30 +418,78 @@ __global__ __launch_bounds__(WTH) void rollout_wide_kernel(RolloutArgs a) {
             double vk[16];
 #pragma unroll
             for (int i = 0; i < 16; ++i) vk[i] = 0.0;
+            double vk1[NH * K];  // SPL: slot 1's partial sums of its env half (compile-time slots)
+#pragma unroll
+            for (int i = 0; i < NH * K; ++i) vk1[i] = 0.0;
 #pragma unroll
             for (int j = 0; j < FPL; ++j) {
                 if (j > 0 && !fv[j]) continue;
                 double u[A];  // U row of the feature, once per step; clipped actions are LDS broadcasts
 #pragma unroll
                 for (int q = 0; q < A; ++q) u[q] = S.U[q][fo[j]];
+                const bool half = SPL && j == 1;
 #pragma unroll
-                for (int n = 0; n < NN; ++n) {
+                for (int n = 0; n < (half ? NH : NN); ++n) {
                     asm volatile("" ::: "memory");  // re-read the action row per (feature, env): no hoisting
+                    const int ne = half ? hb * NH + n : n;
                     double pu[A];
 #pragma unroll
-                    for (int q = 0; q < A; ++q) pu[q] = u[q] * S.ac[n][q];
+                    for (int q = 0; q < A; ++q) pu[q] = u[q] * S.ac[ne][q];
                     const double sn = tanh_d3(dd[j] * s[j][n] + tree_sum(pu) + cc[j], S.t2);
 #pragma unroll
-                    for (int k = 0; k < K; ++k) vk[n * K + k] = fma(V[j][k], sn, vk[n * K + k]);
+                    for (int k = 0; k < K; ++k) {
+                        if (half) vk1[n * K + k] = fma(V[j][k], sn, vk1[n * K + k]);
+                        else vk[n * K + k] = fma(V[j][k], sn, vk[n * K + k]);
+                    }
                     s[j][n] = sn;
+                }
+            }
+            if constexpr (SPL) {
+#pragma unroll
+                for (int i = 0; i < NH * K; ++i) {
+                    vk[i] += hb == 0 ? vk1[i] : 0.0;
+                    vk[NH * K + i] += hb == 1 ? vk1[i] : 0.0;
                 }
             }
             PGM_STAMP(4);
             wave_sum16_d(vk, &S.objp[par][w][0]);
             PGM_STAMP(5);
         }
+        if constexpr (SPL) {  // slot 1: this lane's env half; the pair's batch moments in fixed (half) order
+            constexpr int j = 1;
 #pragma unroll
-        for (int j = 0; j < FPL; ++j) {
+            for (int n = 0; n < NH; ++n) {
+                const int dn = hb ? done[NH + n] : done[n];
+                if (dn && fv[j]) s[j][n] = a.st.s0[(size_t)(hb * NH + n) * O + fo[j]];  // auto-reset
+            }
+            if (nc.use_ob) {
+                double ls = 0.0;
+#pragma unroll
+                for (int n = 0; n < NH; ++n) ls += s[j][n];
+                const double lo_ = __shfl_xor(ls, 32, 64);
+                const double sum = hb == 0 ? ls + lo_ : lo_ + ls;
+                const double bmean = sum * (1.0 / NN);
+                double lq = 0.0;
+#pragma unroll
+                for (int n = 0; n < NH; ++n) lq = fma(s[j][n] - bmean, s[j][n] - bmean, lq);
+                const double oq = __shfl_xor(lq, 32, 64);
+                const double sq = hb == 0 ? lq + oq : oq + lq;
+                chan_merge(mean[j], var[j], cnt, bmean, sq * (1.0 / NN), (double)NN);
+                inv[j] = rsqrt_d(var[j] + nc.eps);
+            }
+            if (fv[j]) {
+#pragma unroll
+                for (int n = 0; n < NH; ++n) {
+                    double v = s[j][n];
+                    if (nc.use_ob) v = clipd((v - mean[j]) * inv[j], -nc.clipob, nc.clipob);
+                    const float f = (float)v;  // VecPyTorch .float() (envs.py:192)
+                    S.x[hb * NH + n][fo[j]] = f;
+                    obs[((size_t)(step + 1) * NN + hb * NH + n) * O + fo[j]] = f;
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < (SPL ? 1 : FPL); ++j) {
             if (j > 0 && !fv[j]) continue;
 #pragma unroll
             for (int n = 0; n < NN; ++n)
@@ -467,10 +531,14 @@ __global__ __launch_bounds__(WTH) void rollout_wide_kernel(RolloutArgs a) {
 #pragma unroll
     for (int j = 0; j < FPL; ++j) {
         if (!fv[j]) continue;
+        const bool half = SPL && j == 1;
 #pragma unroll
-        for (int n = 0; n < NN; ++n) a.st.s[((size_t)p * NN + n) * O + fo[j]] = s[j][n];
-        a.ns.ob_mean[(size_t)p * O + fo[j]] = mean[j];
-        a.ns.ob_var[(size_t)p * O + fo[j]] = var[j];
+        for (int n = 0; n < (half ? NH : NN); ++n)
+            a.st.s[((size_t)p * NN + (half ? hb * NH + n : n)) * O + fo[j]] = s[j][n];
+        if (!half || hb == 0) {
+            a.ns.ob_mean[(size_t)p * O + fo[j]] = mean[j];
+            a.ns.ob_var[(size_t)p * O + fo[j]] = var[j];
+        }
     }
     if (t == 0) a.ns.ob_count[p] = cnt;
 #pragma unroll

@@ -31,6 +31,21 @@ __host__ __device__ inline NormCfg norm_cfg(const pgm_norm_state& ns) {
 
 // Chan merge of a batch (bm, bv, n) into (mean, var, count) -- running_mean_std.py:20-31
 // (one fp64 division: the reference's three divisions by tot_count become a multiply by 1/tot)
+// 1 / x in fp64: hardware reciprocal + two Newton steps (~1 ulp; no IEEE divide sequence on a step chain)
+__device__ __forceinline__ double rcp_d(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+    r = fma(r, fma(-x, r, 1.0), r);
+    return fma(r, fma(-x, r, 1.0), r);
+}
+// chan_merge with 1 / (count + n) supplied (formed once per step for every statistic that shares the count)
+__device__ __forceinline__ void chan_merge_i(double& mean, double& var, double count, double bm, double bv, double n,
+                                             double inv_tot) {
+    const double delta = bm - mean;
+    const double new_mean = mean + delta * n * inv_tot;
+    const double m2 = var * count + bv * n + delta * delta * count * n * inv_tot;
+    mean = new_mean;
+    var = m2 * inv_tot;
+}
 __device__ __forceinline__ void chan_merge(double& mean, double& var, double count, double bm, double bv, double n) {
     const double delta = bm - mean;
     const double inv_tot = 1.0 / (count + n);

@@ -187,9 +187,11 @@ __global__ __launch_bounds__(WTH) void rollout_wide_kernel(RolloutArgs a) {
     for (int n = 0; n < NN; ++n) elapsed[n] = a.st.elapsed[p * NN + n];
 
     // ---- statistics wave: lane i = n*K + k < NN*K (objective accumulator + obj_rms of objective k),
-    // lane 32 + n < 32 + NN (ret of env n + ret_rms)
-    const bool olane = w == SW && l < NN * K, rlane = w == SW && l >= 32 && l < 32 + NN;
-    const int on = olane ? l / K : 0, ok = olane ? l % K : 0, rn = rlane ? l - 32 : 0;
+    // lane 32 + n*K (ret of env n + ret_rms): both groups are the lanes of one residue mod K in a 16-lane row,
+    // so one set of DPP row rotations forms every batch moment
+    const bool olane = w == SW && l < NN * K;
+    const bool rlane = w == SW && l >= 32 && l < 32 + NN * K && ((l - 32) % K) == 0;
+    const int on = olane ? l / K : 0, ok = olane ? l % K : 0, rn = rlane ? (l - 32) / K : 0;
     double objacc = olane ? a.st.obj_acc[((size_t)p * NN + on) * K + ok] : 0.0;
     double retv = rlane ? a.st.ret[p * NN + rn] : 0.0;
     double smean = 0.0, svar = 1.0, scnt = 1.0, sinv = 1.0;
@@ -264,43 +266,45 @@ __global__ __launch_bounds__(WTH) void rollout_wide_kernel(RolloutArgs a) {
     for (int n = 0; n < NN; ++n) done_prev[n] = 0;
 
     // statistics of step st (objective sums in objp[par], e2[par]) -> rewards, accumulators, obj/ret_rms
-    auto finish_step = [&](int st, int par) {
+    // sum over the lanes of this lane's residue mod K in its 16-lane row (the batch of one statistic)
+    auto group_sum = [&](double v) {
+        if constexpr (K <= 8) v += dpp_d<0x128>(v);  // row_ror:8
+        if constexpr (K <= 4) v += dpp_d<0x124>(v);
+        if constexpr (K <= 2) v += dpp_d<0x122>(v);
+        if constexpr (K <= 1) v += dpp_d<0x121>(v);
+        return v;
+    };
+    auto finish_step = [&](int st, int par) {  // wave SW only (wave-uniform call): every lane runs the DPP folds
+        double x = 0.0, raw = 0.0;
         if (olane) {
             double sum = 0.0;
 #pragma unroll
             for (int ww = 0; ww < WW; ++ww) sum += S.objp[par][ww][l];
-            const double raw = sum + ebase - ecoef * S.e2[par][on];
+            raw = sum + ebase - ecoef * S.e2[par][on];
             objacc = obj_valid ? objacc * nc.gamma + raw : raw;
+            x = objacc;
+        }
+        if (rlane) {  // ret = ret * gamma + 0 (SynthMO's scalar reward)
+            retv = retv * nc.gamma + 0.0;
+            x = retv;
+        }
+        const bool mrg = (olane && nc.use_obj) || rlane;  // obj_rms (if used) / ret_rms over the envs
+        const double bmean = group_sum(mrg ? x : 0.0) * (1.0 / NN);
+        const double bsq = group_sum(mrg ? (x - bmean) * (x - bmean) : 0.0);
+        if (mrg) {
+            chan_merge_i(smean, svar, scnt, bmean, bsq * (1.0 / NN), (double)NN, rcp_d(scnt + (double)NN));
+            scnt += (double)NN;
+        }
+        if (olane) {
             double r = raw;
-            if (nc.use_obj) {  // batch moments over the envs of objective k (lanes l ^ K*m)
-                double bsum = objacc;
-#pragma unroll
-                for (int m = K; m < NN * K; m <<= 1) bsum += __shfl_xor(bsum, m, 64);
-                const double bmean = bsum * (1.0 / NN);
-                double bsq = (objacc - bmean) * (objacc - bmean);
-#pragma unroll
-                for (int m = K; m < NN * K; m <<= 1) bsq += __shfl_xor(bsq, m, 64);
-                chan_merge(smean, svar, scnt, bmean, bsq * (1.0 / NN), (double)NN);
-                scnt += (double)NN;
+            if (nc.use_obj) {
                 sinv = rsqrt_d(svar + nc.eps);
                 r = clipd(r * sinv, -nc.cliprew, nc.cliprew);
             }
             rew[(size_t)st * NN * K + l] = (float)r;
             if (sel_lane_i(done_prev, on)) objacc = 0.0;
         }
-        if (rlane) {  // ret = ret * gamma + 0 (SynthMO's scalar reward), ret_rms over the envs
-            retv = retv * nc.gamma + 0.0;
-            double bsum = retv;
-#pragma unroll
-            for (int m = 1; m < NN; m <<= 1) bsum += __shfl_xor(bsum, m, 64);
-            const double bmean = bsum * (1.0 / NN);
-            double bsq = (retv - bmean) * (retv - bmean);
-#pragma unroll
-            for (int m = 1; m < NN; m <<= 1) bsq += __shfl_xor(bsq, m, 64);
-            chan_merge(smean, svar, scnt, bmean, bsq * (1.0 / NN), (double)NN);
-            scnt += (double)NN;
-            if (sel_lane_i(done_prev, rn)) retv = 0.0;
-        }
+        if (rlane && sel_lane_i(done_prev, rn)) retv = 0.0;
         obj_valid = 1;
     };
 
@@ -455,6 +459,7 @@ __global__ __launch_bounds__(WTH) void rollout_wide_kernel(RolloutArgs a) {
             wave_sum16_d(vk, &S.objp[par][w][0]);
             PGM_STAMP(5);
         }
+        const double itot = rcp_d(cnt + (double)NN);  // shared by every feature's merge of this step
         if constexpr (SPL) {  // slot 1: this lane's env half; the pair's batch moments in fixed (half) order
             constexpr int j = 1;
 #pragma unroll
@@ -474,7 +479,7 @@ __global__ __launch_bounds__(WTH) void rollout_wide_kernel(RolloutArgs a) {
                 for (int n = 0; n < NH; ++n) lq = fma(s[j][n] - bmean, s[j][n] - bmean, lq);
                 const double oq = __shfl_xor(lq, 32, 64);
                 const double sq = hb == 0 ? lq + oq : oq + lq;
-                chan_merge(mean[j], var[j], cnt, bmean, sq * (1.0 / NN), (double)NN);
+                chan_merge_i(mean[j], var[j], cnt, bmean, sq * (1.0 / NN), (double)NN, itot);
                 inv[j] = rsqrt_d(var[j] + nc.eps);
             }
             if (fv[j]) {
@@ -502,7 +507,7 @@ __global__ __launch_bounds__(WTH) void rollout_wide_kernel(RolloutArgs a) {
                 double sq = 0.0;
 #pragma unroll
                 for (int n = 0; n < NN; ++n) sq = fma(s[j][n] - bmean, s[j][n] - bmean, sq);
-                chan_merge(mean[j], var[j], cnt, bmean, sq * (1.0 / NN), (double)NN);
+                chan_merge_i(mean[j], var[j], cnt, bmean, sq * (1.0 / NN), (double)NN, itot);
                 inv[j] = rsqrt_d(var[j] + nc.eps);
             }
             if (fv[j]) {

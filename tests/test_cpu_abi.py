@@ -109,3 +109,32 @@ def test_adam_state_roundtrip():
     opt2.load_state_dict({'state': st, 'param_groups': opt.state_dict()['param_groups']})
     for i in st:
         assert torch.allclose(opt2.state_dict()['state'][i]['exp_avg'], opt.state_dict()['state'][i]['exp_avg'].float().double())
+
+
+@pytest.mark.parametrize('env,P,N,T', [('MO-Walker2d-v2', 40, 4, 2048), ('MO-Hopper-v3', 27, 4, 2048),
+                                       ('MO-Humanoid-v2', 20, 8, 2048), ('MO-Humanoid-v2', 3, 8, 64)])
+def test_update_workspace_covers_every_split(env, P, N, T):
+    """pgm_ppo_update_workspace_bytes covers the largest row split a launch may pick (PGM_NS_MAX = 4 parts per
+    tower): tagged norm granules (2 x 4 x P + 1, 256-B padded), exchange slots [P][2 towers][4 parts][2
+    parities], and the packed sample table (obs_dim <= 32) or the parts' private parameter rows (wide)."""
+    from pgmorl_amd import envspec
+    spec = envspec.make_spec(env)
+    O, A, K, H = spec['obs_dim'], spec['act_dim'], spec['obj_num'], 64
+    Q = max(A, K)
+    d = _lib.Dims(P, N, T, O, A, K, H)
+    got = _lib.lib().pgm_ppo_update_workspace_bytes(d)
+    flags = -(-(2 * 4 * P + 1) * 8 // 256) * 256
+    if O <= 32:
+        img = O * H + H * (H + 1) + Q * H + 2 * H + Q + A
+        xslot = -(-(img + 1) // 32) * 32
+        n = O + A + 2 + 2 * K
+        rs = 16 if n <= 16 else 32 if n <= 32 else 64 if n <= 64 else 128
+        want = flags + P * 2 * 4 * 2 * xslot * 8 + P * T * N * rs * 4
+    else:
+        img = H * (H + 1) + Q * H + 2 * H + Q + A
+        nkt = -(-O // 32)
+        nkw = -(-nkt // 4)
+        xslot = -(-((img + nkt * 32 * H + nkw * 16 * 256 + 1) // 2 + 2) // 32) * 32
+        L = ParamLayout(O, A, K).total
+        want = flags + P * 2 * 4 * 2 * xslot * 8 + P * 3 * L * 4
+    assert got == want, (got, want)

@@ -904,9 +904,10 @@ struct T16SmemT {
     float aiv[A];                           // actor 1 / std^2
     float red[32];
     static constexpr int NIMG = W == 4 ? 2 : 1;  // W = 4: wave pairs (0,1) and (2,3) fill one image each
-    union Big {
+    static constexpr int IMGP = (IMG + 3) & ~3;  // image stride: every image 16-B aligned (float4 / LDS-DMA)
+    union alignas(16) Big {
         float scr[W][T16][S16];             // transpose tiles during the passes
-        float GA[NIMG][IMG];                // the workgroup's gradient image(s) after them
+        float GA[NIMG][IMGP];               // the workgroup's gradient image(s) after them
     } big;
 };
 template <int O, int A, int K, int W>
@@ -1419,6 +1420,49 @@ __global__ __launch_bounds__(64 * W) void ppo_update_t16_kernel(MArgs a) {
                     lds_sync_m();
                 }
                 lsum_all = S.red[4];
+                if constexpr (NS == 4 && Sm::NIMG == 2) {
+                    // every partner byte in flight at once: the first two partners (part order) by LDS-DMA into
+                    // the two image buffers (free since own4 was formed: the barriers above), the third into
+                    // registers; one retire + barrier, then the sums in part order
+                    const int hA = hs == 0 ? 1 : 0, hB = hs <= 1 ? 2 : 1, hC = hs <= 2 ? 3 : 2;
+                    const char* xbase = reinterpret_cast<const char*>(a.xb);
+                    constexpr int NDI = (NV4 * 16 + 1023) / 1024;  // 1-KiB LDS-DMA pieces per image
+                    for (int d = w; d < NDI; d += W) {
+                        const int byte = d * 1024 + 16 * l;
+                        if (byte < NV4 * 16) {  // the image tail (TAIL floats) stays untouched in GA[0]
+                            __builtin_amdgcn_global_load_lds((const void*)(xbase + (size_t)slot_of(hA) * a.xslot * 8 + byte),
+                                                             (lds_void_t*)&S.big.GA[0][d * 256], 16, 0, SC1);
+                            __builtin_amdgcn_global_load_lds((const void*)(xbase + (size_t)slot_of(hB) * a.xslot * 8 + byte),
+                                                             (lds_void_t*)&S.big.GA[1][d * 256], 16, 0, SC1);
+                        }
+                    }
+                    u32x4 pc[NG4];
+#pragma unroll
+                    for (int k = 0; k < NG4; ++k) {
+                        const int i = min(t + k * NT, NV4 - 1);
+                        pc[k] = __builtin_amdgcn_raw_buffer_load_b128(xr, slot_of(hC) * a.xslot * 8 + 16 * i, 0, SC1);
+                    }
+                    dma_sync_m();
+#pragma unroll
+                    for (int k = 0; k < NG4; ++k) {
+                        const int i = min(t + k * NT, NV4 - 1);
+                        const float4 va = *reinterpret_cast<const float4*>(&S.big.GA[0][4 * i]);
+                        const float4 vb = *reinterpret_cast<const float4*>(&S.big.GA[1][4 * i]);
+                        const f32x4 fa = f32x4{va.x, va.y, va.z, va.w}, fb = f32x4{vb.x, vb.y, vb.z, vb.w};
+                        const f32x4 fc = f32x4{__uint_as_float(pc[k][0]), __uint_as_float(pc[k][1]),
+                                               __uint_as_float(pc[k][2]), __uint_as_float(pc[k][3])};
+                        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                        for (int h = 0; h < NS; ++h) {
+                            const f32x4 v = h == hs ? own4[k] : h == hA ? fa : h == hB ? fb : fc;
+                            acc = h == 0 ? v : acc + v;
+                        }
+                        ag[k] = acc;
+                        if (t + k * NT < NV4)
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) sq2 = fmaf(acc[q], acc[q], sq2);
+                    }
+                } else {
                 // partner loads in flight KC groups at a time (registers), then the sums in part order
                 constexpr int KC = 2;  // 3 measured slower
 #pragma unroll
@@ -1449,6 +1493,7 @@ __global__ __launch_bounds__(64 * W) void ppo_update_t16_kernel(MArgs a) {
 #pragma unroll
                             for (int q = 0; q < 4; ++q) sq2 = fmaf(acc[q], acc[q], sq2);
                     }
+                }
                 }
                 if (t < TAIL) {
                     float acc = 0.f;

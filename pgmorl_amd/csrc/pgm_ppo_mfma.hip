@@ -1390,13 +1390,11 @@ __global__ __launch_bounds__(64 * W) void ppo_update_t16_kernel(MArgs a) {
                         unsigned long long* flag_mine = a.xb + (size_t)slot_of(hs) * a.xslot + a.xslot - 1;
                         __hip_atomic_store(flag_mine, ((unsigned long long)tag << 32) | __float_as_uint(lsum_wg),
                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        float lparts[NS];
-                        for (int h = 0; h < NS; ++h) {
-                            if (h == hs) {
-                                lparts[h] = lsum_wg;
-                                continue;
-                            }
-                            const unsigned long long* flag_h = a.xb + (size_t)slot_of(h) * a.xslot + a.xslot - 1;
+                    }
+                    if (t < NS) {  // lane h polls part h's flag: the NS - 1 polls run concurrently
+                        float lp = lsum_wg;
+                        if (t != hs) {
+                            const unsigned long long* flag_h = a.xb + (size_t)slot_of(t) * a.xslot + a.xslot - 1;
                             unsigned long long x = 0;
                             for (unsigned spins = 0;; ++spins) {
                                 x = __hip_atomic_load(flag_h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1408,10 +1406,14 @@ __global__ __launch_bounds__(64 * W) void ppo_update_t16_kernel(MArgs a) {
                                 }
                                 __builtin_amdgcn_s_sleep(1);
                             }
-                            lparts[h] = __uint_as_float((unsigned)x);
+                            lp = __uint_as_float((unsigned)x);
                         }
+                        S.red[16 + t] = lp;
+                    }
+                    lds_sync_m();
+                    if (t == 0) {
                         float ls = 0.f;
-                        for (int h = 0; h < NS; ++h) ls += lparts[h];
+                        for (int h = 0; h < NS; ++h) ls += S.red[16 + h];  // part order
                         S.red[4] = ls;
                     }
                     lds_sync_m();

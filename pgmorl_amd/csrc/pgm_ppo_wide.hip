@@ -75,7 +75,8 @@ struct WSmem {
     float dout[4][TS][Q];  // per-wave dL/d(head output) of the current tile
     float dls[4][TS][Q];   // per-wave per-sample dL/d(logstd) of the current tile (actor)
     float aiv[A];          // actor 1 / std^2
-    float red[16];
+    float red[32];  // [0,4) wave sums of squares, 4 norm total, [8,12) wave loss sums, 12 loss total,
+                    // [16, 16 + 2 NS) norm parts, [24, 24 + NS) loss parts (one polling lane each)
     int32_t rowid[4][TS];  // rollout rows of every wave's tile of the current pass
     float act2[4][TS][SCR];  // per-wave tile B: H2, then dZ2
     union Big {            // per-wave transpose tiles (dZ1 shared at the pass end), gradient images after
@@ -631,16 +632,17 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
                     unsigned long long* flag_mine = a.xb + (size_t)slot_of(hs) * a.xslot + a.xslot - 1;
                     __hip_atomic_store(flag_mine, ((unsigned long long)tag << 32) | __float_as_uint(lsum_wg),
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                if (t < NS)  // lane h polls part h's flag: the NS - 1 polls run concurrently
+                    S.red[24 + t] = t == hs ? lsum_wg
+                                            : __uint_as_float((unsigned)spin(a.xb + (size_t)slot_of(t) * a.xslot + a.xslot - 1, tag));
+                PGM_STAMP(8);
+                lds_sync_m();  // every polling lane matched: every wave may load the other parts' gradients
+                if (t == 0) {
                     float ls = 0.f;
-                    for (int hh = 0; hh < NS; ++hh) {  // loss sums in part order
-                        const float v = hh == hs ? lsum_wg
-                                                 : __uint_as_float((unsigned)spin(a.xb + (size_t)slot_of(hh) * a.xslot + a.xslot - 1, tag));
-                        ls = hh == 0 ? v : ls + v;
-                    }
+                    for (int hh = 0; hh < NS; ++hh) ls = hh == 0 ? S.red[24] : ls + S.red[24 + hh];  // part order
                     S.red[12] = ls;
                 }
-                PGM_STAMP(8);
-                lds_sync_m();  // the polling lane matched: every wave may load the other parts' gradients
                 {  // this part's dW1 slice from every other part: all loads in flight, then the part-order sums
                     float ov[NS > 1 ? NS - 1 : 1][NB][RS];
 #pragma unroll
@@ -717,22 +719,24 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
             if (l == 0) S.red[w] = sq;
             lds_sync_m();
             float total = (S.red[0] + S.red[1]) + (S.red[2] + S.red[3]);
-            if (t == 0) {
+            if (t == 0)
                 __hip_atomic_store(a.ws + ppo_norm_granule(a.P, p, m, hs), ((unsigned long long)tag << 32) | __float_as_uint(total),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const bool failed = __hip_atomic_load(a.ws + 2 * a.P, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                float tot = 0.f;
-                for (int mm = 0; mm < 2; ++mm)
-                    for (int hh = 0; hh < NS; ++hh) {
-                        float v = total;
-                        if (mm != m || hh != hs)
-                            v = failed ? 0.f : __uint_as_float((unsigned)spin(a.ws + ppo_norm_granule(a.P, p, mm, hh), tag));
-                        tot = mm == 0 && hh == 0 ? v : tot + v;
-                    }
-                S.red[4] = tot;
+            if (t < 2 * NS) {  // lane (mm, hh) = (t / NS, t % NS) polls that workgroup's granule, all concurrently
+                const int mm = t / NS, hh = t - mm * NS;
+                float v = total;
+                if (mm != m || hh != hs) {
+                    const bool failed = __hip_atomic_load(a.ws + 2 * a.P, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    v = failed ? 0.f : __uint_as_float((unsigned)spin(a.ws + ppo_norm_granule(a.P, p, mm, hh), tag));
+                }
+                S.red[16 + t] = v;
             }
             lds_sync_m();
-            total = S.red[4];
+            {  // (tower, part) order, identical in every workgroup of the task
+                float tot = S.red[16];
+                for (int i = 1; i < 2 * NS; ++i) tot += S.red[16 + i];
+                total = tot;
+            }
             const float coef = fminf(a.hp.max_grad_norm / (sqrtf(total) + 1e-6f), 1.f);
             if (t == 0) {
                 if (m == 0) st_v += 0.5f * lsum_task / (float)(mb * K);
@@ -807,12 +811,10 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
             }
             if constexpr (NS > 1) {
                 lds_sync_m();  // every wave's slice stores drained
-                if (t == 0) {
+                if (t == 0)
                     __hip_atomic_store(a.xb + (size_t)slot_of(hs) * a.xslot + a.xslot - 2, (unsigned long long)tag << 32,
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    for (int hh = 0; hh < NS; ++hh)
-                        if (hh != hs) spin(a.xb + (size_t)slot_of(hh) * a.xslot + a.xslot - 2, tag);
-                }
+                if (t < NS && t != hs) spin(a.xb + (size_t)slot_of(t) * a.xslot + a.xslot - 2, tag);  // concurrent polls
                 lds_sync_m();
                 // the other parts' new slices -> this part's layer-1 copy
 #pragma unroll

@@ -1,0 +1,111 @@
+"""ctypes binding of libpgm_host.so (include/pgm_host.h): the native generation-boundary path (hyperbolic fits,
+greedy selection, EP membership, hypervolume).  Host-only: no torch / GPU runtime involved.  There is no
+fallback: a missing library raises on first use."""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get('PGM_HOST_LIB') or os.path.join(HERE, 'libpgm_host.so')
+PGM_HOST_ABI_VERSION = 1
+
+_P = C.c_void_p
+_I64 = C.c_int64
+_I32 = C.c_int32
+_lib = None
+
+
+class PGMHostError(RuntimeError):
+    pass
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise PGMHostError(f'{LIB_PATH} missing: run python -m pgmorl_amd.build (the boundary has no Python fallback)')
+        L = C.CDLL(LIB_PATH)
+        L.pgm_host_abi_version.restype = C.c_int
+        L.pgm_host_last_error.restype = C.c_char_p
+        L.pgm_fit_hyperbolic.argtypes = [_I64, _P, _P, _P, _P, _P, _P, _P, C.c_int]
+        L.pgm_ep_mask.argtypes = [_I64, C.c_int, _P, _P]
+        L.pgm_hypervolume.argtypes = [_I64, C.c_int, _P, _P]
+        L.pgm_select_greedy.argtypes = [C.c_int, C.c_int, _I64, _P, _I64, _P, C.c_double, C.c_int, C.c_int, _P, _P]
+        if L.pgm_host_abi_version() != PGM_HOST_ABI_VERSION:
+            raise PGMHostError(f'libpgm_host.so ABI {L.pgm_host_abi_version()} != {PGM_HOST_ABI_VERSION}')
+        _lib = L
+    return _lib
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise PGMHostError(f'{what}: {lib().pgm_host_last_error().decode()} (status {rc})')
+
+
+def _f64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def _ptr(a):
+    return a.ctypes.data_as(_P) if a is not None and a.size else None
+
+
+def threads():
+    """Fit / scoring threads: PGM_HOST_THREADS, default the usable CPUs (at most 16)."""
+    n = int(os.environ.get('PGM_HOST_THREADS', '0'))
+    return n if n > 0 else min(16, len(os.sched_getaffinity(0)))
+
+
+def fit_hyperbolic(problems, nthreads=None, return_nfev=False):
+    """problems: list of (x, y, w, a_hi).  Returns [len, 4] fitted (A, a, b, c) (and the evaluation counts)."""
+    n = len(problems)
+    off = np.zeros(n + 1, dtype=np.int64)
+    for i, (x, _, _, _) in enumerate(problems):
+        off[i + 1] = off[i] + len(x)
+    xs = _f64(np.concatenate([p[0] for p in problems])) if n else np.zeros(0)
+    ys = _f64(np.concatenate([p[1] for p in problems])) if n else np.zeros(0)
+    ws = _f64(np.concatenate([p[2] for p in problems])) if n else np.zeros(0)
+    ah = _f64([p[3] for p in problems])
+    out = np.zeros((n, 4), dtype=np.float64)
+    nfev = np.zeros(n, dtype=np.int32)
+    if n:
+        _check(lib().pgm_fit_hyperbolic(n, _ptr(off), _ptr(xs), _ptr(ys), _ptr(ws), _ptr(ah), _ptr(out), _ptr(nfev),
+                                        threads() if nthreads is None else nthreads), 'pgm_fit_hyperbolic')
+    return (out, nfev) if return_nfev else out
+
+
+def ep_mask(objs):
+    o = _f64(objs)
+    n, k = (o.shape[0], o.shape[1]) if o.ndim == 2 else (0, 1)
+    keep = np.zeros(n, dtype=np.uint8)
+    if n:
+        _check(lib().pgm_ep_mask(n, k, _ptr(o), _ptr(keep)), 'pgm_ep_mask')
+    return keep.astype(bool)
+
+
+def hypervolume(objs):
+    o = _f64(objs)
+    if o.size == 0:
+        return 0.0
+    o = o.reshape(len(o), -1)
+    hv = np.zeros(1, dtype=np.float64)
+    _check(lib().pgm_hypervolume(o.shape[0], o.shape[1], _ptr(o), _ptr(hv)), 'pgm_hypervolume')
+    return float(hv[0])
+
+
+STAIRCASE, UPDATE_EP = 0, 1
+
+
+def select_greedy(ep_objs, preds, alpha, n_pick, mode, nthreads=None):
+    """Indices of the greedy picks (fewer than n_pick when the candidates run out); mode STAIRCASE (2-D
+    population) or UPDATE_EP (3-D population)."""
+    p = _f64(preds)
+    k = p.shape[1]
+    e = _f64(ep_objs).reshape(-1, k)
+    picks = np.zeros(max(n_pick, 1), dtype=np.int32)
+    npk = np.zeros(1, dtype=np.int32)
+    _check(lib().pgm_select_greedy(k, int(mode), len(e), _ptr(e), len(p), _ptr(p), float(alpha), int(n_pick),
+                                   threads() if nthreads is None else nthreads, _ptr(picks), _ptr(npk)),
+           'pgm_select_greedy')
+    return [int(i) for i in picks[:npk[0]]]

@@ -1,4 +1,4 @@
-"""Build libpgm.so (gfx950) in-tree with hipcc.  ``python -m pgmorl_amd.build``."""
+"""Build libpgm.so (gfx950) with hipcc and libpgm_host.so with g++, in-tree.  ``python -m pgmorl_amd.build``."""
 import os
 import subprocess
 import sys
@@ -27,6 +27,25 @@ def _newest(paths):
     return max(os.path.getmtime(p) for p in paths)
 
 
+HOST_LIB = os.path.join(HERE, 'libpgm_host.so')
+
+
+def build_host(force=False, verbose=False):
+    """libpgm_host.so: the native generation-boundary path (include/pgm_host.h), host C++ only (g++)."""
+    src = os.path.join(CSRC, 'pgm_host.cpp')
+    hdr = os.path.join(ROOT, 'include', 'pgm_host.h')
+    if not force and os.path.exists(HOST_LIB) and os.path.getmtime(HOST_LIB) >= _newest([src, hdr]):
+        return HOST_LIB
+    cmd = [os.environ.get('CXX', 'g++'), '-O2', '-std=c++17', '-fPIC', '-shared', '-pthread', '-I',
+           os.path.join(ROOT, 'include'), src, '-o', HOST_LIB]
+    if verbose:
+        print(' '.join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f'g++ failed on pgm_host.cpp:\n{r.stdout}\n{r.stderr}')
+    return HOST_LIB
+
+
 def build(force=False, verbose=False, stamps=False):
     """stamps=True builds the diagnostic libpgm_stamps.so (-DPGM_STAMPS phase timers); never shipped."""
     objdir = OBJDIR + ('_stamps' if stamps else '')
@@ -50,6 +69,8 @@ def build(force=False, verbose=False, stamps=False):
             raise RuntimeError(f'hipcc failed on {src}:\n{r.stdout}\n{r.stderr}')
         return o
 
+    if not stamps:
+        build_host(force=force, verbose=verbose)
     with ThreadPoolExecutor(max_workers=min(4, len(SOURCES))) as ex:
         objs = list(ex.map(compile_one, SOURCES))
     if force or not os.path.exists(lib) or os.path.getmtime(lib) < _newest(objs):

@@ -13,19 +13,20 @@ Semantics kept: candidate construction and order, duplicate-direction filters, t
 argmax of HV - alpha * sparsity with first-max tie breaking, virtual-EP updates, the global
 ``np.random`` draws of ``random_selection`` and of the 3-D candidate shuffle.
 
-Generation-boundary speed, results unchanged:
-  * the hyperbolic fits of all population members run over a spawn pool of CPU-only workers
-    (PGM_FIT_WORKERS, default min(15, CPUs - 1)), each the same least_squares call;
-  * 2-D greedy steps screen every candidate with one vectorised pass and re-score exactly (the
-    reference's own computation, strict > in index order) only those within a rounding bound of the
-    best, so the pick and its tie-breaking are the reference's;
-  * 3-D greedy steps score candidate chunks on the same pool (the reference forks one process per
+Generation-boundary path in C++ (libpgm_host.so, include/pgm_host.h):
+  * the soft-L1 hyperbolic fits of all population members run as one batch over the host's threads, a
+    restatement of scipy's bounded 'trf' least_squares (the reference's call, population_2d.py:106);
+  * the greedy knapsack (every round scores every candidate's virtual insertion: staircase HV / EP-order
+    sparsity in 2-D, update_ep + hypervolume + utils.compute_sparsity in 3-D, strict > in index order) runs
+    whole in one native call, the 3-D scoring threaded over candidates (the reference forks one process per
     candidate, population_3d.py:216-237).
+The Python here keeps the reference's candidate construction (test weights, np.random draws, the
+neighbourhood search) and the Population API.
 
 Deliberate differences (documented in DESIGN.md):
-  * The 3-D candidate evaluation uses vectorised numpy (update_ep, prefix-area hypervolume); the
-    order of float summation inside the hypervolume differs from InnerHyperVolume's (it is rounded
-    to 4 dp like hypervolume.py:74).
+  * The 3-D hypervolume sums slabs in an order of its own (rounded to 4 dp like hypervolume.py:74).
+  * Fits agree with scipy's to ~1e-9 when they converge; fits that exhaust max_nfev (ill-conditioned,
+    e.g. a slope at its bound) may stop at a slightly different point (tests/test_host_native.py).
   * The 2-D neighbourhood search (population_2d.py:37-54) has no exit when fewer than four
     distinct weights are reachable and spins forever; here it stops once a larger threshold
     cannot add any node.  When no node is reachable at all (the reference raises inside
@@ -36,9 +37,8 @@ Deliberate differences (documented in DESIGN.md):
 from copy import deepcopy
 
 import numpy as np
-from scipy.optimize import least_squares
 
-from .pareto import compute_sparsity as _sparsity_sorted
+from . import _host
 from .pareto import get_ep_indices, weight_grid
 
 # --------------------------------------------------------------------------- prediction model
@@ -88,12 +88,12 @@ def _hyperbolic(x, A, a, b, c):
     return A * (e - 1) / (e + 1) + c
 
 
-def predict_hyperbolic(args, opt_graph, optgraph_id, test_weights, bounded_search=False, objs_arr=None):
-    """population_2d.py:27-118 (bounded_search=False) / population_3d.py:23-112 (True, which adds
-    the ``threshold >= 1.0`` exit of population_3d.py:46)."""
+def _fit_inputs(args, opt_graph, optgraph_id, test_weights, bounded_search, objs_arr):
+    """population_2d.py:27-104 / population_3d.py:23-97 up to the fits: the widening neighbourhood search, the
+    Gaussian distance weights and one (x, y, w, A upper bound) fit problem per objective.  Returns
+    (original objs, sum-normalised test weights, problems or None when no node is reachable)."""
     test_weights = np.array(test_weights, dtype=np.float64)
     test_weights = test_weights / test_weights.sum(axis=1, keepdims=True)
-    objs_arr = np.asarray(opt_graph.objs, dtype=np.float64) if objs_arr is None else objs_arr
     threshold, sigma = 0.1, 0.03
     t_max = None if bounded_search else _max_useful_threshold(opt_graph, optgraph_id, objs_arr)
     while True:
@@ -106,245 +106,45 @@ def predict_hyperbolic(args, opt_graph, optgraph_id, test_weights, bounded_searc
             break
         threshold *= 2.0
         sigma *= 2.0
-
     original = np.asarray(opt_graph.objs[optgraph_id], dtype=np.float64)
     if len(objs_data) == 0:
-        return {'sample_index': optgraph_id, 'predictions': [original.copy() for _ in range(len(test_weights))]}
-
+        return original, test_weights, None
     objs_data = np.array(objs_data, dtype=np.float64)
     weights_data = np.array(weights_data, dtype=np.float64)
     delta_objs_data = np.array(delta_objs_data, dtype=np.float64)
     dist = np.linalg.norm(np.abs(objs_data - original) / np.abs(original), axis=1)
     w = np.exp(-((dist / sigma) ** 2) / 2.0)
-
-    def fun(p, x, y):
-        return (_hyperbolic(x, *p) - y) * w
-
-    def jac(p, x, y):
-        A, a, b, _ = p
-        e = np.exp(a * (x - b))
-        J = np.empty((4, len(x)))
-        J[0] = (e - 1) / (e + 1) * w
-        J[1] = A * (x - b) * (2. * e) / ((e + 1) ** 2) * w
-        J[2] = A * (-a) * (2. * e) / ((e + 1) ** 2) * w
-        J[3] = w
-        return J.T
-
-    deltas = []
+    problems = []
     for dim in range(args.obj_num):
         x, y = weights_data[:, dim], delta_objs_data[:, dim]
-        a_hi = np.clip(np.max(y) - np.min(y), 1.0, 500.0)
-        res = least_squares(fun, np.ones(4), loss='soft_l1', f_scale=20., args=(x, y), jac=jac,
-                            bounds=([0, 0.1, -5., -500.], [a_hi, 20., 5., 500.]))
-        deltas.append(_hyperbolic(test_weights.T[dim], *res.x))
-    deltas = np.array(deltas).T
-    return {'sample_index': optgraph_id, 'predictions': [original + deltas[i] for i in range(len(test_weights))]}
+        problems.append((x, y, w, float(np.clip(np.max(y) - np.min(y), 1.0, 500.0))))
+    return original, test_weights, problems
 
 
-def _predict_chunk(payload):
-    """Pool worker: predict_hyperbolic for a chunk of (node, test weights) jobs on a snapshot of the graph."""
-    args_d, graph, jobs, bounded = payload
-    import argparse
-    args = argparse.Namespace(**args_d)
-    og = _GraphView(*graph)
-    objs_arr = np.asarray(og.objs, dtype=np.float64)
-    return [predict_hyperbolic(args, og, node, tw, bounded_search=bounded, objs_arr=objs_arr) for node, tw in jobs]
-
-
-class _GraphView:
-    """The fields of an OptGraph that predict_hyperbolic reads (picklable snapshot for the fit workers)."""
-
-    def __init__(self, weights, objs, delta_objs, succ):
-        self.weights, self.objs, self.delta_objs, self.succ = weights, objs, delta_objs, succ
-
-
-_POOL = None
-
-
-def _fit_pool():
-    """Lazily started spawn pool for the hyperbolic fits (CPU-only workers: numpy / scipy, no GPU runtime).
-    Size: PGM_FIT_WORKERS, default min(15, usable CPUs - 1); 0 or 1 disables it."""
-    global _POOL
-    import os
-    n = int(os.environ.get('PGM_FIT_WORKERS', min(15, max(1, len(os.sched_getaffinity(0)) - 1))))
-    if n <= 1:
-        return None
-    if _POOL is None:
-        import multiprocessing as mp
-        import sys
-        import types
-        # workers start from a bare __main__ (not the caller's script, which may import torch and open the
-        # GPU) with no device visible: CPU-only processes
-        saved_main = sys.modules['__main__']
-        saved_env = {k: os.environ.get(k) for k in ('HIP_VISIBLE_DEVICES', 'ROCR_VISIBLE_DEVICES')}
-        sys.modules['__main__'] = types.ModuleType('__main__')
-        os.environ['HIP_VISIBLE_DEVICES'] = os.environ['ROCR_VISIBLE_DEVICES'] = ''
-        try:
-            _POOL = mp.get_context('spawn').Pool(n)
-        finally:
-            sys.modules['__main__'] = saved_main
-            for k, v in saved_env.items():
-                if v is None:
-                    os.environ.pop(k, None)
-                else:
-                    os.environ[k] = v
-    return _POOL
-
-
-def predict_all(args, opt_graph, jobs, bounded_search, min_parallel=16):
-    """predict_hyperbolic for every (node, test_weights) job, in order: in-process for few jobs, else chunked
-    over the fit pool (each chunk carries one snapshot of the graph)."""
-    pool = _fit_pool() if len(jobs) >= min_parallel else None
-    if pool is None:
-        objs_arr = np.asarray(opt_graph.objs, dtype=np.float64)
-        return [predict_hyperbolic(args, opt_graph, node, tw, bounded_search=bounded_search, objs_arr=objs_arr)
-                for node, tw in jobs]
-    graph = (list(opt_graph.weights), list(opt_graph.objs), list(opt_graph.delta_objs), [list(x) for x in opt_graph.succ])
-    args_d = {'obj_num': args.obj_num}
-    nch = min(len(jobs), 4 * pool._processes)
-    chunks = [jobs[i::nch] for i in range(nch)]  # strided chunks balance cheap and expensive fits
-    outs = pool.map(_predict_chunk, [(args_d, graph, ch, bounded_search) for ch in chunks])
-    res = [None] * len(jobs)
-    for i, out in enumerate(outs):
-        res[i::nch] = out
-    return res
-
-
-def _screen_2d(ep, preds, alpha):
-    """Vectorised HV - alpha * sparsity of (virtual EP + candidate) for every candidate (2 objectives), in a
-    float order of its own (screening only: see Population2d._best_candidate).  Returns (scores, magnitude
-    of the summed terms) for the rounding bound."""
-    C, n = len(preds), len(ep)
-    x0, x1 = preds[:, 0], preds[:, 1]
-    if n:
-        q0, q1 = ep[:, 0], ep[:, 1]
-        dom_by_x = (x0[:, None] >= q0[None]) & (x1[:, None] >= q1[None]) & \
-                   ((x0[:, None] > q0[None]) | (x1[:, None] > q1[None]))       # [C, n] EP point dropped
-        x_dom = ((q0[None] >= x0[:, None]) & (q1[None] >= x1[:, None]) &
-                 ((q0[None] > x0[:, None]) | (q1[None] > x1[:, None]))).any(1)  # candidate dropped
-    else:
-        dom_by_x = np.zeros((C, 0), dtype=bool)
-        x_dom = np.zeros(C, dtype=bool)
-    x_keep = ~x_dom & (x0 >= 0) & (x1 >= 0)
-    # merged sequence per candidate: EP points (already obj0-ascending) with the candidate at its slot
-    pos = np.searchsorted(ep[:, 0], x0, side='left') if n else np.zeros(C, dtype=int)
-    j = np.arange(n + 1)[None, :]
-    src = np.where(j < pos[:, None], j, j - 1)
-    is_x = j == pos[:, None]
-    src_c = np.clip(src, 0, max(n - 1, 0))
-    p0 = np.where(is_x, x0[:, None], ep[src_c, 0] if n else 0.0)
-    p1 = np.where(is_x, x1[:, None], ep[src_c, 1] if n else 0.0)
-    keep = np.where(is_x, x_keep[:, None], ~np.take_along_axis(np.pad(dom_by_x, ((0, 0), (0, 1))), src_c, 1)
-                    if n else False)
-    # staircase HV: (x_i - x_prev) * y_i over kept points, x_prev the previous kept x (ascending)
-    kx = np.where(keep, np.maximum(p0, 0.0), 0.0)
-    prev = np.concatenate([np.zeros((C, 1)), np.maximum.accumulate(kx, axis=1)[:, :-1]], 1)
-    terms = np.where(keep, (kx - prev) * np.maximum(p1, 0.0), 0.0)
-    hv = terms.sum(1)
-    # EP-order sparsity: squared steps between consecutive kept points
-    big = np.where(keep, p0, np.nan)
-    last0 = _ffill(big)
-    last1 = _ffill(np.where(keep, p1, np.nan))
-    d0 = p0 - np.concatenate([np.full((C, 1), np.nan), last0[:, :-1]], 1)
-    d1 = p1 - np.concatenate([np.full((C, 1), np.nan), last1[:, :-1]], 1)
-    step = np.where(keep & ~np.isnan(d0), d0 * d0 + d1 * d1, 0.0)
-    cnt = keep.sum(1)
-    sp = np.where(cnt >= 2, step.sum(1) / np.maximum(cnt - 1, 1), 0.0)
-    mag = np.abs(terms).sum(1) + alpha * np.abs(step).sum(1) / np.maximum(cnt - 1, 1)
-    return hv - alpha * sp, mag
-
-
-def _ffill(a):
-    """Forward-fill NaNs along axis 1."""
-    idx = np.where(~np.isnan(a), np.arange(a.shape[1])[None, :], 0)
-    np.maximum.accumulate(idx, axis=1, out=idx)
-    out = np.take_along_axis(a, idx, 1)
+def predict_all(args, opt_graph, jobs, bounded_search):
+    """predict_hyperbolic for every (node, test_weights) job, in order.  The per-objective soft-L1 fits of all
+    jobs (population_2d.py:105-113: least_squares(fun, ones(4), loss='soft_l1', f_scale=20, jac=jac,
+    bounds=([0, .1, -5, -500], [A_hi, 20, 5, 500]))) run as ONE batch in libpgm_host.so (a C++ restatement of
+    scipy's bounded 'trf' with the exact trust-region solver, over the host's threads)."""
+    objs_arr = np.asarray(opt_graph.objs, dtype=np.float64)
+    prep = [_fit_inputs(args, opt_graph, node, tw, bounded_search, objs_arr) for node, tw in jobs]
+    problems = [p for _, _, probs in prep if probs is not None for p in probs]
+    params = _host.fit_hyperbolic(problems) if problems else np.zeros((0, 4))
+    out, k = [], 0
+    for (node, _), (original, tw, probs) in zip(jobs, prep):
+        if probs is None:  # nothing reachable: the prediction is the unchanged objective vector
+            out.append({'sample_index': node, 'predictions': [original.copy() for _ in range(len(tw))]})
+            continue
+        deltas = np.array([_hyperbolic(tw.T[dim], *params[k + dim]) for dim in range(args.obj_num)]).T
+        k += args.obj_num
+        out.append({'sample_index': node, 'predictions': [original + deltas[i] for i in range(len(tw))]})
     return out
 
 
-# --------------------------------------------------------------------------- virtual EP metrics
-
-
-def update_ep(ep_objs_batch, new_objs):
-    """morl/utils.py:41-66, vectorised: drop EP points weakly dominated by ``new_objs``; insert it
-    (before the first point with a larger obj0) unless an EP point beats it by more than 1e-5."""
-    new_objs = np.asarray(new_objs, dtype=np.float64)
-    ep = np.asarray(ep_objs_batch, dtype=np.float64).reshape(-1, len(new_objs))
-    if (new_objs < 0).any():
-        return ep.copy()
-    keep = ~(new_objs >= ep).all(axis=1)
-    beaten = ((ep >= new_objs - 1e-5).all(axis=1) & (ep > new_objs + 1e-5).any(axis=1)).any()
-    out = ep[keep]
-    if beaten:
-        return out
-    larger = np.nonzero(new_objs[0] < out[:, 0])[0]
-    pos = int(larger[0]) if len(larger) else len(out)
-    return np.insert(out, pos, new_objs, axis=0)
-
-
-def hypervolume_nd(front):
-    """Dominated volume w.r.t. the origin, rounded to 4 dp (morl/hypervolume.py:41-74 semantics:
-    points with a negative coordinate do not count).  Slices along the last objective; each slice's
-    area is computed for all prefixes at once as a masked running maximum over a global ordering."""
-    f = np.asarray(front, dtype=np.float64)
-    if f.size == 0:
-        return 0.0
-    f = f[(f >= 0).all(axis=1)]
-    if len(f) == 0:
-        return 0.0
-    if f.shape[1] == 1:
-        return round(float(f[:, 0].max()), 4)
-    if f.shape[1] == 2:
-        return round(_area_prefixes(f[:, :1], f[:, 1:2].T, np.ones((1, len(f)), bool))[0], 4)
-    if f.shape[1] != 3:
-        from .pareto import compute_hypervolume
-        return compute_hypervolume(f)
-    order = np.argsort(-f[:, 2], kind='stable')
-    f = f[order]
-    n = len(f)
-    inc = np.tri(n, dtype=bool)                        # prefix i holds points 0..i (z descending)
-    areas = _area_prefixes(f[:, :1], np.broadcast_to(f[:, 1], (n, n)), inc)
-    z = f[:, 2]
-    dz = z - np.append(z[1:], 0.0)
-    return round(float(np.dot(areas, dz)), 4)
-
-
-def _area_prefixes(x, y, inc):
-    """Area of the union of boxes [0, x_j] x [0, y_j] over each row's included points."""
-    xs = x[:, 0]
-    o = np.argsort(-xs, kind='stable')
-    dx = xs[o] - np.append(xs[o][1:], 0.0)
-    h = np.where(inc[:, o], y[:, o], 0.0)
-    return (np.maximum.accumulate(h, axis=1) * dx).sum(axis=1)
-
-
-def _hv_2d_staircase(ep_objs):
-    """population_2d.py:185-192: staircase over the EP (ascending obj0), reference point (0, 0)."""
-    hv, x = 0.0, 0.0
-    for o in ep_objs:
-        hv += (max(0.0, o[0]) - x) * (max(0.0, o[1]) - 0.0)
-        x = max(0.0, o[0])
-    return hv
-
-
-def _sparsity_ep_order(ep_objs):
-    """population_2d.py:194-202: mean squared step between consecutive EP points."""
-    if len(ep_objs) < 2:
-        return 0.0
-    return float(np.sum(np.square(np.diff(ep_objs, axis=0)))) / (len(ep_objs) - 1)
-
-
-def _evaluate_3d(virtual_ep, pred):
-    """population_3d.py:216-237 per candidate: update_ep, then hypervolume and sparsity of the new front."""
-    e = update_ep(virtual_ep, pred)
-    if len(e) == 0:
-        return 0.0, 0.0
-    return hypervolume_nd(e), _sparsity_sorted(e)
-
-
-def _score_chunk_3d(payload):
-    virtual_ep, preds = payload
-    return np.array([_evaluate_3d(virtual_ep, x) for x in preds], dtype=np.float64).reshape(-1, 2)
+def predict_hyperbolic(args, opt_graph, optgraph_id, test_weights, bounded_search=False):
+    """population_2d.py:27-118 (bounded_search=False) / population_3d.py:23-112 (True, which adds the
+    ``threshold >= 1.0`` exit of population_3d.py:46)."""
+    return predict_all(args, opt_graph, [(optgraph_id, test_weights)], bounded_search)[0]
 
 
 # --------------------------------------------------------------------------- populations
@@ -415,47 +215,32 @@ class _PopulationBase:
             test_weights = self._test_weights(args, opt_graph, sample.optgraph_id)
             if len(test_weights) > 0:
                 jobs.append((sample, test_weights))
-        # the hyperbolic fits of every population member: independent small least-squares problems, fanned
-        # out over a process pool when there are many (the reference forks per candidate in 3-D,
-        # population_3d.py:216-237); results are the same function's, in job order
+        # the hyperbolic fits of every population member: independent small least-squares problems, one
+        # native batch (the reference fits them one after another)
         preds = predict_all(args, opt_graph, [(s.optgraph_id, tw) for s, tw in jobs], self.bounded_search)
         for (sample, test_weights), res in zip(jobs, preds):
             for w, pred in zip(test_weights, res['predictions']):
                 candidates.append({'sample': sample, 'weight': w, 'prediction': pred})
 
         virtual_ep = np.array([np.asarray(s.objs, dtype=np.float64) for s in ep.sample_batch]).reshape(-1, args.obj_num)
-        mask = np.ones(len(candidates), dtype=bool)
-        predicted_offspring_objs, elite_batch, scalarization_batch = [], [], []
-        alpha = args.sparsity
         pred_arr = np.array([c['prediction'] for c in candidates], dtype=np.float64).reshape(-1, args.obj_num)
-        for _ in range(args.num_tasks):
-            best_id = self._best_candidate(virtual_ep, pred_arr, mask, alpha)
-            if best_id == -1:
-                print('Too few candidates')
-                break
+        picks = _host.select_greedy(virtual_ep, pred_arr, args.sparsity, args.num_tasks, self.select_mode)
+        if len(picks) < args.num_tasks:
+            print('Too few candidates')
+        predicted_offspring_objs, elite_batch, scalarization_batch = [], [], []
+        for best_id in picks:
             c = candidates[best_id]
             elite_batch.append(c['sample'])
             sc = deepcopy(scalarization_template)
             sc.update_weights(c['weight'] / np.sum(c['weight']))
             scalarization_batch.append(sc)
-            mask[best_id] = False
-            virtual_ep = self._virtual_insert(virtual_ep, c['prediction'])
             predicted_offspring_objs.append(np.array(c['prediction'], dtype=np.float64))
         return elite_batch, scalarization_batch, predicted_offspring_objs
-
-    def _best_candidate(self, virtual_ep, preds, mask, alpha):
-        """First index of the maximum of HV - alpha * sparsity over the unmasked candidates (strict > scan in
-        index order, population_2d.py:276-292), or -1."""
-        best_id, best = -1, -np.inf
-        for i in np.nonzero(mask)[0]:
-            hv, sp = self._evaluate(virtual_ep, preds[i])
-            if hv - alpha * sp > best:
-                best, best_id = hv - alpha * sp, int(i)
-        return best_id
 
 
 class Population2d(_PopulationBase):
     """morl/population_2d.py:123-319."""
+    select_mode = _host.STAIRCASE
 
     def __init__(self, args):
         self.pbuffer_num = args.pbuffer_num
@@ -491,44 +276,30 @@ class Population2d(_PopulationBase):
         return out
 
     def compute_hypervolume(self, objs_batch):
+        """population_2d.py:185-192: staircase over the EP (ascending obj0), reference point (0, 0)."""
         objs = np.asarray(objs_batch, dtype=np.float64)
-        return _hv_2d_staircase(objs[get_ep_indices(objs)])
+        hv, x = 0.0, 0.0
+        for o in objs[get_ep_indices(objs)]:
+            hv += (max(0.0, o[0]) - x) * (max(0.0, o[1]) - 0.0)
+            x = max(0.0, o[0])
+        return hv
 
     def compute_sparsity(self, objs_batch):
+        """population_2d.py:194-202: mean squared step between consecutive EP points."""
         objs = np.asarray(objs_batch, dtype=np.float64)
-        return _sparsity_ep_order(objs[get_ep_indices(objs)])
-
-    def _evaluate(self, virtual_ep, pred):
-        new = np.vstack([virtual_ep, np.asarray(pred, dtype=np.float64)[None]])
-        e = new[get_ep_indices(new)]
-        return _hv_2d_staircase(e), _sparsity_ep_order(e)
-
-    def _best_candidate(self, virtual_ep, preds, mask, alpha):
-        """Same result as the exact scan, fast: every candidate's score is first computed vectorised (the new
-        front = virtual EP minus the points the candidate dominates, plus the candidate, in obj0 order) with a
-        different float summation order; only the candidates within a rounding bound of the best screened
-        score are then re-scored with the exact reference computation, scanned in index order with the strict
-        > of the reference.  A candidate outside the bound scores below the best exactly, so the pick and
-        its first-max tie-breaking are the reference's."""
-        idx = np.nonzero(mask)[0]
-        if len(idx) == 0:
-            return -1
-        score, mag = _screen_2d(virtual_ep, preds[idx], alpha)
-        if np.isnan(score).all():  # every score NaN: no strict > ever holds (population_2d.py:286)
-            return -1
-        top = np.nanmax(score)
-        tol = 1e-9 * (np.max(mag) + 1.0)
-        near = idx[score >= top - 2.0 * tol]
-        return _PopulationBase._best_candidate(self, virtual_ep, preds, np.isin(np.arange(len(preds)), near), alpha)
-
-    def _virtual_insert(self, virtual_ep, pred):
-        new = np.vstack([virtual_ep, np.asarray(pred, dtype=np.float64)[None]])
-        return new[get_ep_indices(new)]
+        e = objs[get_ep_indices(objs)]
+        if len(e) < 2:
+            return 0.0
+        sp = 0.0
+        for i in range(1, len(e)):
+            sp += np.sum(np.square(e[i] - e[i - 1]))
+        return sp / (len(e) - 1)
 
 
 class Population3d(_PopulationBase):
     """morl/population_3d.py:120-345."""
     bounded_search = True
+    select_mode = _host.UPDATE_EP
 
     def __init__(self, args):
         vec = weight_grid(args.obj_num, 1.0 / (args.pbuffer_num - 1))
@@ -570,33 +341,6 @@ class Population3d(_PopulationBase):
             if angle < np.pi / 4.0 and not any(np.linalg.norm(s - w) < 1e-3 for s in succ_w):
                 out.append(w)
         return out
-
-    def _evaluate(self, virtual_ep, pred):
-        return _evaluate_3d(virtual_ep, pred)
-
-    def _best_candidate(self, virtual_ep, preds, mask, alpha):
-        """The exact per-candidate scores, computed over the fit pool in chunks when there are many (the
-        reference forks one process per candidate, population_3d.py:216-237); the strict > scan in index order
-        then runs here on the returned (identical) values."""
-        idx = np.nonzero(mask)[0]
-        pool = _fit_pool() if len(idx) >= 64 else None
-        if pool is None:
-            return _PopulationBase._best_candidate(self, virtual_ep, preds, mask, alpha)
-        nch = min(len(idx), 4 * pool._processes)
-        chunks = [idx[i::nch] for i in range(nch)]
-        outs = pool.map(_score_chunk_3d, [(virtual_ep, preds[ch]) for ch in chunks])
-        hv = np.empty(len(preds))
-        sp = np.empty(len(preds))
-        for ch, out in zip(chunks, outs):
-            hv[ch], sp[ch] = out[:, 0], out[:, 1]
-        best_id, best = -1, -np.inf
-        for i in idx:
-            if hv[i] - alpha * sp[i] > best:
-                best, best_id = hv[i] - alpha * sp[i], int(i)
-        return best_id
-
-    def _virtual_insert(self, virtual_ep, pred):
-        return update_ep(virtual_ep, pred)
 
 
 def make_population(args):

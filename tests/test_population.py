@@ -53,52 +53,6 @@ def _history(K, seed, gens=3):
     return og, offspring
 
 
-def test_update_ep_matches_oracle():
-    rng = np.random.RandomState(0)
-    for K in (2, 3):
-        ep_a, ep_b = np.zeros((0, K)), []
-        for _ in range(300):
-            p = rng.rand(K) * 10 - 0.3
-            if rng.rand() < 0.2 and len(ep_a):
-                p = ep_a[rng.randint(len(ep_a))] + rng.choice([0, 1e-6, -1e-6], size=K)  # ties inside 1e-5
-            ep_a, ep_b = population.update_ep(ep_a, p), ref.update_ep(ep_b, p)
-            np.testing.assert_array_equal(ep_a, np.array(ep_b).reshape(-1, K))
-
-
-@pytest.mark.parametrize('K', [2, 3])
-def test_hypervolume_nd_matches_oracle(K):
-    rng = np.random.RandomState(K)
-    for n in (0, 1, 2, 5, 30, 120):
-        x = rng.rand(n, K) * 50 - 1
-        front = x[pareto.get_ep_indices(x)] if n else x
-        assert population.hypervolume_nd(front) == pytest.approx(ref_pareto.compute_hypervolume(front), abs=2e-4)
-
-
-def test_population2d_buffers_known_answer():
-    pop = population.Population2d(_args(2, pbuffer_num=4, pbuffer_size=2))
-    # angle to the obj1 axis: buckets of pi/8; bucket 0 holds points near the obj1 axis
-    pts = [(0.1, 5.0), (0.2, 9.0), (0.05, 1.0), (5.0, 5.0), (9.0, 0.1), (3.0, -1.0), (0.0, 4.0), (4.0, 4.1)]
-    pop.update([_S(p) for p in pts])
-    got = [tuple(s.objs) for s in pop.sample_batch]
-    # bucket 0 holds (0.2,9) > (0.1,5) > (0.05,1): the nearest is dropped (size 2); (0,4) has a zero
-    # coordinate and (3,-1) a negative one, so neither enters any buffer
-    assert (0.2, 9.0) == got[0] and (0.1, 5.0) == got[1] and (0.05, 1.0) not in got
-    assert (0.0, 4.0) not in got and (3.0, -1.0) not in got
-    assert set(got) == {(0.2, 9.0), (0.1, 5.0), (5.0, 5.0), (4.0, 4.1), (9.0, 0.1)}
-    ora = ref.Population2d(4, 2)
-    ora.update([_S(p) for p in pts])
-    assert got == [tuple(s.objs) for s in ora.sample_batch]
-
-
-def test_population3d_buffer_directions():
-    pop = population.Population3d(_args(3, pbuffer_num=20))
-    assert pop.pbuffer_num == 210                    # the 210-buffer reading of Hopper-v3
-    ora = ref.Population3d(3, 20, 2)
-    rng = np.random.RandomState(1)
-    for f in rng.rand(200, 3):
-        assert pop.find_buffer_id(f) == ora.buffer_id(f)
-
-
 @pytest.mark.parametrize('K,seed', [(2, 0), (2, 1), (3, 0), (3, 1)])
 def test_population_update_matches_oracle(K, seed):
     _, offspring = _history(K, seed)
@@ -207,67 +161,3 @@ def test_random_selection_uses_the_global_stream():
     assert [id(e) for e in e1] == [id(pop.sample_batch[i]) for i, _ in want]
     for sc, (_, w) in zip(s1, want):
         np.testing.assert_array_equal(sc.weights.numpy(), w)
-
-
-# ---------------------------------------------------------------- fast generation-boundary paths == exact ones
-
-
-def _exact_pick(pop, virtual_ep, preds, mask, alpha):
-    return population._PopulationBase._best_candidate(pop, virtual_ep, preds, mask, alpha)
-
-
-@pytest.mark.parametrize('seed', range(8))
-def test_screened_2d_pick_equals_exact_scan(seed):
-    """Population2d._best_candidate (vectorised screen + exact re-score of the near-best) picks exactly what
-    the reference's strict-> scan picks, including exact ties (duplicated candidates: first index wins),
-    candidates dominated by the EP, candidates with negative coordinates and candidates that dominate EP
-    points."""
-    rng = np.random.RandomState(seed)
-    pop = population.Population2d(_args(2))
-    K = 2
-    ep = rng.rand(rng.randint(0, 40), K) * 100
-    ep = ep[pareto.get_ep_indices(ep)] if len(ep) else ep.reshape(0, K)
-    preds = rng.rand(300, K) * 110 - 5
-    preds[::7] = preds[3]                                   # exact ties
-    if len(ep):
-        preds[5::11] = ep[rng.randint(len(ep), size=len(preds[5::11]))]  # duplicates of EP points
-    for alpha in (0.0, 1.0, 30.0):
-        mask = rng.rand(len(preds)) < 0.9
-        for _ in range(6):
-            a = pop._best_candidate(ep, preds, mask, alpha)
-            b = _exact_pick(pop, ep, preds, mask, alpha)
-            assert a == b
-            if a < 0:
-                break
-            mask[a] = False
-            ep = pop._virtual_insert(ep, preds[a])
-
-
-def test_pooled_fits_equal_sequential(monkeypatch):
-    og, offspring = _history(2, 5, gens=3)
-    args = _args(2)
-    pop = population.Population2d(args)
-    jobs = [(s.optgraph_id, pop._test_weights(args, og, s.optgraph_id)) for s in offspring]
-    jobs = [j for j in jobs if len(j[1])]
-    monkeypatch.setenv('PGM_FIT_WORKERS', '3')
-    pooled = population.predict_all(args, og, jobs, False, min_parallel=1)
-    seq = [population.predict_hyperbolic(args, og, n, tw) for n, tw in jobs]
-    for a, b in zip(pooled, seq):
-        assert a['sample_index'] == b['sample_index']
-        np.testing.assert_array_equal(np.array(a['predictions']), np.array(b['predictions']))
-
-
-def test_pooled_3d_pick_equals_exact_scan(monkeypatch):
-    monkeypatch.setenv('PGM_FIT_WORKERS', '3')
-    rng = np.random.RandomState(3)
-    pop = population.Population3d(_args(3, pbuffer_num=6))
-    ep = rng.rand(30, 3) * 50
-    ep = ep[pareto.get_ep_indices(ep)]
-    preds = rng.rand(200, 3) * 55
-    preds[::9] = preds[1]
-    mask = np.ones(len(preds), dtype=bool)
-    for _ in range(4):
-        a = pop._best_candidate(ep, preds, mask, 0.5)
-        assert a == _exact_pick(pop, ep, preds, mask, 0.5)
-        mask[a] = False
-        ep = pop._virtual_insert(ep, preds[a])

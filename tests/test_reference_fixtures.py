@@ -196,8 +196,7 @@ class _ForkPopulation2d(Population2d):
     """The fork's two selection changes (WorkingMorl/morl/population_2d.py vs morl/population_2d.py):
     bounded neighbourhood search and update_ep-based hypervolume / sparsity scoring."""
     bounded_search = True
-    _evaluate = Population3d._evaluate
-    _virtual_insert = Population3d._virtual_insert
+    select_mode = Population3d.select_mode
 
 
 def test_prediction_guided_selection_first_picks():

@@ -10,9 +10,12 @@ Semantics follow the reference exactly (bit-exact EP membership and order):
   * hypervolume w.r.t. the origin (maximisation), rounded to 4 dp      -- morl/hypervolume.py:41-74
   * sparsity                                                           -- morl/utils.py:87-100
 The dominance test is an O(n log n) sort-and-sweep for two objectives (exact: the same boolean predicate)
-and chunked [n, chunk] comparisons for more, instead of the reference's per-point O(n^2) loop.
+and the native pairwise test (libpgm_host.so pgm_ep_mask) for more, instead of the reference's per-point
+Python loop.
 """
 import numpy as np
+
+from . import _host
 
 
 def _dominated_2d(objs):
@@ -34,23 +37,14 @@ def _dominated_2d(objs):
     return dom
 
 
-def _dominated_nd(objs, chunk=512):
-    n = len(objs)
-    dom = np.zeros(n, dtype=bool)
-    for i0 in range(0, n, chunk):  # [n, chunk] comparisons at a time (bounded memory)
-        blk = objs[i0:i0 + chunk]
-        ge = (objs[:, None, :] >= blk[None, :, :]).all(-1)  # ge[j, i]: j >= i everywhere
-        gt = (objs[:, None, :] > blk[None, :, :]).any(-1)
-        dom[i0:i0 + chunk] = (ge & gt).any(0)
-    return dom
-
-
 def get_ep_indices(obj_batch_input):
     if len(obj_batch_input) == 0:
         return np.array([])
     objs = np.asarray(obj_batch_input, dtype=np.float64)
-    dominated = _dominated_2d(objs) if objs.shape[1] == 2 and not np.isnan(objs).any() else _dominated_nd(objs)
-    keep = (objs >= 0).all(1) & ~dominated
+    if objs.shape[1] == 2 and not np.isnan(objs).any():
+        keep = (objs >= 0).all(1) & ~_dominated_2d(objs)
+    else:  # libpgm_host.so pgm_ep_mask: the reference's pairwise predicate in C++
+        keep = _host.ep_mask(objs)
     order = np.argsort(objs.T[0])
     return [int(i) for i in order if keep[i]]
 

@@ -889,7 +889,7 @@ __device__ __forceinline__ float group4_sum(float v) {
     return v + __shfl_xor(v, 16, 64);                              // l ^ 16
 }
 
-template <int O, int A, int K, int W, int NBUF>
+template <int O, int A, int K, int W, int NBUF, int NIMG_>
 struct T16SmemT {
     static constexpr int Q = qmax<A, K>();
     static constexpr int IMG = img_floats<O, A, K>();
@@ -903,19 +903,27 @@ struct T16SmemT {
     float dout[W][T16][DQS];                // per-wave dL/d(head output), transposed for dH2
     float aiv[A];                           // actor 1 / std^2
     float red[32];
-    static constexpr int NIMG = W == 4 ? 2 : 1;  // W = 4: wave pairs (0,1) and (2,3) fill one image each
+    static constexpr int NIMG = NIMG_;  // 2: waves [0, W/2) and [W/2, W) fill one image each
     static constexpr int IMGP = (IMG + 3) & ~3;  // image stride: every image 16-B aligned (float4 / LDS-DMA)
     union alignas(16) Big {
         float scr[W][T16][S16];             // transpose tiles during the passes
         float GA[NIMG][IMGP];               // the workgroup's gradient image(s) after them
     } big;
 };
+// LDS plan: double-buffered staging first, then two gradient images (W >= 4), within the 160 KiB of a CU
 template <int O, int A, int K, int W>
-constexpr int t16_nbuf() { return sizeof(T16SmemT<O, A, K, W, 2>) <= 160 * 1024 ? 2 : 1; }
+constexpr int t16_nbuf() { return sizeof(T16SmemT<O, A, K, W, 2, 1>) <= 160 * 1024 ? 2 : 1; }
 template <int O, int A, int K, int W>
-using T16Smem = T16SmemT<O, A, K, W, t16_nbuf<O, A, K, W>()>;
+constexpr int t16_nimg() {
+    return W >= 4 && sizeof(T16SmemT<O, A, K, W, t16_nbuf<O, A, K, W>(), 2>) <= 160 * 1024 ? 2 : 1;
+}
+template <int O, int A, int K, int W>
+using T16Smem = T16SmemT<O, A, K, W, t16_nbuf<O, A, K, W>(), t16_nimg<O, A, K, W>()>;
 
-template <int O, int A, int K, int NS, int W>
+// ONE: the launcher checked mb == NS * W * 16 (every wave owns exactly one tile of one pass per minibatch), so
+// the pass and tile loops are straight-line and the gradient accumulators are no longer loop-carried: they go
+// live at their first MFMA instead of spanning the whole tile (W = 8: no spills)
+template <int O, int A, int K, int NS, int W, bool ONE>
 __global__ __launch_bounds__(64 * W) void ppo_update_t16_kernel(MArgs a) {
     static_assert(O <= 32, "two 16-feature blocks of layer-1 inputs");
     using Sm = T16Smem<O, A, K, W>;
@@ -1026,8 +1034,8 @@ __global__ __launch_bounds__(64 * W) void ppo_update_t16_kernel(MArgs a) {
                 gB1[i] = gB2[i] = 0.f;
             }
 
-            for (int s0 = 0; s0 < mbs; s0 += SBk, ++gp) {
-                const int ns = min(SBk, mbs - s0);
+            for (int s0 = 0; ONE ? s0 < 1 : s0 < mbs; s0 += (ONE ? 1 : SBk), ++gp) {
+                const int ns = ONE ? SBk : min(SBk, mbs - s0);
                 const int cur = NBUF == 2 ? (gp & 1) : 0;
                 if constexpr (NBUF == 2) {
                     if (gp + 1 < npass) issue_rows(cur ^ 1, (gp + 1) & 1);
@@ -1036,7 +1044,7 @@ __global__ __launch_bounds__(64 * W) void ppo_update_t16_kernel(MArgs a) {
                 const float* rb = &S.RB[cur][0];
                 PGM_STAMP(0);
 
-                for (int tile = w; tile * T16 < ns; tile += W) {
+                for (int tile = w; ONE ? tile < w + 1 : tile * T16 < ns; tile += (ONE ? 1 : W)) {
                     const int ts0 = tile * T16;
                     const float* rt = rb + ts0 * RSL;
                     // ---- layer 1: Z1[s][h] = X[s][:] . W1t[:][h]
@@ -1246,17 +1254,18 @@ __global__ __launch_bounds__(64 * W) void ppo_update_t16_kernel(MArgs a) {
             if (l == 0) S.red[8 + w] = lsum;
             PGM_STAMP(12);
 
-            // ---- the W waves' register partials -> the workgroup's image.  W = 4: the wave pairs (0,1), (2,3) fill
-            // images A, B in two rounds (round 0: wave 2i+h stores its half h of the blocks, round 1: it adds its
-            // other half), and the publish sums A + B -- every element is (w0 + w1) + (w2 + w3).  Otherwise W
-            // rounds on one image: in round j wave w owns slice (w + j) mod W (fixed wave order per element).
+            // ---- the W waves' register partials -> the workgroup's image.  The two wave halves fill images A, B in
+            // W/2 rounds each (round j: wave w owns slice (w mod W/2 + j) mod W/2 of its image, the first round
+            // stores, later rounds add: a fixed wave order per element), and the publish sums A + B.  W = 4: every
+            // element is (w0 + w1) + (w2 + w3).
             // Blocks: 0-15 dW2, 16-16+4 K1B dW1, then dWh, then the vectors (b1, b2, head bias, logstd).  The slice
             // is a compile-time parameter of the round body (a uniform branch picks it), so every (index, value)
             // pair is a register and a round's reads all issue before its writes.
             {
                 constexpr int BW1 = 16, BWH = 16 + 4 * K1B, BV = BWH + 4;
-                constexpr int NSL = Sm::NIMG == 2 ? 2 : W;  // slices = rounds
-                float* Gt = S.big.GA[Sm::NIMG == 2 ? (w >> 1) : 0];
+                constexpr int WPI = W / Sm::NIMG;  // waves per image
+                constexpr int NSL = WPI;            // slices = rounds
+                float* Gt = S.big.GA[w / WPI];
                 auto round = [&](auto slc, auto addc) {
                     constexpr int SL = decltype(slc)::value;
                     constexpr bool add = decltype(addc)::value != 0;
@@ -1304,7 +1313,7 @@ __global__ __launch_bounds__(64 * W) void ppo_update_t16_kernel(MArgs a) {
                     }
                 };
                 auto rounds = [&](int j, auto addc) {
-                    const int sl = Sm::NIMG == 2 ? ((w & 1) ^ j) : (w + j) % W;
+                    const int sl = (w % WPI + j) % WPI;
                     if constexpr (NSL == 2) {
                         if (sl == 0) round(ic<0>{}, addc);
                         else round(ic<1>{}, addc);
@@ -1624,8 +1633,8 @@ __global__ __launch_bounds__(64 * W) void ppo_update_t16_kernel(MArgs a) {
     }
 }
 
-template <int O, int A, int K, int NS, int W>
-int launch_t16(const pgm_dims* d, const MArgs& a, hipStream_t stream) {
+template <int O, int A, int K, int NS, int W, bool ONE>
+static int launch_t16_k(const pgm_dims* d, const MArgs& a, hipStream_t stream) {
     using Sm = T16Smem<O, A, K, W>;
     const size_t smem = sizeof(Sm);
     if (smem > 160 * 1024) {
@@ -1633,7 +1642,7 @@ int launch_t16(const pgm_dims* d, const MArgs& a, hipStream_t stream) {
         return PGM_E_UNSUPPORTED;
     }
     static_assert(sizeof(Sm) > 80 * 1024, "residency argument (one workgroup per CU) needs > 80 KiB LDS");
-    auto kern = ppo_update_t16_kernel<O, A, K, NS, W>;
+    auto kern = ppo_update_t16_kernel<O, A, K, NS, W, ONE>;
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update");
     e = hipMemsetAsync(a.ws, 0, ppo_flag_bytes(d->P) + ppo_xbuf_bytes(d, NS), stream);
@@ -1641,6 +1650,13 @@ int launch_t16(const pgm_dims* d, const MArgs& a, hipStream_t stream) {
     const int grid = 8 * NS * ((d->P + 3) / 4);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * W), smem, stream, a);
     return launch_status("pgm_ppo_update");
+}
+
+template <int O, int A, int K, int NS, int W>
+int launch_t16(const pgm_dims* d, const MArgs& a, hipStream_t stream) {
+    const int mb = d->T * d->N / a.hp.num_mini_batch;
+    if (mb == NS * W * T16) return launch_t16_k<O, A, K, NS, W, true>(d, a, stream);
+    return launch_t16_k<O, A, K, NS, W, false>(d, a, stream);
 }
 
 static int device_cus() { return device_cu_count(); }

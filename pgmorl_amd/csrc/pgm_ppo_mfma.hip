@@ -155,7 +155,9 @@ struct MArgs {
 // MODE 0: one workgroup per task (joint towers).  MODE 1 (SPLIT): one workgroup per tower.  MODE 2: each tower
 // on TWO workgroups that take one half of every minibatch's rows each and add their gradient images through
 // tagged granules (both compute half0 + half1 in that order, so their Adam steps stay bitwise identical).
-template <int O, int A, int K, int MODE>
+// ONE (MODE 2, mb = 256): every wave owns exactly one 32-row tile of one pass per minibatch; the pass and tile
+// loops are straight-line so the gradient accumulators are not loop-carried
+template <int O, int A, int K, int MODE, bool ONE>
 __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
     constexpr bool SPLIT = MODE >= 1;
     constexpr int NS = MODE == 2 ? 2 : 1;  // workgroups per tower
@@ -278,8 +280,8 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
             }
             float lsum = 0.f;
 
-            for (int s0 = 0; s0 < mbs; s0 += SBk, ++gp) {
-                const int ns = min(SBk, mbs - s0);
+            for (int s0 = 0; ONE ? s0 < 1 : s0 < mbs; s0 += (ONE ? 1 : SBk), ++gp) {
+                const int ns = ONE ? SBk : min(SBk, mbs - s0);
                 const int cur = NBUF == 2 ? (gp & 1) : 0;
                 if constexpr (NBUF == 2) {  // stage the next pass while this one computes
                     if (gp + 1 < npass) issue_rows(cur ^ 1, (gp + 1) & 1);
@@ -288,7 +290,7 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                 const float* rb = &S.RB[cur][0];
                 PGM_STAMP(0);
 
-                for (int tile = sh; tile * TS < ns; tile += NWT) {
+                for (int tile = sh; ONE ? tile < sh + 1 : tile * TS < ns; tile += (ONE ? 1 : NWT)) {
                     const int ts0 = tile * TS;
                     const float* rt = rb + ts0 * RSL;  // this tile's staged rows
                     // ---- layer 1: Z1[s][h] = X[s][:] . W1t[:][h]  (two independent accumulator chains
@@ -609,15 +611,33 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                 float* G0 = S.big.GA[0];
                 const float* G1 = S.big.GA[1];
                 const float lsum_wg = (S.red[8] + S.red[9]) + (S.red[10] + S.red[11]);
-                for (int i = t; i < NV4; i += MT) {
-                    u32x4 v;
+                // ONE (registers to spare): this half's summed image stays in registers, published from them and
+                // reused as the own term of the gather; otherwise written back to GA[0] and re-read there
+                float4 own4[ONE ? NG4 : 1];
+                if constexpr (ONE) {
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const float g = G0[4 * i + q] + G1[4 * i + q];
-                        G0[4 * i + q] = g;
-                        v[q] = __float_as_uint(g);
+                    for (int k = 0; k < NG4; ++k) {
+                        const int i = min(t + k * MT, NV4 - 1);
+                        const float4 a0 = *reinterpret_cast<const float4*>(&G0[4 * i]);
+                        const float4 a1 = *reinterpret_cast<const float4*>(&G1[4 * i]);
+                        own4[k] = make_float4(a0.x + a1.x, a0.y + a1.y, a0.z + a1.z, a0.w + a1.w);
+                        if (t + k * MT < NV4) {
+                            const u32x4 v = {__float_as_uint(own4[k].x), __float_as_uint(own4[k].y),
+                                             __float_as_uint(own4[k].z), __float_as_uint(own4[k].w)};
+                            __builtin_amdgcn_raw_buffer_store_b128(v, xr, off_mine + 16 * i, 0, SC1);
+                        }
                     }
-                    __builtin_amdgcn_raw_buffer_store_b128(v, xr, off_mine + 16 * i, 0, SC1);
+                } else {
+                    for (int i = t; i < NV4; i += MT) {
+                        u32x4 v;
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            const float g = G0[4 * i + q] + G1[4 * i + q];
+                            G0[4 * i + q] = g;
+                            v[q] = __float_as_uint(g);
+                        }
+                        __builtin_amdgcn_raw_buffer_store_b128(v, xr, off_mine + 16 * i, 0, SC1);
+                    }
                 }
                 if (t < TAIL) {
                     const float g = G0[4 * NV4 + t] + G1[4 * NV4 + t];
@@ -654,7 +674,7 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                 for (int k = 0; k < NG4; ++k) {
                     const int i = min(t + k * MT, NV4 - 1);
                     const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(xr, off_other + 16 * i, 0, SC1);
-                    const float4 mine = *reinterpret_cast<const float4*>(&G0[4 * i]);
+                    const float4 mine = ONE ? own4[ONE ? k : 0] : *reinterpret_cast<const float4*>(&G0[4 * i]);
                     const float mv[4] = {mine.x, mine.y, mine.z, mine.w};
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
@@ -1661,15 +1681,15 @@ int launch_t16(const pgm_dims* d, const MArgs& a, hipStream_t stream) {
 
 static int device_cus() { return device_cu_count(); }
 
-template <int O, int A, int K, int MODE>
-int launch_mode(const pgm_dims* d, const MArgs& a, hipStream_t stream) {
+template <int O, int A, int K, int MODE, bool ONE>
+int launch_mode_k(const pgm_dims* d, const MArgs& a, hipStream_t stream) {
     constexpr bool SPLIT = MODE >= 1;
     const size_t smem = sizeof(MSmem<O, A, K, SPLIT>);
     if (smem > 160 * 1024) {
         set_error("pgm_ppo_update: LDS image %zu bytes exceeds 160 KiB", smem);
         return PGM_E_UNSUPPORTED;
     }
-    auto kern = ppo_update_mfma_kernel<O, A, K, MODE>;
+    auto kern = ppo_update_mfma_kernel<O, A, K, MODE, ONE>;
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update");
     // norm granules, timeout flag (and MODE 2: the exchange slots) start at tag 0; MODE 0 resets the flag
@@ -1679,6 +1699,16 @@ int launch_mode(const pgm_dims* d, const MArgs& a, hipStream_t stream) {
     const int grid = MODE == 2 ? 16 * ((d->P + 3) / 4) : SPLIT ? 2 * d->P : d->P;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(MT), smem, stream, a);
     return launch_status("pgm_ppo_update");
+}
+
+template <int O, int A, int K, int MODE>
+int launch_mode(const pgm_dims* d, const MArgs& a, hipStream_t stream) {
+    using Sm = MSmem<O, A, K, true>;
+    if constexpr (MODE == 2) {  // 2 workgroups x 4 waves x one 32-row tile = the minibatch, in one pass
+        if (d->T * d->N / a.hp.num_mini_batch == 2 * 4 * TS && Sm::SBk >= 4 * TS)
+            return launch_mode_k<O, A, K, MODE, true>(d, a, stream);
+    }
+    return launch_mode_k<O, A, K, MODE, false>(d, a, stream);
 }
 
 template <int O, int A, int K>

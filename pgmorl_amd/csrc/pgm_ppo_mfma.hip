@@ -611,33 +611,15 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                 float* G0 = S.big.GA[0];
                 const float* G1 = S.big.GA[1];
                 const float lsum_wg = (S.red[8] + S.red[9]) + (S.red[10] + S.red[11]);
-                // ONE (registers to spare): this half's summed image stays in registers, published from them and
-                // reused as the own term of the gather; otherwise written back to GA[0] and re-read there
-                float4 own4[ONE ? NG4 : 1];
-                if constexpr (ONE) {
+                for (int i = t; i < NV4; i += MT) {
+                    u32x4 v;
 #pragma unroll
-                    for (int k = 0; k < NG4; ++k) {
-                        const int i = min(t + k * MT, NV4 - 1);
-                        const float4 a0 = *reinterpret_cast<const float4*>(&G0[4 * i]);
-                        const float4 a1 = *reinterpret_cast<const float4*>(&G1[4 * i]);
-                        own4[k] = make_float4(a0.x + a1.x, a0.y + a1.y, a0.z + a1.z, a0.w + a1.w);
-                        if (t + k * MT < NV4) {
-                            const u32x4 v = {__float_as_uint(own4[k].x), __float_as_uint(own4[k].y),
-                                             __float_as_uint(own4[k].z), __float_as_uint(own4[k].w)};
-                            __builtin_amdgcn_raw_buffer_store_b128(v, xr, off_mine + 16 * i, 0, SC1);
-                        }
+                    for (int q = 0; q < 4; ++q) {
+                        const float g = G0[4 * i + q] + G1[4 * i + q];
+                        G0[4 * i + q] = g;
+                        v[q] = __float_as_uint(g);
                     }
-                } else {
-                    for (int i = t; i < NV4; i += MT) {
-                        u32x4 v;
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            const float g = G0[4 * i + q] + G1[4 * i + q];
-                            G0[4 * i + q] = g;
-                            v[q] = __float_as_uint(g);
-                        }
-                        __builtin_amdgcn_raw_buffer_store_b128(v, xr, off_mine + 16 * i, 0, SC1);
-                    }
+                    __builtin_amdgcn_raw_buffer_store_b128(v, xr, off_mine + 16 * i, 0, SC1);
                 }
                 if (t < TAIL) {
                     const float g = G0[4 * NV4 + t] + G1[4 * NV4 + t];
@@ -674,7 +656,7 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                 for (int k = 0; k < NG4; ++k) {
                     const int i = min(t + k * MT, NV4 - 1);
                     const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(xr, off_other + 16 * i, 0, SC1);
-                    const float4 mine = ONE ? own4[ONE ? k : 0] : *reinterpret_cast<const float4*>(&G0[4 * i]);
+                    const float4 mine = *reinterpret_cast<const float4*>(&G0[4 * i]);
                     const float mv[4] = {mine.x, mine.y, mine.z, mine.w};
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {

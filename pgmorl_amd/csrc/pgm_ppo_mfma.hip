@@ -33,6 +33,16 @@
 
 PGM_STAMP_UNIT(mfma)
 
+// unroll depths of the feature-contracting MFMA loops (A/B diagnostics: scripts/build_var.sh, -DPGM_EXP=n)
+#ifndef PGM_EXP
+#define PGM_EXP 0
+#endif
+#define PGM_PRAGMA(x) _Pragma(#x)
+#define PGM_UNROLL(n) PGM_PRAGMA(unroll n)
+#define PGM_U_L2 (PGM_EXP == 1 ? 16 : PGM_EXP == 2 ? 32 : 8)
+#define PGM_U_HEAD (PGM_EXP == 3 ? 8 : PGM_EXP == 4 ? 32 : 4)
+#define PGM_U16 (PGM_EXP == 5 ? 8 : PGM_EXP == 6 ? 16 : 4)
+
 namespace pgm {
 
 // ---------------------------------------------------------------- packed sample table
@@ -316,7 +326,7 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                     wave_lds_fence();
                     // ---- layer 2: Z2[s][o] = H1[s][:] . W2t[:][o]   (A from the transpose tile)
                     z[0] = z[1] = f32x16{0};
-#pragma unroll 8
+PGM_UNROLL(PGM_U_L2)
                     for (int ks = 0; ks < H / 2; ++ks) {
                         const int k = 2 * ks + h;
                         const float av = scr[c * SCR + k];
@@ -341,7 +351,7 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                     float outv[Q];
 #pragma unroll
                     for (int q = 0; q < Q; ++q) outv[q] = 0.f;
-#pragma unroll 4
+PGM_UNROLL(PGM_U_HEAD)
                     for (int u = 0; u < TS; ++u) {
                         const float hv = scr[c * SCR + h * TS + u];
 #pragma unroll
@@ -448,7 +458,7 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                         for (int r = 0; r < 16; ++r) scr[rowof(r, h) * SCR + ob * TS + c] = dZ2[ob][r];
                     wave_lds_fence();
                     z[0] = z[1] = f32x16{0};
-#pragma unroll 8
+PGM_UNROLL(PGM_U_L2)
                     for (int ks = 0; ks < H / 2; ++ks) {
                         const int k = 2 * ks + h;  // output unit o
                         const float av = scr[c * SCR + k];
@@ -1074,7 +1084,7 @@ __global__ __launch_bounds__(64 * W) void ppo_update_t16_kernel(MArgs a) {
                     // ---- layer 2: Z2[s][o] = H1[s][:] . W2t[:][o]  (A from the transpose tile)
 #pragma unroll
                     for (int ob = 0; ob < 4; ++ob) z[ob] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
+PGM_UNROLL(PGM_U16)
                     for (int ks = 0; ks < H / 4; ++ks) {
                         const int k = 4 * ks + g;
                         const float av = scr[c * S16 + k];
@@ -1098,7 +1108,7 @@ __global__ __launch_bounds__(64 * W) void ppo_update_t16_kernel(MArgs a) {
                     // ---- heads on the MFMA: out[s][q] = H2[s][:] . Wh[q][:]  (q = lane column, < Q)
                     f32x4 ho = f32x4{0.f, 0.f, 0.f, 0.f};
                     const bool qv = c < Q;
-#pragma unroll 4
+PGM_UNROLL(PGM_U16)
                     for (int ks = 0; ks < H / 4; ++ks) {
                         const int k = 4 * ks + g;
                         ho = mfma16(scr[c * S16 + k], qv ? Wt.Wh[qv ? c : 0][k] : 0.f, ho);
@@ -1192,7 +1202,7 @@ __global__ __launch_bounds__(64 * W) void ppo_update_t16_kernel(MArgs a) {
                     // into the pipe first, dW2 queues behind them
 #pragma unroll
                     for (int ib = 0; ib < 4; ++ib) z[ib] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
+PGM_UNROLL(PGM_U16)
                     for (int ks = 0; ks < H / 4; ++ks) {
                         const int k = 4 * ks + g;  // output unit o
                         const float av = scr[c * S16 + k];

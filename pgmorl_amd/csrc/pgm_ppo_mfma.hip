@@ -39,9 +39,11 @@ PGM_STAMP_UNIT(mfma)
 #endif
 #define PGM_PRAGMA(x) _Pragma(#x)
 #define PGM_UNROLL(n) PGM_PRAGMA(unroll n)
-#define PGM_U_L2 (PGM_EXP == 1 ? 16 : PGM_EXP == 2 ? 32 : 8)
-#define PGM_U_HEAD (PGM_EXP == 3 ? 8 : PGM_EXP == 4 ? 32 : 4)
-#define PGM_U16 (PGM_EXP == 5 ? 8 : PGM_EXP == 6 ? 16 : 4)
+// (measured, Walker: MODE 2 layer-2 / dH1 loops 8 -> 32: 6.54 -> 6.46 ms; VALU heads 4 -> 32: -> 6.48 ms; t16 loops
+// 4 -> 16: 5.40 -> 5.12 ms)
+#define PGM_U_L2 (PGM_EXP == 1 ? 8 : PGM_EXP == 2 ? 16 : 32)
+#define PGM_U_HEAD (PGM_EXP == 3 ? 4 : PGM_EXP == 4 ? 8 : 32)
+#define PGM_U16 (PGM_EXP == 5 ? 4 : PGM_EXP == 6 ? 8 : 16)
 
 namespace pgm {
 
@@ -326,7 +328,7 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                     wave_lds_fence();
                     // ---- layer 2: Z2[s][o] = H1[s][:] . W2t[:][o]   (A from the transpose tile)
                     z[0] = z[1] = f32x16{0};
-PGM_UNROLL(PGM_U_L2)
+PGM_UNROLL(ONE ? PGM_U_L2 : 8)
                     for (int ks = 0; ks < H / 2; ++ks) {
                         const int k = 2 * ks + h;
                         const float av = scr[c * SCR + k];
@@ -351,7 +353,7 @@ PGM_UNROLL(PGM_U_L2)
                     float outv[Q];
 #pragma unroll
                     for (int q = 0; q < Q; ++q) outv[q] = 0.f;
-PGM_UNROLL(PGM_U_HEAD)
+PGM_UNROLL(ONE ? PGM_U_HEAD : 4)
                     for (int u = 0; u < TS; ++u) {
                         const float hv = scr[c * SCR + h * TS + u];
 #pragma unroll
@@ -458,7 +460,7 @@ PGM_UNROLL(PGM_U_HEAD)
                         for (int r = 0; r < 16; ++r) scr[rowof(r, h) * SCR + ob * TS + c] = dZ2[ob][r];
                     wave_lds_fence();
                     z[0] = z[1] = f32x16{0};
-PGM_UNROLL(PGM_U_L2)
+PGM_UNROLL(ONE ? PGM_U_L2 : 8)
                     for (int ks = 0; ks < H / 2; ++ks) {
                         const int k = 2 * ks + h;  // output unit o
                         const float av = scr[c * SCR + k];
@@ -1084,7 +1086,7 @@ __global__ __launch_bounds__(64 * W) void ppo_update_t16_kernel(MArgs a) {
                     // ---- layer 2: Z2[s][o] = H1[s][:] . W2t[:][o]  (A from the transpose tile)
 #pragma unroll
                     for (int ob = 0; ob < 4; ++ob) z[ob] = f32x4{0.f, 0.f, 0.f, 0.f};
-PGM_UNROLL(PGM_U16)
+PGM_UNROLL(ONE ? PGM_U16 : 4)
                     for (int ks = 0; ks < H / 4; ++ks) {
                         const int k = 4 * ks + g;
                         const float av = scr[c * S16 + k];
@@ -1108,7 +1110,7 @@ PGM_UNROLL(PGM_U16)
                     // ---- heads on the MFMA: out[s][q] = H2[s][:] . Wh[q][:]  (q = lane column, < Q)
                     f32x4 ho = f32x4{0.f, 0.f, 0.f, 0.f};
                     const bool qv = c < Q;
-PGM_UNROLL(PGM_U16)
+PGM_UNROLL(ONE ? PGM_U16 : 4)
                     for (int ks = 0; ks < H / 4; ++ks) {
                         const int k = 4 * ks + g;
                         ho = mfma16(scr[c * S16 + k], qv ? Wt.Wh[qv ? c : 0][k] : 0.f, ho);
@@ -1202,7 +1204,7 @@ PGM_UNROLL(PGM_U16)
                     // into the pipe first, dW2 queues behind them
 #pragma unroll
                     for (int ib = 0; ib < 4; ++ib) z[ib] = f32x4{0.f, 0.f, 0.f, 0.f};
-PGM_UNROLL(PGM_U16)
+PGM_UNROLL(ONE ? PGM_U16 : 4)
                     for (int ks = 0; ks < H / 4; ++ks) {
                         const int k = 4 * ks + g;  // output unit o
                         const float av = scr[c * S16 + k];

@@ -31,6 +31,15 @@
 
 PGM_STAMP_UNIT(wupd)
 
+// unroll depths of the layer-2 / dH1 and VALU-head loops (A/B: scripts/build_var.sh, -DPGM_EXP=n)
+#ifndef PGM_EXP
+#define PGM_EXP 0
+#endif
+#define PGM_PRAGMA_W(x) _Pragma(#x)
+#define PGM_UNROLL_W(n) PGM_PRAGMA_W(unroll n)
+#define PGM_UW_L2 (PGM_EXP == 7 || PGM_EXP == 9 ? 32 : 8)
+#define PGM_UW_HEAD (PGM_EXP == 8 || PGM_EXP == 9 ? 32 : 4)
+
 namespace pgm {
 
 namespace {
@@ -125,7 +134,9 @@ int wide_xslot_words(int O, int A, int K) {
 
 namespace {
 
-template <int O, int A, int K, int NS>
+// ONE: mb = NS * 4 * 32 (each wave owns exactly one 32-row tile of one pass per minibatch; Humanoid N = 8, NS = 4):
+// the pass loop is straight-line, so the gradient accumulators are not loop-carried
+template <int O, int A, int K, int NS, bool ONE>
 __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
     static_assert(O > 32 && O % 8 == 0, "wide kernel: obs_dim > 32, multiple of 8 (float4 halves)");
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -219,13 +230,13 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
             for (int j = 0; j < NKW; ++j) dW1[j][0] = dW1[j][1] = f32x16{0};
             float lsum = 0.f;
 
-            for (int ps = 0; ps < npass; ++ps) {
+            for (int ps = 0; ONE ? ps < 1 : ps < npass; ++ps) {
                 const int i0 = (ps * 4 + w) * TS;  // this wave's tile of the pass
                 const int si = i0 + c;
                 const bool ok = si < mbs;
                 const int row = perm[min(si, mbs - 1)];
                 if (h == 0) S.rowid[w][c] = row;
-                if (i0 < mbs) {  // wave-uniform
+                if (ONE || i0 < mbs) {  // wave-uniform
                     // per-sample loss operands of this lane's sample, gathered now (random rows: an HBM round trip
                     // that the layer-1 stream hides) -- critic: old values, returns; actor: action, old logp, adv
                     float pa[A], pv[K], pr[K], plp = 0.f, pad = 0.f;
@@ -291,7 +302,7 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
                     PGM_STAMP(0);
                     // ---- layer 2 (A from tile A, transposed)
                     z[0] = z[1] = f32x16{0};
-#pragma unroll 8
+PGM_UNROLL_W(PGM_UW_L2)
                     for (int ks = 0; ks < H / 2; ++ks) {
                         const int k = 2 * ks + h;
                         const float av = scr[c * SCR + k];
@@ -310,7 +321,7 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
                     float outv[Q];
 #pragma unroll
                     for (int q = 0; q < Q; ++q) outv[q] = 0.f;
-#pragma unroll 4
+PGM_UNROLL_W(PGM_UW_HEAD)
                     for (int u = 0; u < TS; ++u) {
                         const float hv = scr2[c * SCR + h * TS + u];
 #pragma unroll
@@ -419,7 +430,7 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
                         for (int r = 0; r < 16; ++r) scr2[rowof(r, h) * SCR + ob * TS + c] = dZ2[ob][r];
                     wave_lds_fence();
                     z[0] = z[1] = f32x16{0};
-#pragma unroll 8
+PGM_UNROLL_W(PGM_UW_L2)
                     for (int ks = 0; ks < H / 2; ++ks) {
                         const int k = 2 * ks + h;
                         const float av = scr2[c * SCR + k];
@@ -922,9 +933,11 @@ int ppo_update_wide(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params,
                 hipLaunchKernelGGL(kern, dim3(grid), dim3(MT), smem, stream, a);
                 return launch_status("pgm_ppo_update");
             };
-            if (ns == 4) return launch(ppo_update_wide_kernel<O, A, K, 4>, 32 * groups);
-            if (ns == 2) return launch(ppo_update_wide_kernel<O, A, K, 2>, 16 * groups);
-            return launch(ppo_update_wide_kernel<O, A, K, 1>, 2 * d->P);
+            const int mb = d->T * d->N / hp->num_mini_batch;
+            if (ns == 4 && mb == 4 * 4 * TS) return launch(ppo_update_wide_kernel<O, A, K, 4, true>, 32 * groups);
+            if (ns == 4) return launch(ppo_update_wide_kernel<O, A, K, 4, false>, 32 * groups);
+            if (ns == 2) return launch(ppo_update_wide_kernel<O, A, K, 2, false>, 16 * groups);
+            return launch(ppo_update_wide_kernel<O, A, K, 1, false>, 2 * d->P);
         }
     });
 }

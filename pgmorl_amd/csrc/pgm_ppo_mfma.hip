@@ -458,6 +458,19 @@ PGM_UNROLL(ONE ? PGM_U_HEAD : 4)
                     for (int ob = 0; ob < 2; ++ob)
 #pragma unroll
                         for (int r = 0; r < 16; ++r) scr[rowof(r, h) * SCR + ob * TS + c] = dZ2[ob][r];
+                    // ---- dW2^T[in][o] += H1^T dZ2: straight from the C-layout registers.  GW2_FIRST: issued while the
+                    // dZ2 transpose tile lands (its MFMAs cover the LDS round trip); otherwise behind dH1, in the
+                    // MFMA pipe while the VALU forms dZ1 from the dH1 results
+                    constexpr bool GW2_FIRST = PGM_EXP == 11;
+                    auto gw2 = [&]() {
+#pragma unroll
+                        for (int r = 0; r < 16; ++r)
+#pragma unroll
+                            for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+                                for (int ob = 0; ob < 2; ++ob) gW2[ib][ob] = mfma(H1[ib][r], dZ2[ob][r], gW2[ib][ob]);
+                    };
+                    if constexpr (GW2_FIRST) gw2();
                     wave_lds_fence();
                     z[0] = z[1] = f32x16{0};
 PGM_UNROLL(ONE ? PGM_U_L2 : 8)
@@ -467,14 +480,7 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
 #pragma unroll
                         for (int ib = 0; ib < 2; ++ib) z[ib] = mfma(av, W.W2t[ib * TS + c][k], z[ib]);
                     }
-                    // ---- dW2^T[in][o] += H1^T dZ2: straight from the C-layout registers (runs in the MFMA pipe
-                    // while the VALU forms dZ1 from the dH1 results)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r)
-#pragma unroll
-                        for (int ib = 0; ib < 2; ++ib)
-#pragma unroll
-                            for (int ob = 0; ob < 2; ++ob) gW2[ib][ob] = mfma(H1[ib][r], dZ2[ob][r], gW2[ib][ob]);
+                    if constexpr (!GW2_FIRST) gw2();
                     f32x16 dZ1[2];
 #pragma unroll
                     for (int ib = 0; ib < 2; ++ib)
@@ -1199,9 +1205,20 @@ PGM_UNROLL(ONE ? PGM_U16 : 4)
                     for (int ob = 0; ob < 4; ++ob)
 #pragma unroll
                         for (int r = 0; r < 4; ++r) scr[(4 * g + r) * S16 + ob * T16 + c] = dZ2[ob][r];
+                    // ---- dW2^T[in][o] += H1^T dZ2 straight from the C registers.  GW2_FIRST: issued while the dZ2
+                    // transpose tile lands; otherwise behind dH1 (whose MFMAs then go into the pipe first)
+                    constexpr bool GW2_FIRST = PGM_EXP == 12;
+                    auto gw2 = [&]() {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+#pragma unroll
+                            for (int ib = 0; ib < 4; ++ib)
+#pragma unroll
+                                for (int ob = 0; ob < 4; ++ob) gW2[ib][ob] = mfma16(H1[ib][r], dZ2[ob][r], gW2[ib][ob]);
+                    };
+                    if constexpr (GW2_FIRST) gw2();
                     wave_lds_fence();
-                    // ---- dH1 = dZ2 W2 (A = dZ2 through the transpose tile, B = W2t[in][o] column); its MFMAs go
-                    // into the pipe first, dW2 queues behind them
+                    // ---- dH1 = dZ2 W2 (A = dZ2 through the transpose tile, B = W2t[in][o] column)
 #pragma unroll
                     for (int ib = 0; ib < 4; ++ib) z[ib] = f32x4{0.f, 0.f, 0.f, 0.f};
 PGM_UNROLL(ONE ? PGM_U16 : 4)
@@ -1211,13 +1228,7 @@ PGM_UNROLL(ONE ? PGM_U16 : 4)
 #pragma unroll
                         for (int ib = 0; ib < 4; ++ib) z[ib] = mfma16(av, Wt.W2t[ib * T16 + c][k], z[ib]);
                     }
-                    // ---- dW2^T[in][o] += H1^T dZ2 straight from the C registers
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-#pragma unroll
-                        for (int ib = 0; ib < 4; ++ib)
-#pragma unroll
-                            for (int ob = 0; ob < 4; ++ob) gW2[ib][ob] = mfma16(H1[ib][r], dZ2[ob][r], gW2[ib][ob]);
+                    if constexpr (!GW2_FIRST) gw2();
                     f32x4 dZ1[4];
 #pragma unroll
                     for (int ib = 0; ib < 4; ++ib)

@@ -2,7 +2,7 @@
 set -e
 src=$1; shift
 cd "$(dirname "$0")/.."
-python -m pgmorl_amd.build > /dev/null
+# (run python -m pgmorl_amd.build once beforehand: parallel invocations of this script must not race on it)
 for n in "$@"; do
   mkdir -p pgmorl_amd/build_var$n
   objs=""

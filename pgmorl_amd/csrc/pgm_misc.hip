@@ -17,7 +17,7 @@ namespace pgm {
 //   !use_gae: A_t = g*m_{t+1}*(b_{t+1} if proper), B_t = r_t*b + (1-b)*V_t (proper) or r_t, y_T = V_T
 // Split T into C chunks per lane: pass 1 composes each chunk's affine map, a per-lane sweep over
 // the C chunk maps gives every chunk's incoming y, pass 2 re-walks the chunk and writes R.
-constexpr int GT = 256;
+constexpr int GT = 1024;  // threads per task: N*K lanes x GT/(N*K) chunks (Walker: 128 chunks of 16 steps)
 
 struct GaeArgs {
     int N, T, K;

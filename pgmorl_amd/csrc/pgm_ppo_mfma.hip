@@ -295,10 +295,14 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
             for (int s0 = 0; ONE ? s0 < 1 : s0 < mbs; s0 += (ONE ? 1 : SBk), ++gp) {
                 const int ns = ONE ? SBk : min(SBk, mbs - s0);
                 const int cur = NBUF == 2 ? (gp & 1) : 0;
-                if constexpr (NBUF == 2) {  // stage the next pass while this one computes
+                // stage the next pass while this one computes; LATE_STAGE (single-tile A/B): issued behind the
+                // layer-1 MFMAs, so the index reads and DMA issue overlap the matrix pipe
+                constexpr bool LATE_STAGE = ONE && NBUF == 2 && PGM_EXP == 31;
+                auto stage_next = [&]() {
                     if (gp + 1 < npass) issue_rows(cur ^ 1, (gp + 1) & 1);
                     if (gp + 2 < npass) issue_idx(gp + 2, gp & 1);
-                }
+                };
+                if constexpr (NBUF == 2 && !LATE_STAGE) stage_next();
                 const float* rb = &S.RB[cur][0];
                 PGM_STAMP(0);
 
@@ -315,6 +319,7 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
 #pragma unroll
                         for (int hb = 0; hb < 2; ++hb) z[hb] = mfma(av, k < O ? W.W1t[k][hb * TS + c] : 0.f, z[hb]);
                     }
+                    if constexpr (LATE_STAGE) stage_next();
                     f32x16 H1[2];
 #pragma unroll
                     for (int hb = 0; hb < 2; ++hb) {

@@ -1685,7 +1685,7 @@ static int launch_t16_k(const pgm_dims* d, const MArgs& a, hipStream_t stream) {
 template <int O, int A, int K, int NS, int W>
 int launch_t16(const pgm_dims* d, const MArgs& a, hipStream_t stream) {
     const int mb = d->T * d->N / a.hp.num_mini_batch;
-    if (mb == NS * W * T16) return launch_t16_k<O, A, K, NS, W, true>(d, a, stream);
+    if (mb == NS * W * T16 && !getenv("PGM_NO_ONE")) return launch_t16_k<O, A, K, NS, W, true>(d, a, stream);
     return launch_t16_k<O, A, K, NS, W, false>(d, a, stream);
 }
 
@@ -1715,7 +1715,7 @@ template <int O, int A, int K, int MODE>
 int launch_mode(const pgm_dims* d, const MArgs& a, hipStream_t stream) {
     using Sm = MSmem<O, A, K, true>;
     if constexpr (MODE == 2) {  // 2 workgroups x 4 waves x one 32-row tile = the minibatch, in one pass
-        if (d->T * d->N / a.hp.num_mini_batch == 2 * 4 * TS && Sm::SBk >= 4 * TS)
+        if (d->T * d->N / a.hp.num_mini_batch == 2 * 4 * TS && Sm::SBk >= 4 * TS && !getenv("PGM_NO_ONE"))
             return launch_mode_k<O, A, K, MODE, true>(d, a, stream);
     }
     return launch_mode_k<O, A, K, MODE, false>(d, a, stream);

@@ -13,6 +13,7 @@ storage.py:133) and uploads them -- bit-compatible with the CPU oracle; ``rng='d
 counter-based device streams keyed by j (same distribution, no host work; the benchmark mode).
 Like the reference, all tasks of an iteration share one noise stream.
 """
+import os
 import time
 
 import numpy as np
@@ -174,6 +175,9 @@ class MOPGPopulation:
                     log(f'[RL] Updates {j + 1}, num timesteps {steps}, FPS {int(steps / max(dt, 1e-9))}, '
                         f'time {dt:.2f} seconds (x{P} tasks on {ws} device(s))')
             tb.wait_eval()
+            if os.environ.get('PGM_DEBUG_TASKS'):
+                print(f'[debug] generation at iteration {iteration}: P={P} local={Pl} iters={len(its)} '
+                      f'failed={int(tb.update_failed.item())}', flush=True)
             tb.check_update()  # a timed-out exchange never becomes an offspring (raises PGMError)
             for rec, ob in zip(recs, objs_i):
                 rec[:, :tb.K] = ob

@@ -35,10 +35,13 @@ constexpr int ppo_img_floats(int O, int A, int K) {  // TowerImg<O, A, K> of pgm
     return O * H + H * (H + 1) + Q * H + 2 * H + Q + A;
 }
 constexpr int PGM_NS_MAX = 4;  // workgroups per tower of the row-split updates
-inline size_t ppo_flag_bytes(int P) { return ((size_t)(2 * PGM_NS_MAX * P + 1) * 8 + 255) / 256 * 256; }
-// norm granule of (task p, tower m, row part hs): row part 0 below the timeout word, the others above it
-__host__ __device__ inline int ppo_norm_granule(int P, int p, int m, int hs) {
-    return hs == 0 ? 2 * p + m : 2 * P + 1 + 2 * P * (hs - 1) + 2 * p + m;
+inline size_t ppo_flag_bytes(int P) { return ((size_t)(4 * PGM_NS_MAX * P + 1) * 8 + 255) / 256 * 256; }
+// norm granule of (task p, tower m, row part hs, step parity par): (row part 0, parity 0) below the timeout word
+// (word 2P), the others above it.  Double-buffered by step parity like the image slots: a workgroup rewrites a
+// granule only two steps later, after every reader has matched it, so a delayed poll can never miss its tag.
+__host__ __device__ inline int ppo_norm_granule(int P, int p, int m, int hs, int par) {
+    const int q = 2 * hs + par;
+    return q == 0 ? 2 * p + m : 2 * P + 1 + 2 * P * (q - 1) + 2 * p + m;
 }
 inline int ppo_xslot(int O, int A, int K) { return (ppo_img_floats(O, A, K) + 1 + 31) / 32 * 32; }  // granules
 inline size_t ppo_xbuf_bytes(const pgm_dims* d, int ns = PGM_NS_MAX) {

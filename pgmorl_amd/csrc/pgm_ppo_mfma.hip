@@ -725,7 +725,7 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
             if constexpr (SPLIT) {  // tagged 8-byte granule hand-off with the other tower's workgroup
                 if (t == 0) {
                     const unsigned tag = (unsigned)(nstep + 1);
-                    unsigned long long* ws = a.ws + (hs == 0 ? 2 * p : 2 * a.P + 1 + 2 * p);
+                    unsigned long long* ws = a.ws + ppo_norm_granule(a.P, p, 0, hs, nstep & 1);
                     __hip_atomic_store(ws + m, ((unsigned long long)tag << 32) | __float_as_uint(total),
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     unsigned long long x = 0;
@@ -1571,7 +1571,7 @@ PGM_UNROLL(ONE ? PGM_U16 : 4)
             PGM_STAMP(8);
             if (t == 0) {
                 const unsigned tag = (unsigned)(nstep + 1);
-                unsigned long long* gr = a.ws + ppo_norm_granule(a.P, p, 0, hs);
+                unsigned long long* gr = a.ws + ppo_norm_granule(a.P, p, 0, hs, nstep & 1);
                 __hip_atomic_store(gr + m, ((unsigned long long)tag << 32) | __float_as_uint(total), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
                 unsigned long long x = 0;

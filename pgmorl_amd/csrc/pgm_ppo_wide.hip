@@ -731,14 +731,14 @@ PGM_UNROLL_W(PGM_UW_L2)
             lds_sync_m();
             float total = (S.red[0] + S.red[1]) + (S.red[2] + S.red[3]);
             if (t == 0)
-                __hip_atomic_store(a.ws + ppo_norm_granule(a.P, p, m, hs), ((unsigned long long)tag << 32) | __float_as_uint(total),
+                __hip_atomic_store(a.ws + ppo_norm_granule(a.P, p, m, hs, par), ((unsigned long long)tag << 32) | __float_as_uint(total),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (t < 2 * NS) {  // lane (mm, hh) = (t / NS, t % NS) polls that workgroup's granule, all concurrently
                 const int mm = t / NS, hh = t - mm * NS;
                 float v = total;
                 if (mm != m || hh != hs) {
                     const bool failed = __hip_atomic_load(a.ws + 2 * a.P, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    v = failed ? 0.f : __uint_as_float((unsigned)spin(a.ws + ppo_norm_granule(a.P, p, mm, hh), tag));
+                    v = failed ? 0.f : __uint_as_float((unsigned)spin(a.ws + ppo_norm_granule(a.P, p, mm, hh, par), tag));
                 }
                 S.red[16 + t] = v;
             }

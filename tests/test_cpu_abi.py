@@ -115,7 +115,7 @@ def test_adam_state_roundtrip():
                                        ('MO-Humanoid-v2', 20, 8, 2048), ('MO-Humanoid-v2', 3, 8, 64)])
 def test_update_workspace_covers_every_split(env, P, N, T):
     """pgm_ppo_update_workspace_bytes covers the largest row split a launch may pick (PGM_NS_MAX = 4 parts per
-    tower): tagged norm granules (2 x 4 x P + 1, 256-B padded), exchange slots [P][2 towers][4 parts][2
+    tower): tagged norm granules (2 towers x 4 parts x 2 step parities x P + 1, 256-B padded), exchange slots [P][2 towers][4 parts][2
     parities], and the packed sample table (obs_dim <= 32) or the parts' private parameter rows (wide)."""
     from pgmorl_amd import envspec
     spec = envspec.make_spec(env)
@@ -123,7 +123,7 @@ def test_update_workspace_covers_every_split(env, P, N, T):
     Q = max(A, K)
     d = _lib.Dims(P, N, T, O, A, K, H)
     got = _lib.lib().pgm_ppo_update_workspace_bytes(d)
-    flags = -(-(2 * 4 * P + 1) * 8 // 256) * 256
+    flags = -(-(2 * 4 * 2 * P + 1) * 8 // 256) * 256
     if O <= 32:
         img = O * H + H * (H + 1) + Q * H + 2 * H + Q + A
         xslot = -(-(img + 1) // 32) * 32

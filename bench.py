@@ -52,6 +52,12 @@ def parse():
                          'bench process itself (the box allows 16 processes with the GPU open)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-overlap-eval', action='store_true', help='evaluate on the main stream (A/B)')
+    ap.add_argument('--whole-run', dest='whole_run', action='store_true', default=None,
+                    help='also time the whole PG-MORL run (pgmorl_amd.morl.run: warm-up, generations, selection, '
+                         'writer) on Walker pop=40 with the reference budget (default: on at N=1)')
+    ap.add_argument('--no-whole-run', dest='whole_run', action='store_false')
+    ap.add_argument('--whole-run-steps', type=float, default=5e6,
+                    help='--num-env-steps of the whole run (per task; scripts/walker2d-v2.py:38 uses 5e6)')
     ap.add_argument('--traffic-file', default=None,
                     help='PMC summary (scripts/pmc_summary.py) to quote as roofline.traffic; default: the newest '
                          'profiles/r0*_pmc_*.json whose workload matches this run')
@@ -164,21 +170,86 @@ def cpu_baseline(args, spec, tasks):
                       f'M={args.num_mini_batch}, + eval) of the fp64 torch/numpy oracle, {t1 - t0:.1f} s wall'}
 
 
+def hv_comparison(env_name):
+    """The newest committed full-algorithm device-vs-oracle HV comparison at an equal budget for this env
+    (scripts/hv_full.py: warm-up + prediction-guided generations on both sides, per seed), summarised."""
+    key = {'MO-Walker2d-v2': 'walker', 'MO-Hopper-v2': 'hopper'}.get(env_name)
+    if key is None:
+        return None
+    import re
+
+    def version(path):  # r<round>_hvfull<n>_<env>.json: newest round, then highest n (none = 1)
+        m = re.match(r'r(\d+)_hvfull(\d*)_', os.path.basename(path))
+        return (int(m.group(1)), int(m.group(2) or 1)) if m else (-1, -1)
+    for dev in sorted(glob.glob(os.path.join(ROOT, 'profiles', f'r*_hvfull*_{key}.json')), key=version, reverse=True):
+        orc = dev.replace(f'_{key}.json', f'_oracle_{key}.json').replace('oracle_oracle', 'oracle')
+        if 'oracle' in os.path.basename(dev) or not os.path.exists(orc):
+            continue
+        d, o = json.load(open(dev)), json.load(open(orc))
+        ho = {r['seed']: r['hv'] for r in o['runs']}
+        rel = [(r['hv'] - ho[r['seed']]) / ho[r['seed']] for r in d['runs'] if r['seed'] in ho]
+        if not rel:
+            continue
+        rel = np.array(rel)
+        half = 1.96 * rel.std(ddof=1) / np.sqrt(len(rel)) if len(rel) > 1 else None
+        return {'source': [os.path.relpath(dev, ROOT), os.path.relpath(orc, ROOT)], 'config': d.get('config'),
+                'seeds': len(rel), 'hv_rel_diff_per_seed': [float(x) for x in rel],
+                'hv_rel_diff_mean': float(rel.mean()), 'ci95_half_width': None if half is None else float(half)}
+    return None
+
+
 def hypervolume(args, history, budget):
     """HV of the EP over every offspring objective vector this run produced (morl/ep.py:23-31,
-    morl/hypervolume.py), plus the committed device-vs-oracle comparison at an equal budget
-    (scripts/hv_budget.py -> profiles/r01_hv_budget.json), when one exists for this env."""
+    morl/hypervolume.py), plus the committed device-vs-oracle comparison of the whole algorithm at an equal
+    budget (hv_comparison), when one exists for this env."""
     from pgmorl_amd import pareto
     objs = torch.cat(history).cpu().numpy()
     idx = pareto.get_ep_indices(objs)
     hv = {'hv': pareto.compute_hypervolume(objs[idx]) if len(idx) else 0.0, 'ep_size': len(idx),
           'budget_env_steps': budget, 'rng': 'perf-mode device streams', 'ref_point': 0}
-    path = os.path.join(ROOT, 'profiles', 'r01_hv_budget.json')
-    if os.path.exists(path):
-        rows = [r for r in json.load(open(path)).get('runs', []) if r.get('env') == args.env_name]
-        if rows:
-            hv['vs_oracle_equal_budget'] = {'source': 'profiles/r01_hv_budget.json', 'runs': rows}
+    cmp_ = hv_comparison(args.env_name)
+    if cmp_ is not None:
+        hv['vs_oracle_equal_budget'] = cmp_
     return hv
+
+
+def whole_run(args, iter_value):
+    """The whole-node metric of the reference (morl/morl.py:62-175 driven by morl/run.py): pgmorl_amd.morl.run
+    end to end -- warm-up, every generation's MOPG on the device, EP / population / OptGraph, prediction-guided
+    selection (native fits), the per-generation text dumps and the final EP policies -- on MO-Walker2d-v2 with
+    pop = 40 (delta 1/39), update_iter 20, the reference's flags (scripts/walker2d-v2.py) and budget.  Timed
+    from entering run() to its return (results tree complete); value = train env-steps / that wall time."""
+    import tempfile
+    from pgmorl_amd import pareto
+    from pgmorl_amd.morl import run as morl_run
+    from pgmorl_amd.run import get_parser, merge_argv
+    save = tempfile.mkdtemp(prefix='pgm_whole_', dir=os.environ.get('TMPDIR', '/tmp'))
+    argv = ['--env-name', 'MO-Walker2d-v2', '--obj-num', '2', '--num-env-steps', str(int(args.whole_run_steps)),
+            '--warmup-iter', '80', '--update-iter', '20', '--min-weight', '0.0', '--max-weight', '1.0',
+            '--delta-weight', repr(1.0 / 39), '--eval-num', '1', '--pbuffer-num', '100', '--pbuffer-size', '2',
+            '--selection-method', 'prediction-guided', '--num-weight-candidates', '7', '--num-tasks', '40',
+            '--sparsity', '1.0', '--obj-rms', '--ob-rms', '--raw', '--rl-log-interval', '0', '--seed', '0',
+            '--save-dir', save]
+    ns = get_parser().parse_args(merge_argv(argv))
+    old = torch.get_default_dtype()
+    torch.set_default_dtype(torch.float64)  # morl/run.py:53
+    try:
+        t0 = time.perf_counter()
+        ep = morl_run(ns, device='cuda', rng='device', log=lambda *m: None)
+        wall = time.perf_counter() - t0
+    finally:
+        torch.set_default_dtype(old)
+    tm = ep.timing
+    objs = np.asarray(ep.obj_batch)
+    import shutil
+    shutil.rmtree(save, ignore_errors=True)
+    v = tm['train_env_steps'] / wall
+    return {'value': v, 'unit': 'env steps/sec', 'wall_s': wall, 'train_env_steps': tm['train_env_steps'],
+            'generations': len(tm['generations']), 'mopg_s': tm['rl_s'], 'boundary_host_s': tm['host_s'],
+            'init_s': tm['init_s'], 'host_share': tm['host_s'] / wall, 'vs_iteration_bench': v / iter_value,
+            'hv': pareto.compute_hypervolume(objs) if len(objs) else 0.0, 'ep_size': int(len(objs)),
+            'config': 'MO-Walker2d-v2 (SynthMO) pop=40, prediction-guided, warmup_iter 80, update_iter 20, '
+                      f'num_env_steps {int(args.whole_run_steps)}, N=4, T=2048, E=10, M=32, device RNG, seed 0'}
 
 
 def main():
@@ -312,6 +383,12 @@ def main():
                                                                  E) / (world * PEAK_HBM_GBS * 1e9)},
     }
     out['hypervolume'] = hypervolume(args, history, G * N * T * len(history))
+    if args.whole_run is None:
+        args.whole_run = world == 1 and args.env_name == 'MO-Walker2d-v2' and args.scaling == 'weak'
+    if args.whole_run:
+        del tb, history
+        torch.cuda.empty_cache()
+        out['whole_run'] = whole_run(args, value)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out['cpu_baseline'] = cb = cpu_baseline(args, spec, G)
         out['vs_96vcpu_extrapolated'] = value / cb['extrapolated_96vcpu']

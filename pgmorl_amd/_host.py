@@ -23,6 +23,11 @@ class PGMHostError(RuntimeError):
 def lib():
     global _lib
     if _lib is None:
+        if not os.environ.get('PGM_HOST_LIB') and os.path.exists(os.path.join(HERE, 'csrc', 'pgm_host.cpp')):
+            # rebuild when pgm_host.cpp / pgm_host.h are newer than the library (no-op otherwise): a stale
+            # binary must never serve the selection path
+            from .build import build_host
+            build_host()
         if not os.path.exists(LIB_PATH):
             raise PGMHostError(f'{LIB_PATH} missing: run python -m pgmorl_amd.build (the boundary has no Python fallback)')
         L = C.CDLL(LIB_PATH)

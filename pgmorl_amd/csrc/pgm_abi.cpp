@@ -1,6 +1,7 @@
 // Host plumbing of the C ABI: version, thread-local error string, parameter layout.
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #include "pgm_common.hpp"
 
@@ -35,6 +36,31 @@ int device_cu_count() {
             cus = 1;
     }
     return cus;
+}
+
+int check_coresident(const void* kern, int block, size_t smem, int grid, const char* what) {
+    int per_cu = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, block, smem);
+    if (e != hipSuccess) return hip_fail(e, what);
+    int cus = device_cu_count();
+    if (const char* o = getenv("PGM_TEST_RESIDENT_CUS")) cus = atoi(o);  // test-only: pretend a smaller device
+    if (per_cu < 1 || (long long)grid > (long long)per_cu * cus) {
+        set_error("%s: %d workgroups of %d threads (%zu B LDS) cannot all be co-resident: occupancy %d per CU x %d "
+                  "CUs; shard the tasks over more GPUs", what, grid, block, smem, per_cu, cus);
+        return PGM_E_UNSUPPORTED;
+    }
+    return PGM_OK;
+}
+
+DbgDelay dbg_delay_from_env() {
+    DbgDelay d{0, 0, 0, 0u};
+    const char* s = getenv("PGM_TEST_DELAY");
+    if (s && *s) {
+        int st = 0, bl = 0, wh = 0;
+        unsigned cy = 0;
+        if (sscanf(s, "%d:%d:%d:%u", &st, &bl, &wh, &cy) == 4) d = DbgDelay{st, bl, wh, cy};
+    }
+    return d;
 }
 
 static inline int32_t round_up(int32_t x, int32_t m) { return (x + m - 1) / m * m; }

@@ -61,6 +61,26 @@ inline size_t ppo_workspace_bytes(const pgm_dims* d) {
            (size_t)d->P * d->T * d->N * ppo_row_stride(d->O, d->A, d->K) * sizeof(float);
 }
 int device_cu_count();  // CUs of the current device (cached)
+// Co-residency precondition of the persistent update kernels (their workgroups spin on each other's tagged
+// flags, so every workgroup of the grid must be resident at once): the occupancy query for this kernel,
+// block size and LDS must admit grid <= blocks-per-CU x CUs.  PGM_E_UNSUPPORTED (with the numbers) otherwise.
+int check_coresident(const void* kern, int block, size_t smem, int grid, const char* what);
+
+// Test-only exchange delay (PGM_TEST_DELAY="step:block:where:cycles", parsed by the launcher; cycles 0 = off):
+// workgroup `block` stalls `cycles` shader cycles at hand-off point `where` of Adam step `step` -- 0 before
+// publishing its gradient image, 1 between its image flag store and its partner poll, 2 between its tower-norm
+// granule store and its poll.  Provokes the delayed-poll orders the step-parity double buffering must survive.
+struct DbgDelay {
+    int step, block, where;
+    unsigned cycles;
+};
+DbgDelay dbg_delay_from_env();
+__device__ __forceinline__ void dbg_delay(const DbgDelay& d, int nstep, int where) {
+    if (d.cycles != 0u && nstep == d.step && (int)blockIdx.x == d.block && where == d.where) {
+        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+        while (__builtin_amdgcn_s_memtime() - t0 < (unsigned long long)d.cycles) __builtin_amdgcn_s_sleep(8);
+    }
+}
 
 // ---------------------------------------------------------------- device helpers
 // Branch-free fp32 tanh (~14 VALU ops, rel. error ~3e-7): odd Taylor series through x^9 for |x| < 0.25

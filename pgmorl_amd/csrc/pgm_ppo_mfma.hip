@@ -161,6 +161,7 @@ struct MArgs {
     int xslot;               // 8-byte words per exchange slot (image payload, flag granule in the last word)
     int xbytes;              // bytes of the exchange buffer
     int P;
+    DbgDelay dbg;            // test-only exchange delay (PGM_TEST_DELAY; cycles 0 = off)
 };
 
 
@@ -634,6 +635,7 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
                 float* G0 = S.big.GA[0];
                 const float* G1 = S.big.GA[1];
                 const float lsum_wg = (S.red[8] + S.red[9]) + (S.red[10] + S.red[11]);
+                dbg_delay(a.dbg, nstep, 0);
                 for (int i = t; i < NV4; i += MT) {
                     u32x4 v;
 #pragma unroll
@@ -657,6 +659,7 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
                     const unsigned long long* flag_other = a.xb + (size_t)slot_other * a.xslot + a.xslot - 1;
                     __hip_atomic_store(flag_mine, ((unsigned long long)tag << 32) | __float_as_uint(lsum_wg),
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    dbg_delay(a.dbg, nstep, 1);
                     unsigned long long x = 0;
                     for (unsigned spins = 0;; ++spins) {
                         x = __hip_atomic_load(flag_other, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -728,6 +731,7 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
                     unsigned long long* ws = a.ws + ppo_norm_granule(a.P, p, 0, hs, nstep & 1);
                     __hip_atomic_store(ws + m, ((unsigned long long)tag << 32) | __float_as_uint(total),
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    dbg_delay(a.dbg, nstep, 2);
                     unsigned long long x = 0;
                     const bool failed = __hip_atomic_load(a.ws + 2 * a.P, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     for (unsigned spins = 0; !failed; ++spins) {
@@ -1404,6 +1408,7 @@ PGM_UNROLL(ONE ? PGM_U16 : 4)
                     }
                 }
                 if constexpr (NS > 1) {
+                    dbg_delay(a.dbg, nstep, 0);
                     const int off_mine = slot_of(hs) * a.xslot * 8;
 #pragma unroll
                     for (int k = 0; k < NG4; ++k) {
@@ -1431,6 +1436,7 @@ PGM_UNROLL(ONE ? PGM_U16 : 4)
                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     }
                     if (t < NS) {  // lane h polls part h's flag: the NS - 1 polls run concurrently
+                        dbg_delay(a.dbg, nstep, 1);
                         float lp = lsum_wg;
                         if (t != hs) {
                             const unsigned long long* flag_h = a.xb + (size_t)slot_of(t) * a.xslot + a.xslot - 1;
@@ -1574,6 +1580,7 @@ PGM_UNROLL(ONE ? PGM_U16 : 4)
                 unsigned long long* gr = a.ws + ppo_norm_granule(a.P, p, 0, hs, nstep & 1);
                 __hip_atomic_store(gr + m, ((unsigned long long)tag << 32) | __float_as_uint(total), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
+                dbg_delay(a.dbg, nstep, 2);
                 unsigned long long x = 0;
                 const bool failed = __hip_atomic_load(a.ws + 2 * a.P, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 for (unsigned spins = 0; !failed; ++spins) {
@@ -1675,9 +1682,10 @@ static int launch_t16_k(const pgm_dims* d, const MArgs& a, hipStream_t stream) {
     auto kern = ppo_update_t16_kernel<O, A, K, NS, W, ONE>;
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update");
+    const int grid = 8 * NS * ((d->P + 3) / 4);
+    if (int rc = check_coresident((const void*)kern, 64 * W, smem, grid, "pgm_ppo_update")) return rc;
     e = hipMemsetAsync(a.ws, 0, ppo_flag_bytes(d->P) + ppo_xbuf_bytes(d, NS), stream);
     if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update (workspace reset)");
-    const int grid = 8 * NS * ((d->P + 3) / 4);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * W), smem, stream, a);
     return launch_status("pgm_ppo_update");
 }
@@ -1704,9 +1712,12 @@ int launch_mode_k(const pgm_dims* d, const MArgs& a, hipStream_t stream) {
     if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update");
     // norm granules, timeout flag (and MODE 2: the exchange slots) start at tag 0; MODE 0 resets the flag
     // word too, so word 2P always reports THIS call
+    const int grid = MODE == 2 ? 16 * ((d->P + 3) / 4) : SPLIT ? 2 * d->P : d->P;
+    if constexpr (SPLIT) {  // workgroups exchange through spin-waits: all of them must be resident together
+        if (int rc = check_coresident((const void*)kern, MT, smem, grid, "pgm_ppo_update")) return rc;
+    }
     e = hipMemsetAsync(a.ws, 0, ppo_flag_bytes(d->P) + (MODE == 2 ? ppo_xbuf_bytes(d) : 0), stream);
     if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update (workspace reset)");
-    const int grid = MODE == 2 ? 16 * ((d->P + 3) / 4) : SPLIT ? 2 * d->P : d->P;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(MT), smem, stream, a);
     return launch_status("pgm_ppo_update");
 }
@@ -1762,7 +1773,7 @@ int ppo_update_mfma(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params,
     MArgs a{d->N, d->T, make_layout(d->O, d->A, d->K, d->H), *hp, params, adam_m, adam_v, adam_step, lr, perms,
             (const float*)(ws + ppo_flag_bytes(d->P) + ppo_xbuf_bytes(d)), stats, (unsigned long long*)ws,
             (unsigned long long*)(ws + ppo_flag_bytes(d->P)), ppo_xslot(d->O, d->A, d->K), (int)ppo_xbuf_bytes(d),
-            d->P};
+            d->P, dbg_delay_from_env()};
     return dispatch_dims(d->O, d->A, d->K, "pgm_ppo_update", [&](auto o, auto aa, auto k) -> int {
         constexpr int O = decltype(o)::value, A = decltype(aa)::value, K = decltype(k)::value;
         if constexpr (O > 32) {

@@ -930,6 +930,7 @@ int ppo_update_wide(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params,
                 hipError_t e2 = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                     (int)smem);
                 if (e2 != hipSuccess) return hip_fail(e2, "pgm_ppo_update");
+                if (int rc = check_coresident((const void*)kern, MT, smem, grid, "pgm_ppo_update")) return rc;
                 hipLaunchKernelGGL(kern, dim3(grid), dim3(MT), smem, stream, a);
                 return launch_status("pgm_ppo_update");
             };

@@ -78,6 +78,7 @@ def run(args, device='cuda', rng='device', log=print, runtime=None):
     episode = iteration = 0
     rank, ws = world()
     writer = rank == 0  # every rank holds the same host state; one writes the results tree
+    gen_writer = GenerationWriter() if writer else None
     while iteration < total_num_updates:
         log('\n------------------------------- Warm-up Stage -------------------------------' if episode == 0 else
             f'\n-------------------- Evolutionary Stage: Generation {episode:3} --------------------')
@@ -148,9 +149,9 @@ def run(args, device='cuda', rng='device', log=print, runtime=None):
         iteration = min(iteration + rl_num_updates, total_num_updates)
         rl_num_updates = args.update_iter
         if writer:
-            write_generation(args.save_dir, iteration, args.obj_num, ep, population, opt_graph, elite_batch,
-                             scalarization_batch, all_offspring_batch,
-                             predicted_offspring_objs if args.selection_method == 'prediction-guided' else None)
+            gen_writer.submit(generation_record(
+                args.save_dir, iteration, args.obj_num, ep, population, opt_graph, elite_batch, scalarization_batch,
+                all_offspring_batch, predicted_offspring_objs if args.selection_method == 'prediction-guided' else None))
         t2 = time.perf_counter()
         steps = len(task_batch) * n_its * args.num_steps * args.num_processes
         timing['rl_s'] += t1 - t0
@@ -160,6 +161,7 @@ def run(args, device='cuda', rng='device', log=print, runtime=None):
                                       'rl_s': round(t1 - t0, 4), 'host_s': round(t2 - t1, 4)})
     runtime.materialize(list(ep.sample_batch), dst=0)  # collective: EP snapshots onto the writing rank
     if writer:
+        gen_writer.join()
         write_final(args, ep)
         timing['wall_s'] = time.perf_counter() - t_start
         timing['env_steps_per_s_whole_run'] = timing['train_env_steps'] / timing['wall_s']
@@ -177,14 +179,65 @@ def run(args, device='cuda', rng='device', log=print, runtime=None):
     return ep
 
 
+def generation_record(save_dir, iteration, obj_num, ep, population, opt_graph, elite_batch, scalarization_batch,
+                      all_offspring_batch, predicted_offspring_objs=None):
+    """The data write_generation dumps, detached from the live EP / population / OptGraph (which the next
+    generation mutates): plain lists of the (never mutated) objective / weight arrays."""
+    return dict(save_dir=save_dir, iteration=iteration, obj_num=obj_num, ep_objs=ep.obj_batch,
+                pop_objs=[s.objs for s in population.sample_batch],
+                pop_ids=[s.optgraph_id for s in population.sample_batch],
+                og_weights=list(opt_graph.weights), og_objs=list(opt_graph.objs), og_prev=list(opt_graph.prev),
+                elites=[e.objs for e in elite_batch], weights=[sc.weights for sc in scalarization_batch],
+                predictions=predicted_offspring_objs,
+                offsprings=[s.objs for offs in all_offspring_batch for s in offs])
+
+
+class GenerationWriter:
+    """Writes the per-generation text dumps on a background thread (nothing in the loop reads them back), so
+    the next generation's MOPG launches are not queued behind the formatting; join() before the final files."""
+
+    def __init__(self):
+        import queue
+        import threading
+        self._q = queue.Queue()
+        self._err = None
+        self._t = threading.Thread(target=self._loop, name='pgm-writer', daemon=True)
+        self._t.start()
+
+    def _loop(self):
+        while True:
+            rec = self._q.get()
+            if rec is None:
+                return
+            try:
+                write_generation_record(rec)
+            except BaseException as e:  # surfaced by join()
+                self._err = e
+
+    def submit(self, rec):
+        self._q.put(rec)
+
+    def join(self):
+        self._q.put(None)
+        self._t.join()
+        if self._err is not None:
+            raise self._err
+
+
 def write_generation(save_dir, iteration, obj_num, ep, population, opt_graph, elite_batch, scalarization_batch,
                      all_offspring_batch, predicted_offspring_objs=None):
     """The per-generation text dumps of morl/morl.py:182-221: ep/objs.txt, population/{objs,optgraph}.txt,
     elites/{elites,weights,predictions,offsprings}.txt under save_dir/<iteration>/ ('{:5f}' CSV rows;
     optgraph.txt = node count, 'w;objs;prev' rows, population count, the members' node ids).
     predictions.txt is written only for prediction-guided selection (predicted_offspring_objs not None)."""
-    fmt = _fmt(obj_num)
-    base = os.path.join(save_dir, str(iteration))
+    write_generation_record(generation_record(save_dir, iteration, obj_num, ep, population, opt_graph, elite_batch,
+                                              scalarization_batch, all_offspring_batch, predicted_offspring_objs))
+
+
+def write_generation_record(r):
+    """write_generation from a generation_record."""
+    fmt = _fmt(r['obj_num'])
+    base = os.path.join(r['save_dir'], str(r['iteration']))
 
     def rows(path, vecs):
         with open(path, 'w') as fp:
@@ -192,22 +245,22 @@ def write_generation(save_dir, iteration, obj_num, ep, population, opt_graph, el
                 fp.write((fmt + '\n').format(*v))
 
     os.makedirs(os.path.join(base, 'ep'), exist_ok=True)
-    rows(os.path.join(base, 'ep', 'objs.txt'), ep.obj_batch)
+    rows(os.path.join(base, 'ep', 'objs.txt'), r['ep_objs'])
     os.makedirs(os.path.join(base, 'population'), exist_ok=True)
-    rows(os.path.join(base, 'population', 'objs.txt'), [s.objs for s in population.sample_batch])
+    rows(os.path.join(base, 'population', 'objs.txt'), r['pop_objs'])
     with open(os.path.join(base, 'population', 'optgraph.txt'), 'w') as fp:
-        fp.write('{}\n'.format(len(opt_graph.objs)))
-        for i in range(len(opt_graph.objs)):
-            fp.write((fmt + ';' + fmt + ';{}\n').format(*opt_graph.weights[i], *opt_graph.objs[i], opt_graph.prev[i]))
-        fp.write('{}\n'.format(len(population.sample_batch)))
-        for s in population.sample_batch:
-            fp.write('{}\n'.format(s.optgraph_id))
+        fp.write('{}\n'.format(len(r['og_objs'])))
+        for w, o, pv in zip(r['og_weights'], r['og_objs'], r['og_prev']):
+            fp.write((fmt + ';' + fmt + ';{}\n').format(*w, *o, pv))
+        fp.write('{}\n'.format(len(r['pop_ids'])))
+        for i in r['pop_ids']:
+            fp.write('{}\n'.format(i))
     os.makedirs(os.path.join(base, 'elites'), exist_ok=True)
-    rows(os.path.join(base, 'elites', 'elites.txt'), [e.objs for e in elite_batch])
-    rows(os.path.join(base, 'elites', 'weights.txt'), [sc.weights for sc in scalarization_batch])
-    if predicted_offspring_objs is not None:
-        rows(os.path.join(base, 'elites', 'predictions.txt'), predicted_offspring_objs)
-    rows(os.path.join(base, 'elites', 'offsprings.txt'), [s.objs for offs in all_offspring_batch for s in offs])
+    rows(os.path.join(base, 'elites', 'elites.txt'), r['elites'])
+    rows(os.path.join(base, 'elites', 'weights.txt'), r['weights'])
+    if r['predictions'] is not None:
+        rows(os.path.join(base, 'elites', 'predictions.txt'), r['predictions'])
+    rows(os.path.join(base, 'elites', 'offsprings.txt'), r['offsprings'])
 
 
 def write_final(args, ep):

@@ -65,8 +65,9 @@ class EP:
         arr = np.empty(len(sample_batch), dtype=object)
         arr[:] = sample_batch
         self.sample_batch = np.append(self.sample_batch, arr)
-        for s in sample_batch:
-            self.obj_batch = np.vstack([self.obj_batch, s.objs]) if len(self.obj_batch) > 0 else np.array([s.objs])
+        if sample_batch:  # the reference appends row by row (morl/ep.py:25-28); one vstack gives the same array
+            new = np.array([s.objs for s in sample_batch])
+            self.obj_batch = np.vstack([self.obj_batch, new]) if len(self.obj_batch) > 0 else new
         if len(self.obj_batch) == 0:
             return
         self.index(get_ep_indices(self.obj_batch))

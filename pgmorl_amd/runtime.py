@@ -21,6 +21,8 @@ from ._lib import (Dims, EnvSpec, EnvState, NormState, PGMError, PPOHParams, Rol
 from .layout import ParamLayout
 
 F32, F64, I32 = torch.float32, torch.float64, torch.int32
+UPDATE_TIMEOUT_MSG = ('pgm_ppo_update: a cross-workgroup exchange timed out (workspace word 2P set); the update '
+                      'kernel\'s workgroups were not co-resident -- the parameters are invalid')
 
 
 def _ptr(t):
@@ -32,63 +34,140 @@ def _stream():
 
 
 class TaskBatch:
-    """HBM state of P tasks sharing env, rollout shape and PPO hyper-parameters."""
+    """HBM state of P tasks sharing env, rollout shape and PPO hyper-parameters.
+
+    ``capacity`` (>= P) sizes every buffer once; ``set_active(P)`` then runs the first P task slots without
+    reallocating (the generation loop keeps one TaskBatch for populations of varying size).  The public
+    tensors (``params``, ``ob_mean``, ``obs``, ...) are views of the active slots.  Two packed regions make the
+    per-iteration snapshot and the per-generation load single copies:
+      * ``state``  [3][capacity][L] fp32: params | Adam exp_avg | exp_avg_sq (``params`` = state[0, :P], ...);
+      * ``stats64`` flat fp64: the segments of ``STAT_SEGMENTS`` (task weights and every running statistic),
+        each [capacity][width] contiguous -- a whole-buffer copy is one iteration's record of every task.
+    """
+    # (name, width per task: int, or the attribute of the dims it is); the order is the stats64 layout
+    STAT_SEGMENTS = (('weights', 'K'), ('ob_mean', 'O'), ('ob_var', 'O'), ('ob_count', 0), ('ret_mean', 0),
+                     ('ret_var', 0), ('ret_count', 0), ('obj_mean', 'K'), ('obj_var', 'K'), ('obj_count', 0))
 
     def __init__(self, env_name, P, num_processes=4, num_steps=2048, seed=0, eval_num=1, gamma=0.995,
                  gae_lambda=0.95, use_gae=True, use_proper_time_limits=True, ob_rms=True, obj_rms=True, raw=True,
                  clip_param=0.2, ppo_epoch=10, num_mini_batch=32, value_loss_coef=0.5, entropy_coef=0.0,
-                 max_grad_norm=0.5, adam_eps=1e-5, use_clipped_value_loss=True, device='cuda'):
+                 max_grad_norm=0.5, adam_eps=1e-5, use_clipped_value_loss=True, device='cuda', capacity=None):
         self.spec = envspec.make_spec(env_name)
         sp = self.spec
         self.env_name = env_name
+        self.capacity = Pc = max(P, capacity or P)
         self.P, self.N, self.T = P, num_processes, num_steps
         self.O, self.A, self.K, self.H = sp['obs_dim'], sp['act_dim'], sp['obj_num'], 64
         self.eval_num, self.gamma, self.gae_lambda = eval_num, gamma, gae_lambda
         self.use_gae, self.proper = use_gae, use_proper_time_limits
         self.use_ob_rms, self.use_obj_rms, self.raw = ob_rms, obj_rms, raw
+        self.ppo_epoch, self.num_mini_batch = ppo_epoch, num_mini_batch
         self.dev = torch.device(device)
         self.layout = ParamLayout(self.O, self.A, self.K, self.H)
         L, O, A, K, N, T = self.layout.total, self.O, self.A, self.K, self.N, self.T
-        z = lambda *s, dt=F32: torch.zeros(*s, dtype=dt, device=self.dev)
+        self._full = {}  # name -> full-capacity tensor whose leading dim is the task slot
+
+        def z(name, *s, dt=F32, fill=0.0):
+            t = torch.full((Pc,) + s, fill, dtype=dt, device=self.dev)
+            self._full[name] = t
+            return t
         # spec constants + reset tables (fp64)
         self._spec_t = {k: torch.tensor(np.ascontiguousarray(sp[k]), dtype=F64, device=self.dev)
                         for k in ('d', 'U', 'c', 'V', 'ebase', 'ecoef', 'act_lo', 'act_hi')}
         self.s0_train = torch.tensor(envspec.reset_table(O, seed, N), dtype=F64, device=self.dev)
         self.s0_eval = torch.tensor(envspec.reset_table(O, seed, eval_num), dtype=F64, device=self.dev)
-        # policy + optimiser
-        self.params, self.adam_m, self.adam_v = z(P, L), z(P, L), z(P, L)
-        self.adam_step = z(P, dt=I32)
-        self.lr = z(P)
-        self.weights = z(P, K, dt=F64)
-        # env + running statistics
-        self.s, self.elapsed = z(P, N, O, dt=F64), z(P, N, dt=I32)
-        self.obj_acc, self.obj_valid, self.ret = z(P, N, K, dt=F64), z(P, dt=I32), z(P, N, dt=F64)
-        self.ob_mean, self.ob_var, self.ob_count = z(P, O, dt=F64), z(P, O, dt=F64), z(P, dt=F64)
-        self.ret_mean, self.ret_var, self.ret_count = z(P, dt=F64), z(P, dt=F64), z(P, dt=F64)
-        self.obj_mean, self.obj_var, self.obj_count = z(P, K, dt=F64), z(P, K, dt=F64), z(P, dt=F64)
+        # policy + optimiser: one [3][Pc][L] region
+        self._state = torch.zeros(3, Pc, L, dtype=F32, device=self.dev)
+        z('adam_step', dt=I32)
+        z('lr')
+        # task weights + running statistics: one flat fp64 region (STAT_SEGMENTS)
+        self._seg = []
+        off = 0
+        for name, wd in self.STAT_SEGMENTS:
+            w = getattr(self, wd) if isinstance(wd, str) else 1
+            self._seg.append((name, off, w, isinstance(wd, str)))
+            off += Pc * w
+        self._stats64 = torch.zeros(off, dtype=F64, device=self.dev)
+        # env state
+        z('s', N, O, dt=F64)
+        z('elapsed', N, dt=I32)
+        z('obj_acc', N, K, dt=F64)
+        z('obj_valid', dt=I32)
+        z('ret', N, dt=F64)
         # rollout storage (storage.py:12-30)
-        self.obs = z(P, T + 1, N, O)
-        self.actions, self.logp = z(P, T, N, A), z(P, T, N)
-        self.values, self.returns = z(P, T + 1, N, K), z(P, T + 1, N, K)
-        self.rewards, self.adv = z(P, T, N, K), z(P, T, N)
-        self.masks = torch.ones(P, T + 1, N, dtype=F32, device=self.dev)
-        self.bad_masks = torch.ones(P, T + 1, N, dtype=F32, device=self.dev)
-        self.stats, self.objs = z(P, 3), z(P, K, dt=F64)
-        self.perms = z(ppo_epoch, T * N, dt=I32)
-        self.noise = z(T, N, A)
+        z('obs', T + 1, N, O)
+        z('actions', T, N, A)
+        z('logp', T, N)
+        z('values', T + 1, N, K)
+        z('returns', T + 1, N, K)
+        z('rewards', T, N, K)
+        z('adv', T, N)
+        z('masks', T + 1, N, fill=1.0)
+        z('bad_masks', T + 1, N, fill=1.0)
+        z('stats', 3)
+        z('objs', K, dt=F64)
+        z('_eval_mean', O, dt=F64)
+        z('_eval_var', O, dt=F64)
+        self.perms = torch.zeros(ppo_epoch, T * N, dtype=I32, device=self.dev)
+        self.noise = torch.zeros(T, N, A, dtype=F32, device=self.dev)
         self.hp = PPOHParams(clip_param=clip_param, value_loss_coef=value_loss_coef, entropy_coef=entropy_coef,
                              max_grad_norm=max_grad_norm, adam_eps=adam_eps, beta1=0.9, beta2=0.999,
                              ppo_epoch=ppo_epoch, num_mini_batch=num_mini_batch,
                              use_clipped_value_loss=int(use_clipped_value_loss))
-        self.reset_stats()
-        self._build_structs()
         self._eval_stream, self._eval_done = None, None
-        self._eval_mean, self._eval_var = z(P, O, dt=F64), z(P, O, dt=F64)
-        nws = lib().pgm_ppo_update_workspace_bytes(C.byref(self.dims))
+        nws = lib().pgm_ppo_update_workspace_bytes(C.byref(Dims(Pc, N, T, O, A, K, self.H)))
         self.update_ws = torch.zeros((nws + 7) // 8, dtype=torch.int64, device=self.dev)
         # sticky OR of every update's exchange-timeout word (workspace word 2P, include/pgm_abi.h): a launch
         # whose spin-wait gave up produced invalid parameters; check_update() turns that into PGMError
         self.update_failed = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        self.set_active(P)
+        self.reset_stats()
+
+    def set_active(self, P):
+        """Run the first P task slots (P <= capacity): re-slices the public views and the kernels' dims."""
+        if not 0 < P <= self.capacity:
+            raise ValueError(f'active tasks {P} outside [1, capacity {self.capacity}]')
+        self.P = P
+        for name, t in self._full.items():
+            setattr(self, name, t[:P])
+        self.params, self.adam_m, self.adam_v = self._state[0, :P], self._state[1, :P], self._state[2, :P]
+        for name, off, w, vec in self._seg:
+            v = self._stats64[off:off + self.capacity * w]
+            setattr(self, name, (v.view(self.capacity, w) if vec else v)[:P])
+        self._build_structs()
+
+    @property
+    def state(self):
+        """[3][P][L] view of the active slots (params | exp_avg | exp_avg_sq); strided when P < capacity."""
+        return self._state[:, :self.P]
+
+    def stats64_record(self, out):
+        """Copy the whole flat fp64 statistics region (weights + every running statistic of every slot) into
+        ``out`` (one device copy: an iteration's snapshot record, unpacked on the host by stat_views)."""
+        out.copy_(self._stats64)
+
+    def stat_views(self, flat, P=None):
+        """Host-side split of a stats64 record (numpy [n]) into {name: [P, width] or [P]} arrays."""
+        P = self.P if P is None else P
+        out = {}
+        for name, off, w, vec in self._seg:
+            v = flat[off:off + self.capacity * w]
+            out[name] = (v.reshape(self.capacity, w) if vec else v)[:P]
+        return out
+
+    def load_stats64(self, host_flat):
+        """One H2D copy of a host-built stats64 image (numpy fp64, the stat_views layout)."""
+        self._stats64.copy_(torch.from_numpy(np.ascontiguousarray(host_flat, dtype=np.float64)))
+
+    def new_stats64(self):
+        """A host stats64 image holding fresh RunningMeanStd values (count 1e-4, mean 0, var 1) and zero weights."""
+        flat = np.zeros(self._stats64.numel(), dtype=np.float64)
+        v = self.stat_views(flat, self.capacity)
+        for var in (v['ob_var'], v['ret_var'], v['obj_var']):
+            var[...] = 1.0
+        for cnt in (v['ob_count'], v['ret_count'], v['obj_count']):
+            cnt[...] = 1e-4
+        return flat
 
     # ------------------------------------------------------------------ structs
     def _build_structs(self):
@@ -185,14 +264,20 @@ class TaskBatch:
                                    C.byref(self.c_rb), _ptr(self.stats), _ptr(self.update_ws), _stream()),
               'pgm_ppo_update')
 
-    def check_update(self):
-        """Raise PGMError if any PPO update since the last check timed out in a cross-workgroup exchange
-        (its parameters / Adam state are invalid).  Synchronises with the stream; call it once per
-        generation (MOPGPopulation.run) or after a timed region, not per update."""
-        if int(self.update_failed.item()) != 0:
+    def take_update_failed(self):
+        """True if any PPO update since the last call timed out in a cross-workgroup exchange (its parameters /
+        Adam state are invalid); resets the sticky flag.  Synchronises with the stream."""
+        failed = int(self.update_failed.item()) != 0
+        if failed:
             self.update_failed.zero_()
-            raise PGMError('pgm_ppo_update: a cross-workgroup exchange timed out (workspace word 2P set); '
-                           'the update kernel\'s workgroups were not co-resident -- the parameters are invalid')
+        return failed
+
+    def check_update(self):
+        """Raise PGMError if any PPO update since the last check timed out (take_update_failed).  Call it once
+        per generation or after a timed region, not per update.  Multi-GPU callers share the flag across ranks
+        first (MOPGPopulation.run) so that every rank raises together."""
+        if self.take_update_failed():
+            raise PGMError(UPDATE_TIMEOUT_MSG)
 
     def evaluate(self, ob_mean=None, ob_var=None, out=None):
         mean = self.ob_mean if ob_mean is None else ob_mean

@@ -53,15 +53,22 @@ class WeightedSumScalarization:
 class DeviceSnapshot:
     """Parameters + Adam state of one task, kept on the device of the rank that produced it.
 
+    Snapshots are IMMUTABLE once taken: the per-iteration copies of a generation live in one device arena
+    ([iterations][3][tasks][L], ``MOPGPopulation.run``) and a snapshot is an index into it (``in_arena``), so
+    taking, cloning (Task / Sample.copy_from) and dropping snapshots moves no bytes.  Tensors are views,
+    created on first use.
+
     Multi-GPU: every rank holds the same Samples (identical host state), but a snapshot's tensors live
-    only on its ``owner`` rank; elsewhere it is a remote handle (``data is None``) that
-    ``MOPGPopulation`` moves to the rank that next trains it, or to rank 0 for the final artefacts
-    (shard.move_rows: bytes scale with the moved snapshots, not with the population).  owner None =
-    local (single process, or replicated on every rank like the warm-up policies)."""
+    only on its ``owner`` rank; elsewhere it is a remote handle (no data) that ``MOPGPopulation`` moves to the
+    rank that next trains it, or to rank 0 for the final artefacts (shard.move_rows: bytes scale with the
+    moved snapshots, not with the population).  owner None = local (single process, or replicated on every
+    rank like the warm-up policies)."""
 
     def __init__(self, layout, params, adam_m, adam_v, adam_step, owner=None):
         self.layout = layout
-        self.data = None if params is None else (params, adam_m, adam_v)
+        self._data = None if params is None else (params, adam_m, adam_v)
+        self._arena = None  # (arena [I][3][Pl][L], iteration, slot) -- the block view is made on demand
+        self._blk = None
         self.adam_step = int(adam_step)
         self.owner = owner
 
@@ -69,32 +76,59 @@ class DeviceSnapshot:
     def remote(cls, layout, adam_step, owner):
         return cls(layout, None, None, None, adam_step, owner)
 
+    @classmethod
+    def in_arena(cls, layout, arena, i, slot, adam_step, owner=None):
+        """Snapshot = row (i, :, slot) of a generation's arena (no copy)."""
+        s = cls(layout, None, None, None, adam_step, owner)
+        s._arena = (arena, i, slot)
+        return s
+
     @property
     def is_local(self):
-        return self.data is not None
+        return self._data is not None or self._arena is not None or self._blk is not None
+
+    def block(self):
+        """[3, L] params | exp_avg | exp_avg_sq (a view when the snapshot lives in an arena or was adopted)."""
+        if self._blk is None:
+            if self._arena is not None:
+                ar, i, q = self._arena
+                self._blk = ar[i, :, q]
+            elif self._data is not None:
+                self._blk = torch.stack(self._data)
+            else:
+                raise RuntimeError(f'snapshot lives on rank {self.owner}: move it first (MOPGPopulation.materialize)')
+        return self._blk
+
+    @property
+    def data(self):
+        if self._data is None and (self._arena is not None or self._blk is not None):
+            b = self.block()
+            self._data = (b[0], b[1], b[2])
+        return self._data
 
     def _part(self, i):
-        if self.data is None:
+        d = self.data
+        if d is None:
             raise RuntimeError(f'snapshot lives on rank {self.owner}: move it first (MOPGPopulation.materialize)')
-        return self.data[i]
+        return d[i]
 
     params = property(lambda self: self._part(0))
     adam_m = property(lambda self: self._part(1))
     adam_v = property(lambda self: self._part(2))
 
     def stacked(self):
-        """[3, L] params | exp_avg | exp_avg_sq (a new tensor)."""
-        return torch.stack([self.params, self.adam_m, self.adam_v])
+        """[3, L] params | exp_avg | exp_avg_sq (read-only: snapshots are never written)."""
+        return self.block()
 
     def adopt(self, rows):
-        """Materialise a remote handle from a received [3, L] block (it becomes local)."""
-        self.data = (rows[0].clone(), rows[1].clone(), rows[2].clone())
+        """Materialise a remote handle from a received [3, L] block (it becomes a local replica)."""
+        self._blk, self._data, self._arena = rows, None, None
 
     def clone(self):
-        if self.data is None:
-            return DeviceSnapshot.remote(self.layout, self.adam_step, self.owner)
-        return DeviceSnapshot(self.layout, self.params.clone(), self.adam_m.clone(), self.adam_v.clone(),
-                              self.adam_step, self.owner)
+        """Snapshots are immutable: a clone shares the device storage (no copy)."""
+        c = DeviceSnapshot(self.layout, None, None, None, self.adam_step, self.owner)
+        c._data, c._arena, c._blk = self._data, self._arena, self._blk
+        return c
 
 
 class PolicyHandle:
@@ -131,11 +165,23 @@ class AgentHandle:
 
 class Sample:
     def __init__(self, env_params, actor_critic, agent, objs=None, optgraph_id=None):
-        self.env_params = env_params
+        self._env_params, self._envp_fn = env_params, None
         self.actor_critic = actor_critic
         self.agent = agent
         self.objs = objs
         self.optgraph_id = optgraph_id
+
+    @property
+    def env_params(self):
+        """{'ob_rms', 'ret_rms', 'obj_rms'} RunningMeanStd copies (morl/sample.py:12).  An offspring built by
+        MOPGPopulation.run unpacks them from its host record on first access (most offspring never need them)."""
+        if self._envp_fn is not None:
+            self._env_params, self._envp_fn = self._envp_fn(), None
+        return self._env_params
+
+    @env_params.setter
+    def env_params(self, value):
+        self._env_params, self._envp_fn = value, None
 
     @property
     def snapshot(self):
@@ -144,6 +190,13 @@ class Sample:
     @classmethod
     def from_snapshot(cls, snap, env_params, objs=None, optgraph_id=None):
         return cls(env_params, PolicyHandle(snap), AgentHandle(snap), objs, optgraph_id)
+
+    @classmethod
+    def lazy(cls, snap, env_params_fn, objs=None, optgraph_id=None):
+        """A Sample whose env_params are built by env_params_fn() on first access."""
+        s = cls(None, PolicyHandle(snap), AgentHandle(snap), objs, optgraph_id)
+        s._envp_fn = env_params_fn
+        return s
 
     @classmethod
     def from_reference(cls, ref_sample, layout, device='cuda'):

@@ -1,11 +1,18 @@
 """Task sharding across GPUs and the generation-boundary exchange.
 
 Tasks never interact inside a generation (morl/mopg.py:60-182 touches only its own task), so each
-rank (one process per GPU) owns a contiguous block of ceil(P/G) tasks for the whole generation and
-the only collective is an all-gather at the generation boundary (morl/morl.py:90-125), where every
-rank needs every task's offspring (objective vectors, running statistics and the policy / Adam
-snapshot) to run the identical host EP / OptGraph / selection.  With the "nccl" backend (RCCL over
-xGMI on ROCm) the payload stays in HBM; the same code runs on "gloo" with CPU tensors (tests).
+rank (one process per GPU) owns a contiguous block of ceil(P/G) tasks for the whole generation and the
+data path has no collective.  At the generation boundary (morl/morl.py:90-125) only the fp64 RECORDS of
+every offspring (objective vector, running statistics, Adam step) are all-gathered (``allgather_rows``,
+a few KB), so every rank runs the identical host EP / OptGraph / selection.  Policy / Adam snapshots stay
+on the rank that produced them and move point-to-multipoint (``move_rows``) only when a later generation
+trains them on another rank, or when rank 0 writes the final EP policies.
+
+Snapshot memory model: ``DeviceSnapshot.owner`` stays the PRODUCING rank for the snapshot's whole life.
+A rank that receives a moved snapshot adopts it as an extra local replica (``DeviceSnapshot.adopt``);
+the producer keeps its original, so a moved elite is live on two ranks until both Samples are dropped.
+With the "nccl" backend (RCCL over xGMI on ROCm) the payloads stay in HBM; the same code runs on "gloo"
+with CPU tensors (tests).
 """
 import torch
 import torch.distributed as dist
@@ -84,3 +91,9 @@ def move_rows(moves, local_rows, shape, dtype, device, group=None):
             if moves[k][1] == rank:
                 got[k] = parts[s][j].clone()
     return got, buf.numel() * buf.element_size()
+
+
+def any_rank(flag, device):
+    """Collective: True on EVERY rank when ``flag`` is true on any rank (a failure one rank detected must end
+    the generation on all ranks together, before anyone enters the next collective)."""
+    return allreduce_max([1.0 if flag else 0.0], device)[0] > 0.0

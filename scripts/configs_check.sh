@@ -6,7 +6,7 @@ OUT=$(pwd)/gpurun_out
 mkdir -p $OUT
 run() {  # name, bench args...
   local n=$1; shift
-  timeout -k 10 300 python -u bench.py --no-cpu-baseline "$@" > $OUT/bench_${TAG}_$n.json 2> $OUT/bench_${TAG}_$n.err || { echo BENCH $n FAILED; tail -5 $OUT/bench_${TAG}_$n.err; return 1; }
+  timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-whole-run "$@" > $OUT/bench_${TAG}_$n.json 2> $OUT/bench_${TAG}_$n.err || { echo BENCH $n FAILED; tail -5 $OUT/bench_${TAG}_$n.err; return 1; }
   python -c "import json;d=json.load(open('$OUT/bench_${TAG}_$n.json'));r=d['roofline'];print('$n', round(d['value']/1e6,3),'M/s', round(d['ms_per_step'],2),'ms/step', r['kernel'], round(r['avg_launch_ms'],3),'ms frac', round(r['frac'],3))"
 }
 run walker_p40 && \

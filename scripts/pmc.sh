@@ -10,7 +10,7 @@ mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 400 rocprofv3 --pmc $C --kernel-trace -d $OUT/$C -o $C --output-format csv -- \
-      python $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline "$@" > $OUT/$C.log 2>&1 \
+      python $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-whole-run "$@" > $OUT/$C.log 2>&1 \
       || { echo "PMC $C FAILED"; tail -20 $OUT/$C.log; exit 1; }
 done
 python $R/scripts/pmc_summary.py $OUT "$@" > $R/gpurun_out/pmc_$TAG.json && cat $R/gpurun_out/pmc_$TAG.json

@@ -1,0 +1,88 @@
+"""The update kernels' cross-workgroup exchanges under provoked delays, and the launcher's co-residency check.
+
+Every row-split update (MODE 2: each tower on two workgroups; t16: on four) hands gradient images over through
+16-B sc1 publishes + tagged flag granules, and the two towers hand their squared norms over through tagged 8-B
+granules, all double-buffered by Adam-step parity (pgm_common.hpp ppo_norm_granule).  PGM_TEST_DELAY stalls ONE
+workgroup for a fixed number of cycles at one hand-off point of one step:
+  where 0 -- before it publishes its gradient image (its partners spin on its flag),
+  where 1 -- between its image flag store and its own partner poll (the partners run ahead to the next step),
+  where 2 -- between its tower-norm granule store and its poll: the other tower can finish this step and
+             publish the NEXT step's norm before the delayed poll looks -- the order a single-buffered granule
+             lost (the poll would see the next tag and spin until the timeout word).
+Each case must leave the exchange-timeout word clear (check_update) and the parameters equal to the oracle's.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ppo as oppo
+from pgmorl_amd._lib import PGMError
+
+from .test_gpu_kernels import _close, _update_setup
+
+pytestmark = pytest.mark.gpu
+
+DELAY = 4_000_000  # shader cycles (~2 ms): far beyond one Adam step, far below the 2^26-spin timeout
+
+
+def _run_update(env, P, T, N, E, M, split, delay, monkeypatch):
+    monkeypatch.setenv('PGM_UPDATE_SPLIT', split)
+    if delay is not None:
+        monkeypatch.setenv('PGM_TEST_DELAY', ':'.join(str(x) for x in delay))
+    args, spec, tb, pols, data, perms = _update_setup(env, P, T, N, E, M, seed=17)
+    obs, actions, logp, values, returns, adv = data
+    lr = 3e-4
+    tb.lr.fill_(lr)
+    tb.ppo_update(torch.stack(perms).numpy())
+    tb.check_update()  # PGMError if any spin-wait gave up
+    for p in range(P):
+        agent = oppo.PPO(pols[p], args.clip_param, E, M, args.value_loss_coef, args.entropy_coef, lr=lr, eps=1e-5,
+                         max_grad_norm=args.max_grad_norm)
+        ro = oppo.RolloutStorage(T, N, spec['obs_dim'], spec['act_dim'], spec['obj_num'])
+        ro.obs.copy_(torch.from_numpy(obs[p]).double())
+        ro.actions.copy_(actions[p].double())
+        ro.action_log_probs.copy_(logp[p].double().unsqueeze(-1))
+        ro.value_preds.copy_(values[p].double())
+        ro.returns.copy_(returns[p].double())
+        for e in range(E):
+            for mbt in ro.minibatches(adv[p].double(), M, perms[e]):
+                agent.minibatch_step(*mbt)
+        _close(tb.params[p].cpu(), tb.layout.flatten(pols[p].state_dict(), dtype=np.float64), 2e-6, 1e-5,
+               f'task {p}: params with delay {delay}')
+        assert int(tb.adam_step[p]) == E * M
+
+
+# block ids: MODE 2 (split '2') groups 16 blocks per 4 tasks, block r = half r >> 3 of tower r & 1 of task
+# 4 g + ((r & 7) >> 1); t16 (split '4') groups 32, part r >> 3.  Blocks 0 / 1: task 0's critic / actor, part 0;
+# 8 / 9: part 1; 25: actor part 3 (t16 only).
+CASES = [('2', 0, 0), ('2', 9, 0), ('2', 8, 1), ('2', 1, 1), ('2', 0, 2), ('2', 9, 2),
+         ('4', 0, 0), ('4', 25, 0), ('4', 17, 1), ('4', 0, 2), ('4', 1, 2), ('4', 24, 2)]
+
+
+@pytest.mark.parametrize('split,block,where', CASES)
+def test_delayed_handoff_keeps_parity(gpu, split, block, where, monkeypatch):
+    # Walker, 2 tasks, mb = 256 (the single-tile specialisations of both kernels), 4 Adam steps; the stall
+    # hits step 1 (both parities are exercised before and after it)
+    _run_update('MO-Walker2d-v2', 2, 256, 4, 1, 4, split, (1, block, where, DELAY), monkeypatch)
+
+
+@pytest.mark.parametrize('split', ['2', '4'])
+def test_delay_on_last_step_and_ragged_grid(gpu, split, monkeypatch):
+    # Hopper-v3 (3 objectives), 5 tasks (a ragged last group of the block map), multi-pass minibatches
+    # (mb = 128 with N = 2: not the single-tile path); stall the last task's actor part 0 on the last step
+    P = 5
+    block = (16 if split == '2' else 32) * (P // 4) + 2 * (P % 4 - 1) + 1
+    _run_update('MO-Hopper-v3', P, 128, 2, 1, 2, split, (1, block, 2, DELAY), monkeypatch)
+
+
+def test_coresidency_check_refuses_an_oversized_grid(gpu, monkeypatch):
+    """The launcher refuses (PGM_E_UNSUPPORTED -> PGMError) a grid whose workgroups cannot all be resident:
+    PGM_TEST_RESIDENT_CUS pretends the device has fewer CUs than the grid's workgroups (one per CU)."""
+    monkeypatch.setenv('PGM_UPDATE_SPLIT', '2')
+    monkeypatch.setenv('PGM_TEST_RESIDENT_CUS', '8')  # MODE 2 for 2 tasks = 16 workgroups
+    args, spec, tb, pols, data, perms = _update_setup('MO-Walker2d-v2', 2, 64, 4, 1, 1, seed=3)
+    with pytest.raises(PGMError, match='co-resident'):
+        tb.ppo_update(torch.stack(perms).numpy())
+    monkeypatch.setenv('PGM_TEST_RESIDENT_CUS', '16')  # exactly fits: runs
+    tb.ppo_update(torch.stack(perms).numpy())
+    tb.check_update()

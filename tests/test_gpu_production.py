@@ -29,14 +29,16 @@ from .test_gpu_kernels import (_batch_with_policies, _close, _noise_fn, _oracle_
 
 pytestmark = pytest.mark.gpu
 
-CONFIGS = [('MO-Walker2d-v2', 40, 4), ('MO-HalfCheetah-v2', 20, 4), ('MO-Hopper-v3', 27, 4), ('MO-Humanoid-v2', 20, 8)]
+CONFIGS = [('MO-Hopper-v2', 5, 1), ('MO-Walker2d-v2', 40, 4), ('MO-HalfCheetah-v2', 20, 4), ('MO-Hopper-v3', 27, 4),
+           ('MO-Humanoid-v2', 20, 8)]
+MB = {1: 64, 4: 256, 8: 512}  # production minibatch rows T * N / 32 (config 0 runs N = 1: 64 rows)
 
 
 @pytest.mark.parametrize('env,P,N', CONFIGS)
 def test_production_update_all_tasks(gpu, env, P, N):
     """One launch of pgm_ppo_update over the whole per-GPU population, 2 Adam steps of a production-size
     minibatch (mb = 256 / 512 rows); parameters, Adam moments, step and loss stats of EVERY task."""
-    mb = 256 if N == 4 else 512
+    mb = MB[N]
     M, E = 2, 1
     T = mb * M // N
     args, spec, tb, pols, data, perms = _update_setup(env, P, T, N, E, M, seed=21)
@@ -99,12 +101,13 @@ def test_production_rollout_all_tasks(gpu, env, P, N):
         np.testing.assert_array_equal(masks[p], ro.masks[..., 0].numpy())
 
 
-@pytest.mark.parametrize('env,P,N', [('MO-Walker2d-v2', 40, 4), ('MO-Hopper-v3', 27, 4)])
+@pytest.mark.parametrize('env,P,N', [('MO-Walker2d-v2', 40, 4), ('MO-Hopper-v3', 27, 4), ('MO-Hopper-v2', 5, 1)])
 def test_production_iteration(gpu, env, P, N):
-    """A full MOPG iteration (rollout, GAE, advantages, MODE-2 update over the production grid, evaluation)
-    at the production population with the reference's RNG draws; tasks spread over the grid vs the oracle
-    MOPG_worker (morl/mopg.py:60-182)."""
-    T, E, M = 64, 1, 1  # mb = 256 rows, one Adam step
+    """A full MOPG iteration (rollout, GAE, advantages, the update kernel the launcher picks for this P -- MODE 2
+    for Walker P = 40, 16-row tiles on four workgroups per tower for Hopper-v3 P = 27 and config 0's Hopper-v2
+    P = 5 -- and the evaluation) at the production population with the reference's RNG draws; tasks spread
+    over the grid vs the oracle MOPG_worker (morl/mopg.py:60-182)."""
+    T, E, M = 64, 1, 1  # one production-size minibatch (mb = T * N: 256 rows, config 0's N = 1: 64), one Adam step
     args = small_args(env, num_steps=T, num_processes=N, ppo_epoch=E, num_mini_batch=M, num_env_steps=T * N * 10)
     spec = envspec.make_spec(env)
     A, B = spec['act_dim'], T * N
@@ -135,7 +138,7 @@ def test_production_iteration(gpu, env, P, N):
         _close(objs[p], off.objs, 1e-3, 1e-4, f'{env} task {p}: eval objs')
 
 
-@pytest.mark.parametrize('env,P,eval_num', [('MO-Walker2d-v2', 40, 1), ('MO-HalfCheetah-v2', 20, 1),
+@pytest.mark.parametrize('env,P,eval_num', [('MO-Hopper-v2', 5, 1), ('MO-Walker2d-v2', 40, 1), ('MO-HalfCheetah-v2', 20, 1),
                                              ('MO-Hopper-v3', 27, 2), ('MO-Humanoid-v2', 20, 6)])
 def test_production_eval_all_tasks(gpu, env, P, eval_num):
     """pgm_eval over the production population (Humanoid: eval_num 6, scripts/humanoid-v2.py:45), every task.
@@ -167,3 +170,62 @@ def test_production_eval_all_tasks(gpu, env, P, eval_num):
     atol, rtol = (1e-4, 2e-5) if spec['obs_dim'] <= 48 else (1e-3, 2e-4)
     for p in range(P):
         _close(objs[p], oracle_evaluation(args, spec, s0_eval, pols[p], rms[p]), atol, rtol, f'{env} task {p}: objs')
+
+
+def test_config0_full_iteration_shape(gpu):
+    """Config 0 at its real shape -- Hopper-v2, P = 5, N = 1, T = 2048, M = 32 (minibatch 64: the t16 path with
+    one 16-row tile per row part, not the single-tile specialisation), two epochs -- one launch of pgm_ppo_update
+    for every task vs the oracle, then a full TaskBatch.iteration (rollout of 2,048 steps, GAE, advantages, that
+    update, evaluation) for every task vs oracle.mopg.mopg_worker (scripts/hopper-v2.py:38, morl/mopg.py:60-182)."""
+    env, P, N, T, E, M = 'MO-Hopper-v2', 5, 1, 2048, 2, 32
+    args, spec, tb, pols, data, perms = _update_setup(env, P, T, N, E, M, seed=31)
+    obs, actions, logp, values, returns, adv = data
+    lr = 3e-4
+    tb.lr.fill_(lr)
+    tb.ppo_update(torch.stack(perms).numpy())
+    tb.check_update()
+    params, steps = tb.params.cpu(), tb.adam_step.cpu()
+    for p in range(P):
+        agent = oppo.PPO(pols[p], args.clip_param, E, M, args.value_loss_coef, args.entropy_coef, lr=lr, eps=1e-5,
+                         max_grad_norm=args.max_grad_norm)
+        ro = oppo.RolloutStorage(T, N, spec['obs_dim'], spec['act_dim'], spec['obj_num'])
+        ro.obs.copy_(torch.from_numpy(obs[p]).double())
+        ro.actions.copy_(actions[p].double())
+        ro.action_log_probs.copy_(logp[p].double().unsqueeze(-1))
+        ro.value_preds.copy_(values[p].double())
+        ro.returns.copy_(returns[p].double())
+        for e in range(E):
+            for mbt in ro.minibatches(adv[p].double(), M, perms[e]):
+                agent.minibatch_step(*mbt)
+        assert int(steps[p]) == E * M
+        _close(params[p], tb.layout.flatten(pols[p].state_dict(), dtype=np.float64), 5e-6, 1e-4,
+               f'config 0 task {p}: params after {E * M} Adam steps')
+    # the whole iteration at the production shape (one epoch: the oracle's 2,048-step rollout dominates)
+    E = 1
+    args = small_args(env, num_steps=T, num_processes=N, ppo_epoch=E, num_mini_batch=M, num_env_steps=T * N * 10)
+    A, B = spec['act_dim'], T * N
+    tb = TaskBatch(env, P, num_processes=N, num_steps=T, ppo_epoch=E, num_mini_batch=M)
+    fn = _noise_fn(T, N, A, E, B)
+    w = weights_grid(spec['obj_num'], P)
+    torch.manual_seed(0)
+    samples = [initial_sample(args, spec) for _ in range(P)]
+    for s in samples:
+        with torch.no_grad():
+            for prm in s.actor_critic.parameters():
+                prm.copy_(prm.float().double())
+    for p, s in enumerate(samples):
+        tb.set_task(p, s.actor_critic.state_dict(), {}, s.env_params, w[p])
+    tb.env_reset()
+    total = int(args.num_env_steps) // T // N
+    noise, perms = fn(0)
+    tb.iteration(0, oppo.linear_lr(0, total, args.lr), noise=noise.float(), perms=torch.stack(perms).numpy(),
+                 carry=False)
+    tb.check_update()
+    objs, params = tb.objs.cpu().numpy(), tb.params.cpu().numpy()
+    s0_train = envspec.reset_table(spec['obs_dim'], 0, N)
+    s0_eval = envspec.reset_table(spec['obs_dim'], 0, 1)
+    for p in range(P):
+        off = mopg_worker(args, spec, s0_train, s0_eval, samples[p], w[p], 0, 1, noise_fn=fn)[0]
+        _close(params[p], tb.layout.flatten(off.actor_critic.state_dict(), dtype=np.float64), 5e-5, 1e-3,
+               f'config 0 task {p}: params after a full iteration')
+        _close(objs[p], off.objs, 1e-2, 1e-4, f'config 0 task {p}: eval objs')

@@ -42,27 +42,55 @@ def test_from_reference_roundtrip():
         torch.testing.assert_close(st[i]['exp_avg'], ref_st[i]['exp_avg'].float().double(), rtol=0, atol=0)
         assert float(st[i]['step']) == float(ref_st[i]['step'])
     np.testing.assert_array_equal(dev.objs, ref.objs)
-    # Task deep-copies its elite (morl/task.py:9-10): mutating the task's snapshot leaves the elite alone
+    # Task copies its elite (morl/task.py:9-10).  Snapshots are immutable (the device never writes one: a task's
+    # training state lives in the TaskBatch), so the copy shares the device storage; the host fields are copies
     task = Task(dev, WeightedSumScalarization(2, [0.3, 0.7]))
-    task.sample.snapshot.params.add_(1.0)
-    assert not torch.equal(task.sample.snapshot.params, dev.snapshot.params)
+    assert task.sample.snapshot.params.data_ptr() == dev.snapshot.params.data_ptr()
+    assert task.sample.env_params is not dev.env_params and task.sample.objs is not dev.objs
+    np.testing.assert_array_equal(task.sample.objs, dev.objs)
     assert float(task.scalarization.evaluate(torch.tensor([2.0, 4.0]))) == 0.3 * 2.0 + 0.7 * 4.0
 
 
-def test_record_unpack_matches_fields():
-    args = argparse.Namespace(ob_rms=True, obj_rms=True)
+def test_stats64_record_layout_and_unpack():
+    """TaskBatch's flat fp64 statistics region: the per-task views, a whole-region record split back on the
+    host (stat_views), set_active re-slicing without reallocation, and the RunningMeanStd unpack of a slot."""
+    from pgmorl_amd.runtime import TaskBatch
+    tb = TaskBatch('MO-Hopper-v3', 3, num_processes=2, num_steps=8, device='cpu', capacity=5)
+    O, K = tb.O, tb.K
+    assert tb.capacity == 5 and tb.params.shape == (3, tb.layout.total) and tb.ob_mean.shape == (3, O)
+    assert float(tb.ob_var[2, 0]) == 1.0 and float(tb.obj_count[1]) == 1e-4  # fresh RunningMeanStd
+    base = tb.obs.data_ptr()
+    tb.set_active(5)
+    assert tb.obs.shape[0] == 5 and tb.obs.data_ptr() == base
+    tb.set_active(4)
+    for p in range(4):
+        tb.ob_mean[p] = torch.arange(O, dtype=torch.float64) + 100 * p
+        tb.obj_var[p] = torch.tensor([1.5, 2.5, 3.5]) * (p + 1)
+        tb.ret_count[p] = 7.0 + p
+        tb.weights[p] = torch.tensor([0.2, 0.3, 0.5], dtype=torch.float64)
+    rec = torch.empty_like(tb._stats64)
+    tb.stats64_record(rec)
+    st = tb.stat_views(rec.numpy())
+    assert st['ob_mean'].shape == (4, O) and st['ret_count'].shape == (4,)
+    np.testing.assert_array_equal(st['ob_mean'][3], np.arange(O) + 300)
+    np.testing.assert_array_equal(st['obj_var'][1], [3.0, 5.0, 7.0])
+    np.testing.assert_array_equal(st['weights'][2], [0.2, 0.3, 0.5])
     pop = MOPGPopulation.__new__(MOPGPopulation)
-    pop.args = args
-    O, K = 3, 2
-    rec = np.arange(3 * K + 2 * O + 6, dtype=np.float64)
-    objs, ep, step = pop._unpack(rec, O, K)
-    np.testing.assert_array_equal(objs, [0, 1])
-    np.testing.assert_array_equal(ep['ob_rms'].mean, [2, 3, 4])
-    np.testing.assert_array_equal(ep['ob_rms'].var, [5, 6, 7])
-    assert ep['ob_rms'].count == 8 and float(ep['ret_rms'].mean) == 9 and ep['ret_rms'].count == 11
-    np.testing.assert_array_equal(ep['obj_rms'].mean, [12, 13])
-    np.testing.assert_array_equal(ep['obj_rms'].var, [14, 15])
-    assert ep['obj_rms'].count == 16 and step == 17
+    pop.args = argparse.Namespace(ob_rms=True, obj_rms=True)
+    ep = pop._env_params(st, 2, O, K)
+    np.testing.assert_array_equal(ep['ob_rms'].mean, np.arange(O) + 200)
+    assert ep['ret_rms'].count == 9.0 and ep['ob_rms'].var.shape == (O,)
+    np.testing.assert_array_equal(ep['obj_rms'].var, [4.5, 7.5, 10.5])
+    # an all-gathered record row (multi-GPU remote offspring) splits into the same fields
+    row = np.concatenate([[9.0, 8.0, 7.0], st['ob_mean'][1], st['ob_var'][1], [st['ob_count'][1]],
+                          [st['ret_mean'][1], st['ret_var'][1], st['ret_count'][1]], st['obj_mean'][1],
+                          st['obj_var'][1], [st['obj_count'][1]]])
+    ep2 = pop._env_params(MOPGPopulation._split_record(row, O, K), 0, O, K)
+    ep1 = pop._env_params(st, 1, O, K)
+    for k in ep1:
+        np.testing.assert_array_equal(ep1[k].mean, ep2[k].mean)
+        np.testing.assert_array_equal(ep1[k].var, ep2[k].var)
+        assert ep1[k].count == ep2[k].count
 
 
 def test_host_draws_and_lr_schedule():

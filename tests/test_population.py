@@ -53,6 +53,34 @@ def _history(K, seed, gens=3):
     return og, offspring
 
 
+def test_population2d_buffers_known_answer():
+    """Angular buffer bucketing and the per-buffer distance order (morl/population_2d.py:169-183)."""
+    pop = population.Population2d(_args(2, pbuffer_num=4, pbuffer_size=2))
+    # angle to the obj1 axis: buckets of pi/8; bucket 0 holds points near the obj1 axis
+    pts = [(0.1, 5.0), (0.2, 9.0), (0.05, 1.0), (5.0, 5.0), (9.0, 0.1), (3.0, -1.0), (0.0, 4.0), (4.0, 4.1)]
+    pop.update([_S(p) for p in pts])
+    got = [tuple(s.objs) for s in pop.sample_batch]
+    # bucket 0 holds (0.2,9) > (0.1,5) > (0.05,1): the nearest is dropped (size 2); (0,4) has a zero
+    # coordinate and (3,-1) a negative one, so neither enters any buffer
+    assert (0.2, 9.0) == got[0] and (0.1, 5.0) == got[1] and (0.05, 1.0) not in got
+    assert (0.0, 4.0) not in got and (3.0, -1.0) not in got
+    assert set(got) == {(0.2, 9.0), (0.1, 5.0), (5.0, 5.0), (4.0, 4.1), (9.0, 0.1)}
+    ora = ref.Population2d(4, 2)
+    ora.update([_S(p) for p in pts])
+    assert got == [tuple(s.objs) for s in ora.sample_batch]
+
+
+def test_population3d_buffer_directions():
+    """The 3-D grid-direction buffers (morl/population_3d.py:122-125): 210 of them for --pbuffer-num 20 (the
+    Hopper-v3 reading of SURVEY.md §8(d)), and find_buffer_id equal to the loop restatement."""
+    pop = population.Population3d(_args(3, pbuffer_num=20))
+    assert pop.pbuffer_num == 210
+    ora = ref.Population3d(3, 20, 2)
+    rng = np.random.RandomState(1)
+    for f in rng.rand(200, 3):
+        assert pop.find_buffer_id(f) == ora.buffer_id(f)
+
+
 @pytest.mark.parametrize('K,seed', [(2, 0), (2, 1), (3, 0), (3, 1)])
 def test_population_update_matches_oracle(K, seed):
     _, offspring = _history(K, seed)

@@ -198,3 +198,55 @@ def _place_worker(rank, ws, port, P, errq):
 @pytest.mark.parametrize('ws,P', [(2, 5), (2, 8), (3, 7)])
 def test_place_moves_only_relocated_snapshots_gloo(ws, P):
     _spawn(_place_worker, ws, P)
+
+
+def _failure_worker(rank, ws, port, failing, P, errq):
+    """MOPGPopulation.check_generation over gloo: the rank(s) in ``failing`` saw an exchange timeout in their update;
+    every rank -- also one that owns no task of the generation (tb None) -- must raise PGMError together and then
+    still complete a collective (nobody is left blocked in one)."""
+    try:
+        import argparse
+        from pgmorl_amd._lib import PGMError
+        from pgmorl_amd.mopg import MOPGPopulation
+        os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+        dist.init_process_group('gloo', rank=rank, world_size=ws)
+
+        class _TB:  # stands in for TaskBatch's sticky timeout flag
+            def take_update_failed(self):
+                return rank in failing
+
+        lo, hi = task_block(P, rank, ws)
+        rt = MOPGPopulation(argparse.Namespace(env_name='MO-Hopper-v2'), device='cpu')
+        raised = False
+        try:
+            rt.check_generation(_TB() if hi > lo else None)
+        except PGMError:
+            raised = True
+        assert raised == bool(failing), (rank, raised)
+        dist.barrier()  # every rank got here: no one hangs in the check's collective
+        dist.destroy_process_group()
+        if raised:
+            raise SystemExit(3)  # exits non-zero like the generation loop would
+    except SystemExit:
+        raise
+    except Exception as e:  # surfaced by the parent
+        errq.put(f'rank {rank}: {e!r}')
+        raise
+
+
+@pytest.mark.parametrize('ws,failing,P', [(2, (1,), 4), (3, (0,), 2), (3, (), 5), (2, (0, 1), 2)])
+def test_update_failure_raises_on_every_rank_gloo(ws, failing, P):
+    ctx = mp.get_context('spawn')
+    errq = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_failure_worker, args=(r, ws, port, failing, P, errq)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    errs = []
+    while not errq.empty():
+        errs.append(errq.get())
+    assert not errs, errs
+    want = 3 if failing else 0
+    assert all(p.exitcode == want for p in procs), [p.exitcode for p in procs]

@@ -233,10 +233,13 @@ def whole_run(args, iter_value):
     ns = get_parser().parse_args(merge_argv(argv))
     old = torch.get_default_dtype()
     torch.set_default_dtype(torch.float64)  # morl/run.py:53
+    import contextlib
+    import io
     try:
-        t0 = time.perf_counter()
-        ep = morl_run(ns, device='cuda', rng='device', log=lambda *m: None)
-        wall = time.perf_counter() - t0
+        with contextlib.redirect_stdout(io.StringIO()):  # the selection's 'Too few candidates' notes
+            t0 = time.perf_counter()
+            ep = morl_run(ns, device="cuda", rng="device", log=None)
+            wall = time.perf_counter() - t0
     finally:
         torch.set_default_dtype(old)
     tm = ep.timing
@@ -244,7 +247,9 @@ def whole_run(args, iter_value):
     import shutil
     shutil.rmtree(save, ignore_errors=True)
     v = tm['train_env_steps'] / wall
-    return {'value': v, 'unit': 'env steps/sec', 'wall_s': wall, 'train_env_steps': tm['train_env_steps'],
+    per_gen = [(g['rl_s'], g['host_s']) for g in tm['generations']]
+    return {'value': v, 'unit': 'env steps/sec', 'wall_s': wall, 'final_s': tm.get('final_s'),
+            'generation_rl_host_s': per_gen, 'train_env_steps': tm['train_env_steps'],
             'generations': len(tm['generations']), 'mopg_s': tm['rl_s'], 'boundary_host_s': tm['host_s'],
             'init_s': tm['init_s'], 'host_share': tm['host_s'] / wall, 'vs_iteration_bench': v / iter_value,
             'hv': pareto.compute_hypervolume(objs) if len(objs) else 0.0, 'ep_size': int(len(objs)),

@@ -68,10 +68,11 @@ class ParamLayout:
             shp = self.shapes[key]
             n = int(np.prod(shp))
             o = self.offsets[name]
-            v = flat[o:o + n].astype(np.float64)
+            v = flat[o:o + n].astype(np.float64)  # a fresh array: the tensor may own it
             if tr:
-                v = v.reshape(shp[1], shp[0]).T
-            sd[key] = torch.tensor(np.ascontiguousarray(v).reshape(shp), dtype=dtype)
+                v = np.ascontiguousarray(v.reshape(shp[1], shp[0]).T)
+            t = torch.from_numpy(v.reshape(shp))
+            sd[key] = t if t.dtype == dtype else t.to(dtype)
         return sd
 
     def adam_from_optimizer_state(self, opt_state):

@@ -55,7 +55,8 @@ def initialize_warm_up_batch(args, runtime):
 
 def run(args, device='cuda', rng='device', log=print, runtime=None):
     """The generation loop.  ``runtime`` (default: MOPGPopulation on ``device``) is the MOPG back end: any
-    object with MOPGPopulation's run / evaluate_samples / materialize / _batch(P).layout / device."""
+    object with MOPGPopulation's run / evaluate_samples / materialize / _batch(P).layout / device.
+    ``log=None`` silences the progress lines (and skips formatting them)."""
     np.random.seed(args.seed)
     torch.manual_seed(args.seed)
     t_start = time.perf_counter()
@@ -80,12 +81,13 @@ def run(args, device='cuda', rng='device', log=print, runtime=None):
     writer = rank == 0  # every rank holds the same host state; one writes the results tree
     gen_writer = GenerationWriter() if writer else None
     while iteration < total_num_updates:
-        log('\n------------------------------- Warm-up Stage -------------------------------' if episode == 0 else
-            f'\n-------------------- Evolutionary Stage: Generation {episode:3} --------------------')
+        if log is not None:
+            log('\n------------------------------- Warm-up Stage -------------------------------' if episode == 0 else
+                f'\n-------------------- Evolutionary Stage: Generation {episode:3} --------------------')
         episode += 1
         task_batch = [Task(e, s) for e, s in zip(elite_batch, scalarization_batch)]
         t0 = time.perf_counter()
-        all_offspring_batch = runtime.run(task_batch, iteration, rl_num_updates, start_time, log=log)
+        all_offspring_batch = runtime.run(task_batch, iteration, rl_num_updates, start_time, log=log or (lambda *m: None))
         t1 = time.perf_counter()
         n_its = len(all_offspring_batch[0]) if all_offspring_batch else 0
         all_sample_batch, offspring_batch = [], []
@@ -143,9 +145,10 @@ def run(args, device='cuda', rng='device', log=print, runtime=None):
                     if v > best_v:
                         best, best_v = s, v
                 elite_batch.append(best)
-        log('Selected Tasks:')
-        for e, sc in zip(elite_batch, scalarization_batch):
-            log(f'objs = {e.objs}, weight = {sc.weights}')
+        if log is not None:
+            log('Selected Tasks:')
+            for e, sc in zip(elite_batch, scalarization_batch):
+                log(f'objs = {e.objs}, weight = {sc.weights}')
         iteration = min(iteration + rl_num_updates, total_num_updates)
         rl_num_updates = args.update_iter
         if writer:
@@ -159,10 +162,12 @@ def run(args, device='cuda', rng='device', log=print, runtime=None):
         timing['train_env_steps'] += steps
         timing['generations'].append({'iteration': iteration, 'tasks': len(task_batch), 'iters': n_its,
                                       'rl_s': round(t1 - t0, 4), 'host_s': round(t2 - t1, 4)})
+    t_final = time.perf_counter()
     runtime.materialize(list(ep.sample_batch), dst=0)  # collective: EP snapshots onto the writing rank
     if writer:
         gen_writer.join()
         write_final(args, ep)
+        timing['final_s'] = time.perf_counter() - t_final
         timing['wall_s'] = time.perf_counter() - t_start
         timing['env_steps_per_s_whole_run'] = timing['train_env_steps'] / timing['wall_s']
         timing['env_steps_per_s_rl_only'] = timing['train_env_steps'] / max(timing['rl_s'], 1e-9)
@@ -170,9 +175,10 @@ def run(args, device='cuda', rng='device', log=print, runtime=None):
         timing['world_size'] = ws
         with open(os.path.join(args.save_dir, 'timing.json'), 'w') as fp:
             json.dump(timing, fp, indent=1)
-        log(f"[timing] wall {timing['wall_s']:.2f} s: MOPG {timing['rl_s']:.2f} s, generation-boundary host "
-            f"{timing['host_s']:.2f} s ({100 * timing['host_share']:.1f}%), {timing['train_env_steps']} train env-steps"
-            f" -> {timing['env_steps_per_s_whole_run']:.4g} env-steps/s whole run")
+        if log is not None:
+            log(f"[timing] wall {timing['wall_s']:.2f} s: MOPG {timing['rl_s']:.2f} s, generation-boundary host "
+                f"{timing['host_s']:.2f} s ({100 * timing['host_share']:.1f}%), {timing['train_env_steps']} train env-steps"
+                f" -> {timing['env_steps_per_s_whole_run']:.4g} env-steps/s whole run")
     ep.timing = timing
     if ws > 1:
         torch.distributed.barrier()  # the results tree is complete before any rank returns
@@ -268,10 +274,22 @@ def write_final(args, ep):
     fmt = _fmt(args.obj_num)
     final = os.path.join(args.save_dir, 'final')
     os.makedirs(final, exist_ok=True)
-    for i, s in enumerate(ep.sample_batch):
-        torch.save(s.actor_critic.state_dict(), os.path.join(final, f'EP_policy_{i}.pt'))
-        with open(os.path.join(final, f'EP_env_params_{i}.pkl'), 'wb') as fp:
-            pickle.dump(s.env_params, fp)
+    samples = list(ep.sample_batch)
+    if samples:  # every EP policy's flat parameters in ONE device->host copy, then the reference state_dicts
+        snaps = [s.snapshot for s in samples]
+        flats = torch.stack([sn.params for sn in snaps]).cpu().numpy()
+        envs = [s.env_params for s in samples]
+        layout = snaps[0].layout
+
+        def save(i):
+            torch.save(layout.unflatten(flats[i]), os.path.join(final, f'EP_policy_{i}.pt'))
+            with open(os.path.join(final, f'EP_env_params_{i}.pkl'), 'wb') as fp:
+                pickle.dump(envs[i], fp)
+        # file creation / zip writing release the GIL: a few writer threads overlap them (one EP can hold
+        # thousands of policies)
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(max_workers=8) as ex:
+            list(ex.map(save, range(len(samples))))
     with open(os.path.join(final, 'objs.txt'), 'w') as fp:
         for obj in ep.obj_batch:
             fp.write((fmt + '\n').format(*obj))

@@ -44,20 +44,32 @@ from .pareto import get_ep_indices, weight_grid
 # --------------------------------------------------------------------------- prediction model
 
 
-def collect_nearest_data(opt_graph, optgraph_id, threshold=0.1, objs_arr=None):
+def collect_nearest_data(opt_graph, optgraph_id, threshold=0.1, objs_arr=None, edges=None):
     """population_2d.py:11-21: (objs, sum-normalised next weight, delta objs) of every successor
-    edge leaving a node within ``threshold`` (relative, per objective) of node ``optgraph_id``.
-    ``objs_arr`` = np.array(opt_graph.objs), when the caller already holds it."""
-    objs_data, weights_data, delta_objs_data = [], [], []
+    edge leaving a node within ``threshold`` (relative, per objective) of node ``optgraph_id``, in the
+    reference's order (parents ascending, each parent's successors in insertion order).
+    ``objs_arr`` = np.array(opt_graph.objs) and ``edges`` = _edge_table(opt_graph), when the caller holds them."""
     objs_arr = np.asarray(opt_graph.objs, dtype=np.float64) if objs_arr is None else objs_arr
+    parent, wn, dl = _edge_table(opt_graph) if edges is None else edges
     center = objs_arr[optgraph_id]
     near = np.all(np.abs(center - objs_arr) < np.abs(center) * threshold, axis=1)
-    for i in np.nonzero(near)[0]:
-        for nxt in opt_graph.succ[i]:
-            objs_data.append(opt_graph.objs[i])
-            weights_data.append(opt_graph.weights[nxt] / np.sum(opt_graph.weights[nxt]))
-            delta_objs_data.append(opt_graph.delta_objs[nxt])
-    return objs_data, weights_data, delta_objs_data
+    sel = near[parent]
+    return objs_arr[parent[sel]], wn[sel], dl[sel]
+
+
+def _edge_table(opt_graph):
+    """Every OptGraph edge (parent, child) ordered by parent then child id (= each succ list's insertion
+    order): the parents, the children's sum-normalised weights and their delta objs, as arrays."""
+    par = np.asarray(opt_graph.prev, dtype=np.int64)
+    child = np.nonzero(par >= 0)[0]
+    parent = par[child]
+    order = np.lexsort((child, parent))
+    child, parent = child[order], parent[order]
+    K = len(opt_graph.objs[0]) if len(opt_graph.objs) else 0
+    W = np.asarray(opt_graph.weights, dtype=np.float64).reshape(-1, K)
+    D = np.asarray(opt_graph.delta_objs, dtype=np.float64).reshape(-1, K)
+    wn = W[child] / W[child].sum(axis=1, keepdims=True)
+    return parent, wn, D[child]
 
 
 def _count_distinct(weights_data, enough=4):
@@ -88,7 +100,7 @@ def _hyperbolic(x, A, a, b, c):
     return A * (e - 1) / (e + 1) + c
 
 
-def _fit_inputs(args, opt_graph, optgraph_id, test_weights, bounded_search, objs_arr):
+def _fit_inputs(args, opt_graph, optgraph_id, test_weights, bounded_search, objs_arr, edges=None):
     """population_2d.py:27-104 / population_3d.py:23-97 up to the fits: the widening neighbourhood search, the
     Gaussian distance weights and one (x, y, w, A upper bound) fit problem per objective.  Returns
     (original objs, sum-normalised test weights, problems or None when no node is reachable)."""
@@ -97,7 +109,8 @@ def _fit_inputs(args, opt_graph, optgraph_id, test_weights, bounded_search, objs
     threshold, sigma = 0.1, 0.03
     t_max = None if bounded_search else _max_useful_threshold(opt_graph, optgraph_id, objs_arr)
     while True:
-        objs_data, weights_data, delta_objs_data = collect_nearest_data(opt_graph, optgraph_id, threshold, objs_arr)
+        objs_data, weights_data, delta_objs_data = collect_nearest_data(opt_graph, optgraph_id, threshold, objs_arr,
+                                                                        edges)
         if _count_distinct(weights_data) > 3:
             break
         if bounded_search and threshold >= 1.0:
@@ -127,7 +140,8 @@ def predict_all(args, opt_graph, jobs, bounded_search):
     bounds=([0, .1, -5, -500], [A_hi, 20, 5, 500]))) run as ONE batch in libpgm_host.so (a C++ restatement of
     scipy's bounded 'trf' with the exact trust-region solver, over the host's threads)."""
     objs_arr = np.asarray(opt_graph.objs, dtype=np.float64)
-    prep = [_fit_inputs(args, opt_graph, node, tw, bounded_search, objs_arr) for node, tw in jobs]
+    edges = _edge_table(opt_graph)
+    prep = [_fit_inputs(args, opt_graph, node, tw, bounded_search, objs_arr, edges) for node, tw in jobs]
     problems = [p for _, _, probs in prep if probs is not None for p in probs]
     params = _host.fit_hyperbolic(problems) if problems else np.zeros((0, 4))
     out, k = [], 0

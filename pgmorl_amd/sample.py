@@ -17,6 +17,11 @@ class RunningMeanStd:
     """Parallel-variance running statistics, same fields as baselines' RunningMeanStd
     (externals/baselines/baselines/common/running_mean_std.py:3-31)."""
 
+    def __deepcopy__(self, memo):
+        c = RunningMeanStd.__new__(RunningMeanStd)
+        c.mean, c.var, c.count = np.copy(self.mean), np.copy(self.var), self.count
+        return c
+
     def __init__(self, epsilon=1e-4, shape=()):
         self.mean = np.zeros(shape, 'float64')
         self.var = np.ones(shape, 'float64')
@@ -38,6 +43,12 @@ class WeightedSumScalarization:
     def __init__(self, num_objs, weights=None):
         self.num_objs = num_objs
         self.weights = None if weights is None else torch.tensor(np.asarray(weights, dtype=np.float64))
+
+    def __deepcopy__(self, memo):  # the generic path deep-copies the tensor through its storage (slow)
+        c = WeightedSumScalarization.__new__(WeightedSumScalarization)
+        c.num_objs = self.num_objs
+        c.weights = None if self.weights is None else self.weights.clone()
+        return c
 
     def update_weights(self, weights):
         if weights is not None:
@@ -164,12 +175,35 @@ class AgentHandle:
 
 
 class Sample:
+    __slots__ = ('_env_params', '_envp_fn', '_snap', '_actor_critic', '_agent', 'objs', 'optgraph_id', '__dict__')
+
     def __init__(self, env_params, actor_critic, agent, objs=None, optgraph_id=None):
         self._env_params, self._envp_fn = env_params, None
-        self.actor_critic = actor_critic
-        self.agent = agent
+        self._snap = None
+        self._actor_critic, self._agent = actor_critic, agent
         self.objs = objs
         self.optgraph_id = optgraph_id
+
+    # the policy / agent handles of a device snapshot are made on first access (most offspring never need them)
+    @property
+    def actor_critic(self):
+        if self._actor_critic is None and self._snap is not None:
+            self._actor_critic = PolicyHandle(self._snap)
+        return self._actor_critic
+
+    @actor_critic.setter
+    def actor_critic(self, v):
+        self._actor_critic = v
+
+    @property
+    def agent(self):
+        if self._agent is None and self._snap is not None:
+            self._agent = AgentHandle(self._snap)
+        return self._agent
+
+    @agent.setter
+    def agent(self, v):
+        self._agent = v
 
     @property
     def env_params(self):
@@ -185,16 +219,19 @@ class Sample:
 
     @property
     def snapshot(self):
-        return self.actor_critic.snap
+        return self._snap if self._snap is not None else self.actor_critic.snap
 
     @classmethod
     def from_snapshot(cls, snap, env_params, objs=None, optgraph_id=None):
-        return cls(env_params, PolicyHandle(snap), AgentHandle(snap), objs, optgraph_id)
+        s = cls(env_params, None, None, objs, optgraph_id)
+        s._snap = snap
+        return s
 
     @classmethod
     def lazy(cls, snap, env_params_fn, objs=None, optgraph_id=None):
         """A Sample whose env_params are built by env_params_fn() on first access."""
-        s = cls(None, PolicyHandle(snap), AgentHandle(snap), objs, optgraph_id)
+        s = cls(None, None, None, objs, optgraph_id)
+        s._snap = snap
         s._envp_fn = env_params_fn
         return s
 

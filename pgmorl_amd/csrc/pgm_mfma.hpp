@@ -43,6 +43,18 @@ __device__ __forceinline__ float half_sum(float v) {
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
+// 16x16x4 f32 MFMA: C/D lane l, register r <-> (row 4(l >> 4) + r, column l & 15); A: lane l holds
+// A[i = l & 15][k = l >> 4]; B: lane l holds B[k = l >> 4][j = l & 15]
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+// sum over the four 16-lane groups (lanes c, c + 16, c + 32, c + 48), result in all of them
+__device__ __forceinline__ float group4_sum(float v) {
+    v = half_sum(v);                   // l ^ 32 (v_permlane32_swap)
+    return v + __shfl_xor(v, 16, 64);  // l ^ 16
+}
+
 // torch.min(a,b) / torch.max(a,b) backward weights for the first argument (ties split the gradient in half)
 __device__ __forceinline__ float wmin2(float a, float b) { return a < b ? 1.f : (a == b ? 0.5f : 0.f); }
 __device__ __forceinline__ float wmax2(float a, float b) { return a > b ? 1.f : (a == b ? 0.5f : 0.f); }

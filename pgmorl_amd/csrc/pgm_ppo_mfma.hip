@@ -44,8 +44,36 @@ PGM_STAMP_UNIT(mfma)
 #define PGM_U_L2 (PGM_EXP == 1 ? 8 : PGM_EXP == 2 ? 16 : 32)
 #define PGM_U_HEAD (PGM_EXP == 3 ? 4 : PGM_EXP == 4 ? 8 : 32)
 #define PGM_U16 (PGM_EXP == 5 ? 4 : PGM_EXP == 6 ? 8 : 16)
+// PGM_EXP 22 (A/B only): heads of the 32-row kernel on the 16x16x4 MFMA with the per-(sample, output) loss in its
+// C layout, as the 16-row kernel does.  Measured slower at Walker P = 40 (heads + loss 6.9 K -> 8.7 K cycles per
+// Adam step, update 6.57 -> 6.72 ms): every lane then evaluates the loss of 8 samples (two 16-sample blocks) where
+// the VALU heads give each lane one
+#define PGM_HEADS_MFMA (PGM_EXP == 22)
 
 namespace pgm {
+
+// The image reductions add exactly ONE partial onto a stored one per element per round (store and add ordered by a
+// barrier): a read + add + write in the wave.  PGM_EXP 23 (A/B only): ds_add_f32 instead (the same two-operand sum,
+// the read-modify-write in the LDS) -- measured ~20x slower on gfx950 (MODE 2 stage 1: 2.1 K -> 40.5 K cycles per
+// Adam step; t16 rounds 4.5 K -> 36 K)
+#define PGM_LDS_ADD (PGM_EXP == 23)
+__device__ __forceinline__ void lds_add(float* p, float v) {
+#if PGM_LDS_ADD
+    __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#else
+    *p += v;
+#endif
+}
+
+// clip_grad_norm_'s coefficient min(max_norm / (sqrt(sum of squares) + 1e-6), 1) (torch nn/utils/clip_grad.py):
+// hardware sqrt and a Newton-refined reciprocal (<= 1 ulp) instead of the IEEE expansions, off the critical path's
+// division sequences
+__device__ __forceinline__ float clip_coef(float max_norm, float sumsq) {
+    const float d = __builtin_amdgcn_sqrtf(sumsq) + 1e-6f;
+    float r = __builtin_amdgcn_rcpf(d);
+    r = fmaf(fmaf(-d, r, 1.f), r, r);
+    return fminf(max_norm * r, 1.f);
+}
 
 // ---------------------------------------------------------------- packed sample table
 struct PackArgs {
@@ -182,6 +210,10 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
     constexpr int IMG = Sm::IMG, NT = Sm::NT, SBk = Sm::SBk, RS = Sm::RS;
     constexpr int NBUF = nbuf<O, A, K, SPLIT>();
     constexpr int RSL = Sm::RSL;
+    // single-tile MODE 2: the next pass's row DMA is issued by waves 1-3 while wave 0 polls the tower-norm granule
+    // (they wait at that barrier anyway) and retired by the step's last barrier, instead of at the top of the
+    // step; wave 0 keeps no DMA in its queue so its polls' vmcnt waits do not include it.  PGM_EXP 32: at the top
+    constexpr bool EARLY_STAGE = ONE && MODE == 2 && NBUF == 2 && PGM_EXP != 32;
     constexpr int CR = RS / 4;                         // 16-B chunks per packed row
     constexpr int NDT = (SBk * RSL) / 256;             // LDS-DMA wave instructions per pass (1 KiB each)
     static_assert(NDT * 256 == SBk * RSL, "staging split");
@@ -217,26 +249,29 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
     // Row DMA: instruction d (waves take d = w, w+4, ...) fills LDS floats [256 d, 256 d + 256); lane l's
     // 16 B land at float 256 d + 4 l = row * RSL + 4 chunk.  The pad chunk of a row (chunk == CR)
     // re-reads the row's first chunk.
-    auto issue_idx = [&](int g, int buf) {
+    // (wi, nwv): this wave's index among the nwv waves that share the issue (default: all four)
+    auto issue_idx = [&](int g, int buf, int wi = -1, int nwv = 4) {
+        if (wi < 0) wi = w;
         const int e = g / (nb * npm), rem = g - e * nb * npm, bb = rem / npm, j = rem - bb * npm;
         const int ns = min(SBk, mbs - j * SBk);
         const int32_t* src = a.perms + (size_t)e * B + bb * mb + r0 + j * SBk;
-        for (int r0 = w * 64; r0 < SBk; r0 += 256)  // rows beyond ns re-read the last valid index
+        for (int r0 = wi * 64; r0 < SBk; r0 += 64 * nwv)  // rows beyond ns re-read the last valid index
             __builtin_amdgcn_global_load_lds((const void*)(src + min(r0 + l, ns - 1)),
                                              (lds_void_t*)&S.IB[buf][r0], 4, 0, 0);
     };
-    auto issue_rows = [&](int buf, int ibuf) {
+    auto issue_rows_n = [&](int buf, int ibuf, int wi, auto nwc) {
+        constexpr int NWV = decltype(nwc)::value;
         float* base = &S.RB[buf][0];
-        constexpr int NI = (NDT + 3) / 4;  // instructions per wave (the last round is partial)
+        constexpr int NI = (NDT + NWV - 1) / NWV;  // instructions per wave (the last round is partial)
         int idx[NI];
 #pragma unroll
         for (int i = 0; i < NI; ++i) {  // all index reads first: one LDS latency for the batch
-            const int d = w + 4 * i, pos = d * 256 + 4 * l, row = min(pos / RSL, SBk - 1);
+            const int d = wi + NWV * i, pos = d * 256 + 4 * l, row = min(pos / RSL, SBk - 1);
             idx[i] = S.IB[ibuf][row];
         }
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
-            const int d = w + 4 * i;
+            const int d = wi + NWV * i;
             if (d < NDT) {
                 const int pos = d * 256 + 4 * l, row = pos / RSL, chunk = (pos - row * RSL) >> 2;
                 const float* src = rows + (size_t)idx[i] * RS + (chunk < CR ? chunk : 0) * 4;
@@ -244,6 +279,7 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
             }
         }
     };
+    auto issue_rows = [&](int buf, int ibuf) { issue_rows_n(buf, ibuf, w, ic<4>{}); };
     // element k of row cs of a tile starting at rt
     auto rowf = [&](const float* rt, int cs, int k) { return rt[cs * RSL + k]; };
 
@@ -271,6 +307,7 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
     const float b1c = a.hp.beta1, b2c = a.hp.beta2, eps = a.hp.adam_eps;
     const float vscale = a.hp.value_loss_coef * 0.5f / (float)(mb * K);
     const float ascale = -1.f / (float)mb;
+    const float vstat = 0.5f / (float)(mb * K), astat = 1.f / (float)mb;  // loss statistics scales
     float st_v = 0.f, st_a = 0.f, st_e = 0.f;
     int nstep = 0, gp = 0;
     double b1p = pow((double)b1c, (double)step0), b2p = pow((double)b2c, (double)step0);
@@ -279,9 +316,21 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
 
     for (int e = 0; e < E; ++e) {
         for (int bb = 0; bb < nb; ++bb) {
+            // this step's Adam scalars: beta^step carried in fp64 (torch: 1 - beta ** step), lr / bias correction 1,
+            // 1 / sqrt(bias correction 2); MODE 2 forms them while its image stores drain
+            double b1n = 0.0, b2n = 0.0;
+            float step_size = 0.f, inv_bc2s = 0.f;
+            auto adam_scalars = [&]() {
+                b1n = b1p * (double)b1c;
+                b2n = b2p * (double)b2c;
+                step_size = (float)(lr / (1.0 - b1n));
+                inv_bc2s = 1.f / (float)sqrt(1.0 - b2n);
+                asm volatile("" : "+v"(step_size), "+v"(inv_bc2s));  // formed HERE (the compiler would sink them)
+            };
             f32x16 gW2[2][2], gW1[2];  // [in tile][out tile], [out tile] (O <= 32: one in tile)
             float gWh[2][Q], gB1[2], gB2[2];
             float gsm = 0.f;  // lanes q < Q: head-bias gradient q; lanes 32 + q (actor): logstd gradient q
+            float gbh = 0.f, gls = 0.f;  // MFMA heads: per-lane partial head-bias / logstd sums (column l & 15)
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
 #pragma unroll
@@ -303,7 +352,7 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                     if (gp + 1 < npass) issue_rows(cur ^ 1, (gp + 1) & 1);
                     if (gp + 2 < npass) issue_idx(gp + 2, gp & 1);
                 };
-                if constexpr (NBUF == 2 && !LATE_STAGE) stage_next();
+                if constexpr (NBUF == 2 && !LATE_STAGE && !EARLY_STAGE) stage_next();
                 const float* rb = &S.RB[cur][0];
                 PGM_STAMP(0);
 
@@ -355,6 +404,83 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
 #pragma unroll
                         for (int r = 0; r < 16; ++r) scr[rowof(r, h) * SCR + ob * TS + c] = H2[ob][r];
                     wave_lds_fence();
+#if PGM_HEADS_MFMA
+                    // ---- heads on the 16x16x4 MFMA, two 16-sample blocks sb: out[s][q] = H2[s][:] . Wh[q][:] (A from
+                    // the H2 transpose tile, B = Wh rows), leaving every per-(sample, output) loss term in the C layout
+                    // (register r <-> sample 16 sb + 4 g4 + r, lane column c16 <-> head output q): the actor's
+                    // log-prob of a sample is a 16-lane DPP row sum
+                    const int g4 = l >> 4, c16 = l & 15;
+                    const bool qv = c16 < Q;
+                    f32x4 ho[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+                    for (int ks = 0; ks < H / 4; ++ks) {
+                        const int k = 4 * ks + g4;
+                        const float bw = qv ? W.Wh[qv ? c16 : 0][k] : 0.f;
+#pragma unroll
+                        for (int sb = 0; sb < 2; ++sb) ho[sb] = mfma16(scr[(16 * sb + c16) * SCR + k], bw, ho[sb]);
+                    }
+                    const float bhq = qv ? W.bh[qv ? c16 : 0] : 0.f;
+                    f32x4 dq[2];  // dL/d(head output c16) of sample 16 sb + 4 g4 + r
+                    if (m == 0) {  // value loss over the K objectives (ppo.py:86-94)
+#pragma unroll
+                        for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                const int s = 16 * sb + 4 * g4 + r;
+                                const bool ok = ts0 + s < ns && c16 < K;
+                                const float V = ho[sb][r] + bhq;
+                                const float Vo = rowf(rt, s, O + A + 2 + (c16 < K ? c16 : 0));
+                                const float R = rowf(rt, s, O + A + 2 + K + (c16 < K ? c16 : 0));
+                                float gv, ls;
+                                if (a.hp.use_clipped_value_loss) {
+                                    const float dv = V - Vo;
+                                    const float vc = Vo + fminf(fmaxf(dv, -clip), clip);
+                                    const float l1 = (V - R) * (V - R), l2 = (vc - R) * (vc - R);
+                                    const float inr = (dv >= -clip && dv <= clip) ? 1.f : 0.f;
+                                    gv = wmax2(l1, l2) * 2.f * (V - R) + wmax2(l2, l1) * 2.f * (vc - R) * inr;
+                                    ls = fmaxf(l1, l2);
+                                } else {
+                                    gv = 2.f * (V - R);
+                                    ls = (R - V) * (R - V);
+                                }
+                                dq[sb][r] = ok ? vscale * gv : 0.f;
+                                lsum += ok ? ls : 0.f;
+                                gbh += dq[sb][r];
+                            }
+                    } else {  // clipped surrogate (ppo.py:80-85); log-probs as row sums over the outputs
+                        const bool av_ = c16 < A;
+                        const float aivq = S.aiv[av_ ? c16 : 0], lsq = av_ ? lstd[av_ ? c16 : 0] : 0.f;
+#pragma unroll
+                        for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                const int s = 16 * sb + 4 * g4 + r;
+                                const bool ok = ts0 + s < ns;
+                                const float diff = av_ ? rowf(rt, s, O + (av_ ? c16 : 0)) - (ho[sb][r] + bhq) : 0.f;
+                                const float lpe = av_ ? -0.5f * diff * diff * aivq - lsq - LOG_SQRT_2PI : 0.f;
+                                const float lp = row_sum16(lpe);
+                                const float ratio = expf(lp - rowf(rt, s, O + A));
+                                const float ad = rowf(rt, s, O + A + 1);
+                                const float s1 = ratio * ad;
+                                const float s2 = fminf(fmaxf(ratio, 1.f - clip), 1.f + clip) * ad;
+                                const float inr = (ratio >= 1.f - clip && ratio <= 1.f + clip) ? 1.f : 0.f;
+                                const float gr = ad * (wmin2(s1, s2) + wmin2(s2, s1) * inr);
+                                const float dlp = ok ? ascale * gr * ratio : 0.f;
+                                lsum += (ok && c16 == 0) ? -fminf(s1, s2) : 0.f;
+                                dq[sb][r] = av_ ? dlp * diff * aivq : 0.f;
+                                gbh += dq[sb][r];
+                                gls += av_ ? dlp * (diff * diff * aivq - 1.f) : 0.f;
+                            }
+                    }
+                    // dO tile [sample][q] (this wave's): the dH2 A operand (lane = sample) and the head-weight grads
+                    if (qv) {
+#pragma unroll
+                        for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) S.dout[w][16 * sb + 4 * g4 + r][qv ? c16 : 0] = dq[sb][r];
+                    }
+                    wave_lds_fence();
+#else
                     // ---- heads on the VALU: lane = sample c, half h sums units [32h, 32h+32)
                     float outv[Q];
 #pragma unroll
@@ -429,6 +555,7 @@ PGM_UNROLL(ONE ? PGM_U_HEAD : 4)
 #pragma unroll 8
                         for (int cc = 0; cc < TS; ++cc) gsm += src[cc * Q];
                     }
+#endif
                     PGM_STAMP(5);
                     // ---- head-weight grads (VALU, C layout): gWh[ob][q] += sum_r H2[s][u] dO[s][q]
 #pragma unroll
@@ -444,7 +571,11 @@ PGM_UNROLL(ONE ? PGM_U_HEAD : 4)
 #pragma unroll
                     for (int ks = 0; ks < (Q + 1) / 2; ++ks) {
                         const int q = 2 * ks + h;
+#if PGM_HEADS_MFMA
+                        const float av = q < Q ? S.dout[w][c][q < Q ? q : 0] : 0.f;  // lane = sample c, k = output q
+#else
                         const float av = h ? (2 * ks + 1 < Q ? dO[2 * ks + 1] : 0.f) : dO[2 * ks];
+#endif
 #pragma unroll
                         for (int ob = 0; ob < 2; ++ob) z[ob] = mfma(av, q < Q ? W.Wh[q][ob * TS + c] : 0.f, z[ob]);
                     }
@@ -505,7 +636,9 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
                     wave_lds_fence();  // dH1 finished reading the dZ2 tile before the next tile's writes
                     PGM_STAMP(7);
                 }  // tiles
-                if constexpr (NBUF == 2) {
+                if constexpr (EARLY_STAGE) {
+                    lds_sync_m();  // every wave's tiles done: the image rounds below overwrite the transpose tiles
+                } else if constexpr (NBUF == 2) {
                     dma_sync_m();  // next pass landed (issued a pass ago); this buffer free for reuse
                 } else {
                     lds_sync_m();
@@ -517,6 +650,7 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
                 }
                 PGM_STAMP(1);
             }  // passes
+            // (gp is now the next pass)
 
             // ---- combine the lane halves of the per-column partial sums
 #pragma unroll
@@ -527,6 +661,13 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
                 for (int q = 0; q < Q; ++q) gWh[i][q] = half_sum(gWh[i][q]);
             }
             lsum = wave_sum64(lsum);
+#if PGM_HEADS_MFMA
+            // per-column sums over the four lane groups: lane c < Q of half 0 holds the head-bias gradient of output
+            // c, lane 32 + c the logstd gradient of action c (the VALU heads' gsm lane map)
+            gbh = group4_sum(gbh);
+            gls = group4_sum(gls);
+            gsm = h == 0 ? gbh : gls;
+#endif
             // entropy with the logstd of this step (before Adam)
             float ent = 0.f;
 #pragma unroll
@@ -544,16 +685,15 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
                 for (int stage = 0; stage < 2; ++stage) {
                     const bool add = stage == 1;
                     const int half = (stage == 0) == (pr == 1) ? 0 : 1;  // image half handled in this stage
-                    auto acc = [&](int idx, float val) { Gt[idx] = add ? Gt[idx] + val : val; };
-                    // 16-register blocks: all reads of a block are issued before its writes, so the
-                    // read-modify-write pays one LDS latency per block, not one per element
+                    auto acc = [&](int idx, float val) {
+                        if (add) lds_add(&Gt[idx], val);
+                        else Gt[idx] = val;
+                    };
+                    // 16-register blocks; stage 1 adds in the LDS (ds_add_f32: no read latency in the wave)
                     auto acc16 = [&](auto idx, const f32x16& val) {
                         if (add) {
-                            float tmp[16];
 #pragma unroll
-                            for (int r = 0; r < 16; ++r) tmp[r] = Gt[idx(r)];
-#pragma unroll
-                            for (int r = 0; r < 16; ++r) Gt[idx(r)] = tmp[r] + val[r];
+                            for (int r = 0; r < 16; ++r) lds_add(&Gt[idx(r)], val[r]);
                         } else {
 #pragma unroll
                             for (int r = 0; r < 16; ++r) Gt[idx(r)] = val[r];
@@ -586,9 +726,7 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
                             }
                             if (add) {
 #pragma unroll
-                                for (int j = 0; j < NU; ++j) tmp[j] = Gt[idx[j]];
-#pragma unroll
-                                for (int j = 0; j < NU; ++j) Gt[idx[j]] = tmp[j] + val[j];
+                                for (int j = 0; j < NU; ++j) lds_add(&Gt[idx[j]], val[j]);
                             } else {
 #pragma unroll
                                 for (int j = 0; j < NU; ++j) Gt[idx[j]] = val[j];
@@ -651,6 +789,7 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
                     G0[4 * NV4 + t] = g;
                     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(g), xr, off_mine + 16 * NV4 + 4 * t, 0, SC1);
                 }
+                adam_scalars();  // fp64 bias corrections while the stores drain
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
                 lds_sync_m();
                 PGM_STAMP(10);
@@ -725,6 +864,12 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
             lds_sync_m();
             PGM_STAMP(8);
             float total = (S.red[0] + S.red[1]) + (S.red[2] + S.red[3]);
+            if constexpr (EARLY_STAGE) {  // next pass: rows by waves 1-3 (retired by the step's last barrier)
+                if (w != 0) {
+                    if (gp < npass) issue_rows_n(gp & 1, gp & 1, w - 1, ic<3>{});
+                    if (gp + 1 < npass) issue_idx(gp + 1, (gp + 1) & 1, w - 1, 3);
+                }
+            }
             if constexpr (SPLIT) {  // tagged 8-byte granule hand-off with the other tower's workgroup
                 if (t == 0) {
                     const unsigned tag = (unsigned)(nstep + 1);
@@ -751,27 +896,23 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
                 total = S.red[4];
             }
             PGM_STAMP(9);
-            const float coef = fminf(a.hp.max_grad_norm / (sqrtf(total) + 1e-6f), 1.f);
+            const float coef = clip_coef(a.hp.max_grad_norm, total);
             if (t == 0) {
                 if constexpr (SPLIT) {
                     const float ls = NS == 2 ? S.red[12] : (S.red[8] + S.red[9]) + (S.red[10] + S.red[11]);
-                    if (m == 0) st_v += 0.5f * ls / (float)(mb * K);
-                    else st_a += ls / (float)mb;
+                    if (m == 0) st_v += ls * vstat;
+                    else st_a += ls * astat;
                 } else {
-                    st_v += 0.5f * (S.red[8] + S.red[10]) / (float)(mb * K);
-                    st_a += (S.red[9] + S.red[11]) / (float)mb;
+                    st_v += (S.red[8] + S.red[10]) * vstat;
+                    st_a += (S.red[9] + S.red[11]) * astat;
                 }
                 st_e += ent;
             }
             // ---- Adam, one flat pass over the images (padding: g = m = v = 0 keeps p = 0)
             ++nstep;
-            b1p *= (double)b1c;  // beta^step, carried in fp64 (torch: 1 - beta ** step)
-            b2p *= (double)b2c;
-            const double bc1 = 1.0 - b1p;
-            const double bc2 = 1.0 - b2p;
-            const float step_size = (float)(lr / bc1);
-            const float bc2s = (float)sqrt(bc2);
-            const float inv_bc2s = 1.f / bc2s;
+            if constexpr (NS != 2) adam_scalars();
+            b1p = b1n;
+            b2p = b2n;
             auto adam1 = [&](float g, float& mm, float& vv, float& pp) {
                 const float gc = g * coef;
                 mm = mm + (1.f - b1c) * (gc - mm);
@@ -850,12 +991,13 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
                     vv = vv * b2c + (1.f - b2c) * (g * g);
                     Mo[f] = mm;
                     Vo[f] = vv;
-                    const float pn = Pf[i] - step_size * (mm / (sqrtf(vv) / bc2s + eps));
+                    const float pn = Pf[i] - step_size * (mm / (sqrtf(vv) * inv_bc2s + eps));
                     Pf[i] = pn;
                     if (i >= IMG + oLs && i < IMG + oLs + A) S.aiv[i - IMG - oLs] = expf(-2.f * pn);
                 }
             }
-            lds_sync_m();  // parameters updated before the next minibatch; GA region reused as scr
+            if constexpr (EARLY_STAGE) dma_sync_m();  // + the next pass's rows landed
+            else lds_sync_m();  // parameters updated before the next minibatch; GA region reused as scr
             PGM_STAMP(3);
         }  // minibatches
     }      // epochs
@@ -903,20 +1045,11 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
 // images of a tower are exchanged through 16-B sc1 publishes + tagged flags (every workgroup sums them in
 // row-part order h = 0..NS-1, so all NS copies of the Adam step are bitwise identical), the two towers
 // exchange their squared norms as tagged 8-byte granules, and Adam runs from registers.
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int T16 = 16;       // samples per tile
 constexpr int S16 = H + 2;    // transpose-tile row stride: conflict-free A-operand reads, 2-way (free) writes
 constexpr int DQ = 8;         // head-output columns of the dO transpose tile (Q <= 8)
 constexpr int DQS = DQ + 1;
 
-__device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
-// sum over the four 16-lane groups (lanes c, c + 16, c + 32, c + 48), result in all of them
-__device__ __forceinline__ float group4_sum(float v) {
-    v = half_sum(v);                                               // l ^ 32 (v_permlane32_swap)
-    return v + __shfl_xor(v, 16, 64);                              // l ^ 16
-}
 
 template <int O, int A, int K, int W, int NBUF, int NIMG_>
 struct T16SmemT {
@@ -966,6 +1099,9 @@ __global__ __launch_bounds__(64 * W) void ppo_update_t16_kernel(MArgs a) {
     constexpr int IMG = Sm::IMG, SBk = Sm::SBk, RS = Sm::RS, RSL = Sm::RSL;
     constexpr int NBUF = t16_nbuf<O, A, K, W>();
     constexpr int CR = RS / 4;
+    // single-tile: the next pass's row DMA by waves 1..W-1 while wave 0 polls the tower-norm granule, retired by the
+    // step's last barrier (as in the 32-row kernel); PGM_EXP 32: at the top of the step
+    constexpr bool EARLY_STAGE = ONE && NBUF == 2 && W > 1 && PGM_EXP != 32;
     constexpr int NDT = (SBk * RSL) / 256;
     static_assert(NDT * 256 == SBk * RSL, "staging split");
     constexpr int oW2 = O * H, oWh = oW2 + H * SCR, oB1 = oWh + Q * H, oB2 = oB1 + H, oBh = oB2 + H, oLs = oBh + Q;
@@ -992,26 +1128,29 @@ __global__ __launch_bounds__(64 * W) void ppo_update_t16_kernel(MArgs a) {
     float* __restrict__ Vo = a.v + (size_t)p * L.total;
     const float* rows = a.rows + (size_t)p * B * RS;
 
-    auto issue_idx = [&](int gi, int buf) {
+    // (wi, nwv): this wave's index among the nwv waves sharing the issue
+    auto issue_idx = [&](int gi, int buf, int wi = -1, int nwv = W) {
+        if (wi < 0) wi = w;
         const int e = gi / (nb * npm), rem = gi - e * nb * npm, bb = rem / npm, j = rem - bb * npm;
         const int ns = min(SBk, mbs - j * SBk);
         const int32_t* src = a.perms + (size_t)e * B + bb * mb + r0 + j * SBk;
-        for (int q0 = w * 64; q0 < SBk; q0 += NT)  // rows beyond ns re-read the last valid index
+        for (int q0 = wi * 64; q0 < SBk; q0 += 64 * nwv)  // rows beyond ns re-read the last valid index
             __builtin_amdgcn_global_load_lds((const void*)(src + min(q0 + l, ns - 1)),
                                              (lds_void_t*)&S.IB[buf][q0], 4, 0, 0);
     };
-    auto issue_rows = [&](int buf, int ibuf) {
+    auto issue_rows_n = [&](int buf, int ibuf, int wi, auto nwc) {
+        constexpr int NWV = decltype(nwc)::value;
         float* base = &S.RB[buf][0];
-        constexpr int NI = (NDT + W - 1) / W;
+        constexpr int NI = (NDT + NWV - 1) / NWV;
         int idx[NI];
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
-            const int d = w + W * i, pos = d * 256 + 4 * l, row = min(pos / RSL, SBk - 1);
+            const int d = wi + NWV * i, pos = d * 256 + 4 * l, row = min(pos / RSL, SBk - 1);
             idx[i] = S.IB[ibuf][row];
         }
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
-            const int d = w + W * i;
+            const int d = wi + NWV * i;
             if (d < NDT) {
                 const int pos = d * 256 + 4 * l, row = pos / RSL, chunk = (pos - row * RSL) >> 2;
                 const float* src = rows + (size_t)idx[i] * RS + (chunk < CR ? chunk : 0) * 4;
@@ -1019,6 +1158,7 @@ __global__ __launch_bounds__(64 * W) void ppo_update_t16_kernel(MArgs a) {
             }
         }
     };
+    auto issue_rows = [&](int buf, int ibuf) { issue_rows_n(buf, ibuf, w, ic<W>{}); };
 
     // ---- parameter and Adam moment images from the flat HBM vectors
     float* Pf = &S.Pm.W1t[0][0];
@@ -1042,6 +1182,7 @@ __global__ __launch_bounds__(64 * W) void ppo_update_t16_kernel(MArgs a) {
     const float b1c = a.hp.beta1, b2c = a.hp.beta2, eps = a.hp.adam_eps;
     const float vscale = a.hp.value_loss_coef * 0.5f / (float)(mb * K);
     const float ascale = -1.f / (float)mb;
+    const float vstat = 0.5f / (float)(mb * K), astat = 1.f / (float)mb;  // loss statistics scales
     float st_v = 0.f, st_a = 0.f, st_e = 0.f;
     int nstep = 0, gp = 0;
     double b1p = pow((double)b1c, (double)step0), b2p = pow((double)b2c, (double)step0);
@@ -1066,7 +1207,7 @@ __global__ __launch_bounds__(64 * W) void ppo_update_t16_kernel(MArgs a) {
             for (int s0 = 0; ONE ? s0 < 1 : s0 < mbs; s0 += (ONE ? 1 : SBk), ++gp) {
                 const int ns = ONE ? SBk : min(SBk, mbs - s0);
                 const int cur = NBUF == 2 ? (gp & 1) : 0;
-                if constexpr (NBUF == 2) {
+                if constexpr (NBUF == 2 && !EARLY_STAGE) {
                     if (gp + 1 < npass) issue_rows(cur ^ 1, (gp + 1) & 1);
                     if (gp + 2 < npass) issue_idx(gp + 2, gp & 1);
                 }
@@ -1260,7 +1401,9 @@ PGM_UNROLL(ONE ? PGM_U16 : 4)
                     wave_lds_fence();  // dH1 finished reading the dZ2 tile before the next tile's writes
                     PGM_STAMP(7);
                 }  // tiles
-                if constexpr (NBUF == 2) {
+                if constexpr (EARLY_STAGE) {
+                    lds_sync_m();  // every wave's tiles done: the image rounds overwrite the transpose tiles
+                } else if constexpr (NBUF == 2) {
                     dma_sync_m();
                 } else {
                     lds_sync_m();
@@ -1303,16 +1446,13 @@ PGM_UNROLL(ONE ? PGM_U16 : 4)
                 auto round = [&](auto slc, auto addc) {
                     constexpr int SL = decltype(slc)::value;
                     constexpr bool add = decltype(addc)::value != 0;
-                    // one 4-register block at a time: its reads, then its writes (grouping several blocks per
-                    // read batch measured slower: 4.2 K -> 5.6 K cycles per Adam step)
+                    // one 4-register block at a time; the later rounds add in the LDS (ds_add_f32, one add per
+                    // element per round: the wave order of every element stays fixed)
                     auto put4 = [&](auto idx, const f32x4& v) {
                         if constexpr (add) {
-                            float tmp[4];
-#pragma unroll
-                            for (int r = 0; r < 4; ++r) tmp[r] = idx(r) >= 0 ? Gt[idx(r)] : 0.f;
 #pragma unroll
                             for (int r = 0; r < 4; ++r)
-                                if (idx(r) >= 0) Gt[idx(r)] = tmp[r] + v[r];
+                                if (idx(r) >= 0) lds_add(&Gt[idx(r)], v[r]);
                         } else {
 #pragma unroll
                             for (int r = 0; r < 4; ++r)
@@ -1575,6 +1715,12 @@ PGM_UNROLL(ONE ? PGM_U16 : 4)
 #pragma unroll
             for (int i = 0; i < W; ++i) total += S.red[i];
             PGM_STAMP(8);
+            if constexpr (EARLY_STAGE) {  // next pass (gp after the pass loop): rows by waves 1..W-1
+                if (w != 0) {
+                    if (gp < npass) issue_rows_n(gp & 1, gp & 1, w - 1, ic<W - 1>{});
+                    if (gp + 1 < npass) issue_idx(gp + 1, (gp + 1) & 1, w - 1, W - 1);
+                }
+            }
             if (t == 0) {
                 const unsigned tag = (unsigned)(nstep + 1);
                 unsigned long long* gr = a.ws + ppo_norm_granule(a.P, p, 0, hs, nstep & 1);
@@ -1599,10 +1745,10 @@ PGM_UNROLL(ONE ? PGM_U16 : 4)
             lds_sync_m();
             total = S.red[5];
             PGM_STAMP(9);
-            const float coef = fminf(a.hp.max_grad_norm / (sqrtf(total) + 1e-6f), 1.f);
+            const float coef = clip_coef(a.hp.max_grad_norm, total);
             if (t == 0) {
-                if (m == 0) st_v += 0.5f * lsum_all / (float)(mb * K);
-                else st_a += lsum_all / (float)mb;
+                if (m == 0) st_v += lsum_all * vstat;
+                else st_a += lsum_all * astat;
                 st_e += ent;
             }
             // ---- Adam from registers (padding: g = m = v = 0 keeps p = 0)
@@ -1646,7 +1792,8 @@ PGM_UNROLL(ONE ? PGM_U16 : 4)
                 Pf[i] = pp;
                 if (m == 1 && i >= oLs && i < oLs + A) S.aiv[i - oLs] = expf(-2.f * pp);
             }
-            lds_sync_m();  // parameters updated before the next minibatch; GA region reused as scr
+            if constexpr (EARLY_STAGE) dma_sync_m();  // + the next pass's rows landed
+            else lds_sync_m();  // parameters updated before the next minibatch; GA region reused as scr
             PGM_STAMP(3);
         }  // minibatches
     }      // epochs

@@ -75,6 +75,35 @@ class ParamLayout:
             sd[key] = t if t.dtype == dtype else t.to(dtype)
         return sd
 
+    def unflatten_batch(self, flats):
+        """[E, total] flat vectors -> per state_dict key (STATE_KEYS order) a C-contiguous fp64 [E, *shape] array,
+        row i equal to unflatten(flats[i])[key].  A torch tensor (e.g. on the GPU) is converted and transposed
+        where it lives, then copied to the host once per key."""
+        if isinstance(flats, torch.Tensor):
+            E = flats.shape[0]
+            out = []
+            for key, name, tr in STATE_KEYS:
+                shp = self.shapes[key]
+                n = int(np.prod(shp))
+                o = self.offsets[name]
+                v = flats[:, o:o + n].to(torch.float64)
+                if tr:
+                    v = v.reshape(E, shp[1], shp[0]).transpose(1, 2)
+                out.append(v.contiguous().reshape((E,) + tuple(shp)).cpu().numpy())
+            return out
+        flats = np.asarray(flats)
+        E = flats.shape[0]
+        out = []
+        for key, name, tr in STATE_KEYS:
+            shp = self.shapes[key]
+            n = int(np.prod(shp))
+            o = self.offsets[name]
+            v = flats[:, o:o + n].astype(np.float64)
+            if tr:
+                v = v.reshape(E, shp[1], shp[0]).transpose(0, 2, 1)
+            out.append(np.ascontiguousarray(v).reshape((E,) + tuple(shp)))
+        return out
+
     def adam_from_optimizer_state(self, opt_state):
         """torch Adam state_dict()['state'] -> (m flat, v flat, step int)."""
         if not opt_state:

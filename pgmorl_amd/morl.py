@@ -269,6 +269,90 @@ def write_generation_record(r):
     rows(os.path.join(base, 'elites', 'offsprings.txt'), r['offsprings'])
 
 
+class _StateDictWriter:
+    """torch.save of many state_dicts with identical keys, shapes and dtypes (the EP policies), without re-pickling:
+    the first is saved by torch.save into memory with torch's own CRC-32 computation switched off
+    (torch.serialization.set_crc32_options(False): records carry CRC 0, as torch writes them in that mode); every
+    later file is that zip image with the tensor records' bytes replaced (torch.save stores them uncompressed, 64-B
+    aligned, one record per storage in state_dict order).  The first templated file is read back with
+    torch.load(weights_only=True) and compared; any mismatch falls back to torch.save for every file."""
+
+    def __init__(self, sd):
+        import io
+        import zipfile
+        self.keys = list(sd)
+        b = io.BytesIO()
+        self.crc = True
+        try:
+            from torch.serialization import get_crc32_options, set_crc32_options
+            prev = get_crc32_options()
+            set_crc32_options(False)
+            try:
+                torch.save(sd, b)
+            finally:
+                set_crc32_options(prev)
+            self.crc = False
+        except ImportError:  # an older torch: CRC-32s patched per file
+            torch.save(sd, b)
+        self.tmpl = b.getvalue()
+        self.ok = False
+        try:
+            z = zipfile.ZipFile(io.BytesIO(self.tmpl))
+            info = {i.filename: i for i in z.infolist()}
+            prefix = z.infolist()[0].filename.split('/')[0]
+            cd = {}  # central-directory record offset of each member
+            pos = self.tmpl.rfind(b'PK\x05\x06')
+            cd_off = int.from_bytes(self.tmpl[pos + 16:pos + 20], 'little')
+            n = int.from_bytes(self.tmpl[pos + 10:pos + 12], 'little')
+            o = cd_off
+            for _ in range(n):
+                fl, el, cl = (int.from_bytes(self.tmpl[o + k:o + k + 2], 'little') for k in (28, 30, 32))
+                cd[self.tmpl[o + 46:o + 46 + fl].decode()] = o
+                o += 46 + fl + el + cl
+            self.rec = []
+            for k, key in enumerate(self.keys):
+                zi = info[f'{prefix}/data/{k}']
+                h = zi.header_offset
+                fl, el = (int.from_bytes(self.tmpl[h + k2:h + k2 + 2], 'little') for k2 in (26, 28))
+                t = sd[key]
+                if zi.compress_type != 0 or zi.file_size != t.numel() * t.element_size():
+                    return
+                self.rec.append((h + 30 + fl + el, zi.file_size, h + 14, cd[zi.filename] + 16))
+            self.ok = True
+        except Exception:
+            self.ok = False
+
+    def save(self, sd, path):
+        if not self.ok:
+            torch.save(sd, path)
+            return
+        self.save_records([sd[key].detach().contiguous().numpy() for key in self.keys], path)
+
+    def save_records(self, arrays, path):
+        """The templated file from the state_dict's tensors as numpy arrays (state_dict order, exact dtypes)."""
+        import zlib
+        buf = bytearray(self.tmpl)
+        for (off, size, lcrc, ccrc), arr in zip(self.rec, arrays):
+            data = memoryview(np.ascontiguousarray(arr)).cast('B')
+            buf[off:off + size] = data
+            if self.crc:
+                crc = zlib.crc32(data).to_bytes(4, 'little')
+                buf[lcrc:lcrc + 4] = crc
+                buf[ccrc:ccrc + 4] = crc
+        with open(path, 'wb') as fp:
+            fp.write(buf)
+
+    def verify(self, sd, path):
+        """torch.load of a templated file must equal its state_dict bit for bit (else: torch.save from now on)."""
+        if not self.ok:
+            return
+        got = torch.load(path, weights_only=True)
+        if list(got) != self.keys or not all(torch.equal(got[k], sd[k]) and got[k].dtype == sd[k].dtype
+                                             for k in self.keys):
+            self.ok = False
+            torch.save(sd, path)
+
+
 def write_final(args, ep):
     """morl/morl.py:223-245: final/EP_policy_i.pt, EP_env_params_i.pkl, objs.txt, env_params.txt."""
     fmt = _fmt(args.obj_num)
@@ -277,18 +361,35 @@ def write_final(args, ep):
     samples = list(ep.sample_batch)
     if samples:  # every EP policy's flat parameters in ONE device->host copy, then the reference state_dicts
         snaps = [s.snapshot for s in samples]
-        flats = torch.stack([sn.params for sn in snaps]).cpu().numpy()
+        flats_dev = torch.stack([sn.params for sn in snaps])
+        flats = None
         envs = [s.env_params for s in samples]
         layout = snaps[0].layout
+        sd0 = layout.unflatten(flats_dev[0])
+        sdw = _StateDictWriter(sd0)
+        p0 = os.path.join(final, 'EP_policy_0.pt')
+        sdw.save(sd0, p0)
+        sdw.verify(sd0, p0)
+
+        # every policy's tensors at once: per state_dict key, the [E, *shape] fp64 block (transposed back from the
+        # device's [in][out] weights) -- the per-file work is then byte copies and CRCs
+        blocks = layout.unflatten_batch(flats_dev) if sdw.ok else None
+        if blocks is None:
+            flats = flats_dev.cpu().numpy()
 
         def save(i):
-            torch.save(layout.unflatten(flats[i]), os.path.join(final, f'EP_policy_{i}.pt'))
+            if i:
+                path = os.path.join(final, f'EP_policy_{i}.pt')
+                if blocks is not None:
+                    sdw.save_records([b[i] for b in blocks], path)
+                else:
+                    sdw.save(layout.unflatten(flats[i]), path)
             with open(os.path.join(final, f'EP_env_params_{i}.pkl'), 'wb') as fp:
                 pickle.dump(envs[i], fp)
-        # file creation / zip writing release the GIL: a few writer threads overlap them (one EP can hold
-        # thousands of policies)
+        # file creation and writes release the GIL: two writer threads overlap them with the Python work (one EP
+        # can hold thousands of policies; more threads only contend for the GIL)
         from concurrent.futures import ThreadPoolExecutor
-        with ThreadPoolExecutor(max_workers=8) as ex:
+        with ThreadPoolExecutor(max_workers=2) as ex:
             list(ex.map(save, range(len(samples))))
     with open(os.path.join(final, 'objs.txt'), 'w') as fp:
         for obj in ep.obj_batch:

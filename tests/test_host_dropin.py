@@ -101,3 +101,36 @@ def test_host_draws_and_lr_schedule():
     torch.testing.assert_close(z, want.float(), rtol=0, atol=0)
     assert perms.shape == (2, 16) and sorted(perms[0].tolist()) == list(range(16))
     assert linear_lr(0, 100, 3e-4) == 3e-4 and abs(linear_lr(50, 100, 3e-4) - 1.5e-4) < 1e-18
+
+
+def test_templated_state_dict_files_load_like_torch_save(tmp_path):
+    """write_final's _StateDictWriter: every EP_policy_*.pt after the first is the first file's zip image with the
+    tensor records (and their CRC-32s) replaced; torch.load(weights_only=True) must return each state_dict bit for
+    bit, with the reference keys, shapes and fp64 dtype."""
+    from pgmorl_amd.morl import _StateDictWriter
+    lay = ParamLayout(11, 3, 3)
+    rng = np.random.RandomState(4)
+    sds = [lay.unflatten(rng.randn(lay.total).astype(np.float32)) for _ in range(6)]
+    w = _StateDictWriter(sds[0])
+    assert w.ok
+    w.save(sds[0], str(tmp_path / 'p0.pt'))
+    w.verify(sds[0], str(tmp_path / 'p0.pt'))
+    assert w.ok
+    for i, sd in enumerate(sds[1:], 1):
+        w.save(sd, str(tmp_path / f'p{i}.pt'))
+    for i, sd in enumerate(sds):
+        got = torch.load(str(tmp_path / f'p{i}.pt'), weights_only=True)
+        assert list(got) == [k for k, _, _ in STATE_KEYS]
+        for k in sd:
+            assert got[k].dtype == torch.float64 and torch.equal(got[k], sd[k]), (i, k)
+
+
+def test_unflatten_batch_rows_equal_unflatten():
+    lay = ParamLayout(17, 6, 2)
+    flats = np.random.RandomState(1).randn(5, lay.total).astype(np.float32)
+    blocks = lay.unflatten_batch(flats)
+    for i in range(5):
+        sd = lay.unflatten(flats[i])
+        for (key, _, _), b in zip(STATE_KEYS, blocks):
+            assert b[i].dtype == np.float64 and b[i].flags.c_contiguous
+            np.testing.assert_array_equal(b[i], sd[key].numpy())

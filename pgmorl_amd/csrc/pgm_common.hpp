@@ -214,7 +214,7 @@ __device__ __forceinline__ float counter_normal(uint64_t seed, uint64_t i) {
 
 // ---------------------------------------------------------------- diagnostic phase stamps
 // Built only into libpgm_stamps.so (-DPGM_STAMPS): every wave accumulates s_memtime deltas per phase id
-// (< 16); thread 0 of the sampled workgroup adds its totals to pgm_stamp_acc at the end; read back with pgm_debug_stamps().  Never in the shipped .so.
+// (< 24); thread 0 of the sampled workgroup adds its totals to pgm_stamp_acc at the end; read back with pgm_debug_stamps().  Never in the shipped .so.
 #ifdef PGM_STAMPS
 // one accumulator array + reader per translation unit (no relocatable device code)
 #define PGM_STAMP_UNIT(name)                                                                          \
@@ -237,7 +237,7 @@ __device__ __forceinline__ float counter_normal(uint64_t seed, uint64_t i) {
 // add vmcnt waits that drain the kernel's own stores); PGM_STAMP_FLUSH at the kernel's end publishes them
 #define PGM_STAMP_DECL                                                           \
     unsigned long long pgm_stamp_last = __builtin_amdgcn_s_memtime();            \
-    unsigned long long pgm_stamp_reg[16] = {0};
+    unsigned long long pgm_stamp_reg[24] = {0};
 #define PGM_STAMP(id)                                                            \
     do {                                                                         \
         const unsigned long long now_ = __builtin_amdgcn_s_memtime();            \
@@ -247,7 +247,7 @@ __device__ __forceinline__ float counter_normal(uint64_t seed, uint64_t i) {
 #define PGM_STAMP_FLUSH                                                          \
     do {                                                                         \
         if ((int)blockIdx.x == pgm_stamp_block && threadIdx.x == 0)              \
-            for (int i_ = 0; i_ < 16; ++i_)                                      \
+            for (int i_ = 0; i_ < 24; ++i_)                                      \
                 if (pgm_stamp_reg[i_]) atomicAdd(&pgm_stamp_acc[i_], pgm_stamp_reg[i_]); \
     } while (0)
 #else

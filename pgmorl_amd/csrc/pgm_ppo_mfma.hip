@@ -44,10 +44,12 @@ PGM_STAMP_UNIT(mfma)
 #define PGM_U_L2 (PGM_EXP == 1 ? 8 : PGM_EXP == 2 ? 16 : 32)
 #define PGM_U_HEAD (PGM_EXP == 3 ? 4 : PGM_EXP == 4 ? 8 : 32)
 #define PGM_U16 (PGM_EXP == 5 ? 4 : PGM_EXP == 6 ? 8 : 16)
-// PGM_EXP 22 (A/B only): heads of the 32-row kernel on the 16x16x4 MFMA with the per-(sample, output) loss in its
-// C layout, as the 16-row kernel does.  Measured slower at Walker P = 40 (heads + loss 6.9 K -> 8.7 K cycles per
-// Adam step, update 6.57 -> 6.72 ms): every lane then evaluates the loss of 8 samples (two 16-sample blocks) where
-// the VALU heads give each lane one
+// PGM_EXP 22 (A/B only): heads of the 32-row kernel on the 16x16x4 MFMA with the head OUTPUTS on the accumulator
+// rows and the samples on the columns (out^T = Wh . H2^T): a lane holds 4 outputs of one sample, one
+// v_permlane32_swap per register puts the two 16-sample blocks side by side, so every lane evaluates the loss of ONE
+// sample and the head-bias / logstd column sums become 16-lane DPP row sums.  Measured at Walker P = 40: update 6.33
+// ms against the VALU heads' 6.25 (the 32 chained MFMAs and their operand reads cost what the VALU FMAs did).
+// (Samples on the accumulator rows -- the 16-row kernel's orientation -- put 8 samples' losses on every lane: 6.72 ms.)
 #define PGM_HEADS_MFMA (PGM_EXP == 22)
 
 namespace pgm {
@@ -330,7 +332,8 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
             f32x16 gW2[2][2], gW1[2];  // [in tile][out tile], [out tile] (O <= 32: one in tile)
             float gWh[2][Q], gB1[2], gB2[2];
             float gsm = 0.f;  // lanes q < Q: head-bias gradient q; lanes 32 + q (actor): logstd gradient q
-            float gbh = 0.f, gls = 0.f;  // MFMA heads: per-lane partial head-bias / logstd sums (column l & 15)
+            // MFMA heads: per-lane partial head-bias / logstd sums of outputs q = 4 ((l >> 4) & 1) + r
+            float gbq[4] = {0.f, 0.f, 0.f, 0.f}, glq[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
 #pragma unroll
@@ -362,6 +365,7 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                     // ---- layer 1: Z1[s][h] = X[s][:] . W1t[:][h]  (two independent accumulator chains
                     // interleaved: the 32x32x2 f32 MFMA has a 64-cycle dependent-accumulator latency)
                     f32x16 z[2] = {f32x16{0}, f32x16{0}};
+                    f32x16 H1[2];
 #pragma unroll
                     for (int ks = 0; ks < KS1; ++ks) {
                         const int k = 2 * ks + h;
@@ -370,7 +374,6 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
                         for (int hb = 0; hb < 2; ++hb) z[hb] = mfma(av, k < O ? W.W1t[k][hb * TS + c] : 0.f, z[hb]);
                     }
                     if constexpr (LATE_STAGE) stage_next();
-                    f32x16 H1[2];
 #pragma unroll
                     for (int hb = 0; hb < 2; ++hb) {
                         const float bias = W.b1[hb * TS + c];
@@ -405,81 +408,110 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
                         for (int r = 0; r < 16; ++r) scr[rowof(r, h) * SCR + ob * TS + c] = H2[ob][r];
                     wave_lds_fence();
 #if PGM_HEADS_MFMA
-                    // ---- heads on the 16x16x4 MFMA, two 16-sample blocks sb: out[s][q] = H2[s][:] . Wh[q][:] (A from
-                    // the H2 transpose tile, B = Wh rows), leaving every per-(sample, output) loss term in the C layout
-                    // (register r <-> sample 16 sb + 4 g4 + r, lane column c16 <-> head output q): the actor's
-                    // log-prob of a sample is a 16-lane DPP row sum
+                    // ---- heads on the 16x16x4 MFMA: out^T[q][s] = Wh[q][:] . H2[s][:] for two 16-sample blocks sb
+                    // (A = Wh rows, zero for q >= Q; B = the H2 transpose tile).  C layout of block sb: lane l, register
+                    // r <-> output q = 4 (l >> 4) + r of sample 16 sb + (l & 15) (lane groups 2, 3: zero rows)
                     const int g4 = l >> 4, c16 = l & 15;
-                    const bool qv = c16 < Q;
                     f32x4 ho[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+                    // operands in batches of 8 k-steps, all reads of a batch issued before its MFMAs (one LDS latency
+                    // per batch, not per MFMA); the Wh row read unconditionally (clamped) and masked after
+                    const float* whr = &W.Wh[c16 < Q ? c16 : Q - 1][g4];
+                    const float* h2r = scr + c16 * SCR + g4;
+                    const float qm = c16 < Q ? 1.f : 0.f;
 #pragma unroll
-                    for (int ks = 0; ks < H / 4; ++ks) {
-                        const int k = 4 * ks + g4;
-                        const float bw = qv ? W.Wh[qv ? c16 : 0][k] : 0.f;
+                    for (int kb = 0; kb < H / 32; ++kb) {
+                        float aw[8], b0[8], b1[8];
 #pragma unroll
-                        for (int sb = 0; sb < 2; ++sb) ho[sb] = mfma16(scr[(16 * sb + c16) * SCR + k], bw, ho[sb]);
+                        for (int j = 0; j < 8; ++j) {
+                            const int u = 4 * (8 * kb + j);
+                            aw[j] = whr[u];
+                            b0[j] = h2r[u];
+                            b1[j] = h2r[16 * SCR + u];
+                        }
+                        // every read of the batch issued before its first MFMA (the MFMAs depend on this point)
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(aw[j]), "+v"(b0[j]), "+v"(b1[j]));
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) {
+                            ho[0] = mfma16(aw[j] * qm, b0[j], ho[0]);
+                            ho[1] = mfma16(aw[j] * qm, b1[j], ho[1]);
+                        }
                     }
-                    const float bhq = qv ? W.bh[qv ? c16 : 0] : 0.f;
-                    f32x4 dq[2];  // dL/d(head output c16) of sample 16 sb + 4 g4 + r
-                    if (m == 0) {  // value loss over the K objectives (ppo.py:86-94)
+                    // block 1's lane groups 0, 1 -> lanes 32-63: lane l now holds outputs q = 4 gq + r of sample sl
+                    const int gq = (l >> 4) & 1, sl = 16 * h + c16;
+                    float ov[4];
 #pragma unroll
-                        for (int sb = 0; sb < 2; ++sb)
+                    for (int r = 0; r < 4; ++r) {
+                        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(ho[0][r]), __float_as_uint(ho[1][r]),
+                                                                         false, false);
+                        ov[r] = __uint_as_float(sw[0]);
+                    }
+                    PGM_STAMP(16);
+                    // ---- per-sample loss gradients (ppo.py:80-96) of sample sl; lanes l and l ^ 16 share it
+                    const bool ok = ts0 + sl < ns;
+                    float dq[4];
+                    if (m == 0) {  // value loss over the K objectives (q = r of lane group 0)
 #pragma unroll
-                            for (int r = 0; r < 4; ++r) {
-                                const int s = 16 * sb + 4 * g4 + r;
-                                const bool ok = ts0 + s < ns && c16 < K;
-                                const float V = ho[sb][r] + bhq;
-                                const float Vo = rowf(rt, s, O + A + 2 + (c16 < K ? c16 : 0));
-                                const float R = rowf(rt, s, O + A + 2 + K + (c16 < K ? c16 : 0));
-                                float gv, ls;
-                                if (a.hp.use_clipped_value_loss) {
-                                    const float dv = V - Vo;
-                                    const float vc = Vo + fminf(fmaxf(dv, -clip), clip);
-                                    const float l1 = (V - R) * (V - R), l2 = (vc - R) * (vc - R);
-                                    const float inr = (dv >= -clip && dv <= clip) ? 1.f : 0.f;
-                                    gv = wmax2(l1, l2) * 2.f * (V - R) + wmax2(l2, l1) * 2.f * (vc - R) * inr;
-                                    ls = fmaxf(l1, l2);
-                                } else {
-                                    gv = 2.f * (V - R);
-                                    ls = (R - V) * (R - V);
-                                }
-                                dq[sb][r] = ok ? vscale * gv : 0.f;
-                                lsum += ok ? ls : 0.f;
-                                gbh += dq[sb][r];
+                        for (int r = 0; r < 4; ++r) {
+                            const int q = 4 * gq + r;
+                            const bool qv = q < K;
+                            const float V = ov[r] + (qv ? W.bh[qv ? q : 0] : 0.f);
+                            const float Vo = rowf(rt, sl, O + A + 2 + (qv ? q : 0));
+                            const float R = rowf(rt, sl, O + A + 2 + K + (qv ? q : 0));
+                            float gv, ls;
+                            if (a.hp.use_clipped_value_loss) {
+                                const float dv = V - Vo;
+                                const float vc = Vo + fminf(fmaxf(dv, -clip), clip);
+                                const float l1 = (V - R) * (V - R), l2 = (vc - R) * (vc - R);
+                                const float inr = (dv >= -clip && dv <= clip) ? 1.f : 0.f;
+                                gv = wmax2(l1, l2) * 2.f * (V - R) + wmax2(l2, l1) * 2.f * (vc - R) * inr;
+                                ls = fmaxf(l1, l2);
+                            } else {
+                                gv = 2.f * (V - R);
+                                ls = (R - V) * (R - V);
                             }
-                    } else {  // clipped surrogate (ppo.py:80-85); log-probs as row sums over the outputs
-                        const bool av_ = c16 < A;
-                        const float aivq = S.aiv[av_ ? c16 : 0], lsq = av_ ? lstd[av_ ? c16 : 0] : 0.f;
+                            dq[r] = ok && qv ? vscale * gv : 0.f;
+                            if (ok && qv) lsum += ls;  // every (sample, output) sits in exactly one lane
+                            gbq[r] += dq[r];
+                        }
+                    } else {  // clipped surrogate; the log-prob is the sum over the lane pair's outputs
+                        float diff[4], lpe = 0.f;
 #pragma unroll
-                        for (int sb = 0; sb < 2; ++sb)
+                        for (int r = 0; r < 4; ++r) {
+                            const int q = 4 * gq + r;
+                            const bool qv = q < A;
+                            diff[r] = qv ? rowf(rt, sl, O + (qv ? q : 0)) - (ov[r] + W.bh[qv ? q : 0]) : 0.f;
+                            lpe += qv ? -0.5f * diff[r] * diff[r] * S.aiv[qv ? q : 0] - lstd[qv ? q : 0] - LOG_SQRT_2PI
+                                      : 0.f;
+                        }
+                        const float lp = lpe + __shfl_xor(lpe, 16, 64);
+                        const float ratio = expf(lp - rowf(rt, sl, O + A));
+                        const float ad = rowf(rt, sl, O + A + 1);
+                        const float s1 = ratio * ad;
+                        const float s2 = fminf(fmaxf(ratio, 1.f - clip), 1.f + clip) * ad;
+                        const float inr = (ratio >= 1.f - clip && ratio <= 1.f + clip) ? 1.f : 0.f;
+                        const float gr = ad * (wmin2(s1, s2) + wmin2(s2, s1) * inr);
+                        const float dlp = ok ? ascale * gr * ratio : 0.f;
+                        if (ok && gq == 0) lsum += -fminf(s1, s2);
 #pragma unroll
-                            for (int r = 0; r < 4; ++r) {
-                                const int s = 16 * sb + 4 * g4 + r;
-                                const bool ok = ts0 + s < ns;
-                                const float diff = av_ ? rowf(rt, s, O + (av_ ? c16 : 0)) - (ho[sb][r] + bhq) : 0.f;
-                                const float lpe = av_ ? -0.5f * diff * diff * aivq - lsq - LOG_SQRT_2PI : 0.f;
-                                const float lp = row_sum16(lpe);
-                                const float ratio = expf(lp - rowf(rt, s, O + A));
-                                const float ad = rowf(rt, s, O + A + 1);
-                                const float s1 = ratio * ad;
-                                const float s2 = fminf(fmaxf(ratio, 1.f - clip), 1.f + clip) * ad;
-                                const float inr = (ratio >= 1.f - clip && ratio <= 1.f + clip) ? 1.f : 0.f;
-                                const float gr = ad * (wmin2(s1, s2) + wmin2(s2, s1) * inr);
-                                const float dlp = ok ? ascale * gr * ratio : 0.f;
-                                lsum += (ok && c16 == 0) ? -fminf(s1, s2) : 0.f;
-                                dq[sb][r] = av_ ? dlp * diff * aivq : 0.f;
-                                gbh += dq[sb][r];
-                                gls += av_ ? dlp * (diff * diff * aivq - 1.f) : 0.f;
-                            }
+                        for (int r = 0; r < 4; ++r) {
+                            const int q = 4 * gq + r;
+                            const bool qv = q < A;
+                            const float iv = qv ? S.aiv[qv ? q : 0] : 0.f;
+                            dq[r] = qv ? dlp * diff[r] * iv : 0.f;
+                            gbq[r] += dq[r];
+                            glq[r] += qv ? dlp * (diff[r] * diff[r] * iv - 1.f) : 0.f;
+                        }
                     }
                     // dO tile [sample][q] (this wave's): the dH2 A operand (lane = sample) and the head-weight grads
-                    if (qv) {
 #pragma unroll
-                        for (int sb = 0; sb < 2; ++sb)
-#pragma unroll
-                            for (int r = 0; r < 4; ++r) S.dout[w][16 * sb + 4 * g4 + r][qv ? c16 : 0] = dq[sb][r];
+                    for (int r = 0; r < 4; ++r) {
+                        const int q = 4 * gq + r;
+                        if (q < Q) S.dout[w][sl][q < Q ? q : 0] = dq[r];
                     }
+                    PGM_STAMP(17);
                     wave_lds_fence();
+                    PGM_STAMP(18);
 #else
                     // ---- heads on the VALU: lane = sample c, half h sums units [32h, 32h+32)
                     float outv[Q];
@@ -493,6 +525,7 @@ PGM_UNROLL(ONE ? PGM_U_HEAD : 4)
                     }
 #pragma unroll
                     for (int q = 0; q < Q; ++q) outv[q] = half_sum(outv[q]) + W.bh[q];
+                    PGM_STAMP(16);
                     // ---- per-sample loss gradients (ppo.py:80-96); both halves compute the same sample
                     const int si = ts0 + c;
                     const bool ok = si < ns;
@@ -547,7 +580,9 @@ PGM_UNROLL(ONE ? PGM_U_HEAD : 4)
 #pragma unroll
                         for (int q = 0; q < Q; ++q) S.dout[w][c][q] = dO[q];
                     }
+                    PGM_STAMP(17);
                     wave_lds_fence();
+                    PGM_STAMP(18);
                     // per-column sums of the tile (registers: one accumulator per lane instead of Q + A):
                     // lane q sums dO[.][q], lane 32 + q the logstd terms
                     if (c < (h == 0 ? Q : (m == 1 ? A : 0))) {
@@ -662,11 +697,12 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
             }
             lsum = wave_sum64(lsum);
 #if PGM_HEADS_MFMA
-            // per-column sums over the four lane groups: lane c < Q of half 0 holds the head-bias gradient of output
-            // c, lane 32 + c the logstd gradient of action c (the VALU heads' gsm lane map)
-            gbh = group4_sum(gbh);
-            gls = group4_sum(gls);
-            gsm = h == 0 ? gbh : gls;
+            // column sums over the samples: 16-lane rows (one sample block each), then the two blocks
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                gbq[r] = half_sum(row_sum16(gbq[r]));
+                glq[r] = half_sum(row_sum16(glq[r]));
+            }
 #endif
             // entropy with the logstd of this step (before Adam)
             float ent = 0.f;
@@ -734,11 +770,24 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
                         }
                     }
                     if (half == 1) {
+#if PGM_HEADS_MFMA
+                        if (l == 0 || l == 16) {  // lane 16 gq holds the sums of outputs 4 gq .. 4 gq + 3
+                            const float ec = add ? 0.f : a.hp.entropy_coef;
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                const int q = 4 * (l >> 4) + r;
+                                if (q < NQ) acc(oBh + q, gbq[r]);
+                                // -entropy_coef * d(mean entropy)/d logstd enters once (ppo.py:98)
+                                if (m == 1 && q < A) acc(oLs + q, glq[r] - ec);
+                            }
+                        }
+#else
                         if (h == 0 && c < NQ) acc(oBh + c, gsm);
                         if (m == 1 && h == 1 && c < A) {  // -entropy_coef * d(mean entropy)/d logstd enters once (ppo.py:98)
                             const float ec = add ? 0.f : a.hp.entropy_coef;
                             acc(oLs + c, gsm - ec);
                         }
+#endif
                         if (!add) {  // padding slots of a freshly written image
                             Gt[oW2 + l * SCR + H] = 0.f;
                             for (int q = NQ; q < Q; ++q) Gt[oWh + q * H + l] = 0.f;

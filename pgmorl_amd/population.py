@@ -50,7 +50,7 @@ def collect_nearest_data(opt_graph, optgraph_id, threshold=0.1, objs_arr=None, e
     reference's order (parents ascending, each parent's successors in insertion order).
     ``objs_arr`` = np.array(opt_graph.objs) and ``edges`` = _edge_table(opt_graph), when the caller holds them."""
     objs_arr = np.asarray(opt_graph.objs, dtype=np.float64) if objs_arr is None else objs_arr
-    parent, wn, dl = _edge_table(opt_graph) if edges is None else edges
+    parent, wn, dl = (_edge_table(opt_graph) if edges is None else edges)[:3]
     center = objs_arr[optgraph_id]
     near = np.all(np.abs(center - objs_arr) < np.abs(center) * threshold, axis=1)
     sel = near[parent]
@@ -69,26 +69,32 @@ def _edge_table(opt_graph):
     W = np.asarray(opt_graph.weights, dtype=np.float64).reshape(-1, K)
     D = np.asarray(opt_graph.delta_objs, dtype=np.float64).reshape(-1, K)
     wn = W[child] / W[child].sum(axis=1, keepdims=True)
-    return parent, wn, D[child]
+    has_succ = np.zeros(len(par), dtype=bool)
+    has_succ[parent] = True
+    return parent, wn, D[child], has_succ
 
 
 def _count_distinct(weights_data, enough=4):
+    """population_2d.py:39-44: weights i with every earlier weight j at distance >= 1e-5, counted up to
+    ``enough`` (one vectorised distance row per i instead of the reference's pair loop; same predicate)."""
+    W = np.asarray(weights_data, dtype=np.float64)
     cnt = 0
-    for i in range(len(weights_data)):
-        if all(np.linalg.norm(weights_data[i] - weights_data[j]) >= 1e-5 for j in range(i)):
+    for i in range(len(W)):
+        if i == 0 or bool(np.all(np.linalg.norm(W[i] - W[:i], axis=1) >= 1e-5)):
             cnt += 1
             if cnt >= enough:
                 break
     return cnt
 
 
-def _max_useful_threshold(opt_graph, optgraph_id, objs_arr):
+def _max_useful_threshold(opt_graph, optgraph_id, objs_arr, has_succ=None):
     """Smallest threshold beyond which collect_nearest_data cannot grow any more (nodes relative to a
     centre with a zero coordinate need diff < 0 there: never reachable)."""
     center = np.abs(objs_arr[optgraph_id])
     if np.any(center == 0):
         return 0.0
-    has_succ = np.array([len(s) > 0 for s in opt_graph.succ])
+    if has_succ is None:
+        has_succ = np.array([len(s) > 0 for s in opt_graph.succ])
     if not has_succ.any():
         return 0.0
     diff = np.abs(objs_arr[optgraph_id] - objs_arr[has_succ])
@@ -107,7 +113,8 @@ def _fit_inputs(args, opt_graph, optgraph_id, test_weights, bounded_search, objs
     test_weights = np.array(test_weights, dtype=np.float64)
     test_weights = test_weights / test_weights.sum(axis=1, keepdims=True)
     threshold, sigma = 0.1, 0.03
-    t_max = None if bounded_search else _max_useful_threshold(opt_graph, optgraph_id, objs_arr)
+    t_max = None if bounded_search else _max_useful_threshold(opt_graph, optgraph_id, objs_arr,
+                                                              None if edges is None else edges[3])
     while True:
         objs_data, weights_data, delta_objs_data = collect_nearest_data(opt_graph, optgraph_id, threshold, objs_arr,
                                                                         edges)

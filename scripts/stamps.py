@@ -20,7 +20,7 @@ for p in range(P):
     tb.set_task(p, new_policy(tb.O, tb.A, tb.K).state_dict(), {}, None, [0.5, 0.5])
 tb.env_reset()
 L = _lib.lib()
-buf = (C.c_ulonglong * 64)()
+buf = (C.c_ulonglong * 64)()  # per-phase accumulators (ids < 24)
 SB = int(os.environ.get('STAMP_BLOCK', 0))  # workgroup sampled (update SPLIT: 2p = critic, 2p+1 = actor)
 UNITS = ('rollout', 'update', 'mfma', 'lanes', 'wide', 'wupd')
 for name in UNITS:
@@ -33,7 +33,8 @@ names = {0: "loop/top", 1: 'policy fwd', 2: 'store val + sample', 3: 'logp + dyn
 mnames = {0: 'stage rows', 1: 'pass end sync', 2: 'grad image rounds', 3: 'Adam', 8: 'sumsq', 9: 'norm exchange',
           10: 'half image publish + drain', 11: 'flag hand-off + image gather',
           4: 'tile: L1 + L2 fwd', 5: 'tile: heads + loss', 6: 'tile: gWh, dH2, gW2', 7: 'tile: dH1, gW1',
-          12: 'image: lane sums', 13: 'image: stage 0 work', 14: 'image: stage 1 work', 15: 'image: stage 0 barrier'}
+          12: 'image: lane sums', 13: 'image: stage 0 work', 14: 'image: stage 1 work', 15: 'image: stage 0 barrier',
+          16: 'tile: heads (VALU)', 17: 'tile: loss + dO tile', 18: 'tile: dO fence', 5: 'tile: head column sums'}
 lnames = {0: 'loop/top', 1: 'actor fwd', 6: 'sample', 7: 'dynamics', 2: 'accumulators + row', 3: 'barrier',
           4: 'stats', 5: 'emit'}
 wnames = {0: 'noise + layer-1 slices', 1: 'barrier A', 2: 'L1 sum, L2, head, draw', 3: 'barrier C',

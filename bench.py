@@ -191,10 +191,14 @@ def hv_comparison(env_name):
         if not rel:
             continue
         rel = np.array(rel)
-        half = 1.96 * rel.std(ddof=1) / np.sqrt(len(rel)) if len(rel) > 1 else None
+        half = None
+        if len(rel) > 1:  # Student-t 95% interval of the mean per-seed difference
+            from scipy import stats
+            half = float(stats.t.ppf(0.975, len(rel) - 1) * rel.std(ddof=1) / np.sqrt(len(rel)))
         return {'source': [os.path.relpath(dev, ROOT), os.path.relpath(orc, ROOT)], 'config': d.get('config'),
                 'seeds': len(rel), 'hv_rel_diff_per_seed': [float(x) for x in rel],
-                'hv_rel_diff_mean': float(rel.mean()), 'ci95_half_width': None if half is None else float(half)}
+                'hv_rel_diff_mean': float(rel.mean()), 'ci95_half_width': half,
+                'within_1pct_at_95': None if half is None else bool(abs(rel.mean()) + half < 0.01)}
     return None
 
 

@@ -1,10 +1,12 @@
 #!/bin/bash
-# GPU box: the device side of the full-algorithm HV comparison (scripts/hv_full.py) against the committed
-# oracle JSONs.  Usage: bash scripts/hv_device.sh
+# GPU box: the device side of the full-algorithm HV comparison (scripts/hv_full.py) against a committed oracle JSON.
+# Usage: bash scripts/hv_device.sh TAG ORACLE_JSON [ORACLE_JSON ...]   -> gpurun_out/<TAG>_<env>.json
 set -o pipefail
+TAG=${1:-hv}; shift
 OUT=$(pwd)/gpurun_out
 mkdir -p $OUT
-for E in hopper walker; do
-  timeout -k 10 600 python -u scripts/hv_full.py device --ref profiles/r02_hvfull_oracle_$E.json --out $OUT/r02_hvfull_$E.json > $OUT/hvf_dev_$E.log 2>&1 || { echo HV $E FAILED; tail -20 $OUT/hvf_dev_$E.log; exit 1; }
-  tail -1 $OUT/hvf_dev_$E.log
+for REF in "$@"; do
+  E=$(basename $REF .json | sed 's/.*oracle_//')
+  timeout -k 10 600 python -u scripts/hv_full.py device --ref $REF --out $OUT/${TAG}_$E.json > $OUT/${TAG}_$E.log 2>&1 || { echo HV $E FAILED; tail -20 $OUT/${TAG}_$E.log; exit 1; }
+  tail -1 $OUT/${TAG}_$E.log
 done

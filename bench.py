@@ -252,7 +252,21 @@ def whole_run(args, iter_value):
     shutil.rmtree(save, ignore_errors=True)
     v = tm['train_env_steps'] / wall
     per_gen = [(g['rl_s'], g['host_s']) for g in tm['generations']]
+    gens = tm['generations']
+    task_iters = sum(g['tasks'] * g['iters'] for g in gens)
+    iters = sum(g['iters'] for g in gens)
+    mean_tasks = task_iters / max(iters, 1)
+    bench_iter_ms = 1e3 * args.tasks * args.num_processes * args.num_steps / iter_value
+    g0 = gens[0] if gens else None  # the warm-up generation: all 40 tasks, like the iteration bench
     return {'value': v, 'unit': 'env steps/sec', 'wall_s': wall, 'final_s': tm.get('final_s'),
+            # the selection's trajectory sets how many tasks a generation trains ('Too few candidates' shrinks it,
+            # late generations can be empty), so the raw ratio to the 40-task bench mixes overhead with fewer tasks;
+            # the overhead itself is the non-MOPG share of the wall time and the in-run iteration time at P = 40
+            'tasks_per_generation': [g['tasks'] for g in gens], 'mean_active_tasks': mean_tasks,
+            'overhead_share': (wall - tm['rl_s']) / wall,
+            'warmup_iteration_ms': 1e3 * g0['rl_s'] / g0['iters'] if g0 and g0['iters'] else None,
+            'bench_iteration_ms': bench_iter_ms,
+            'vs_iteration_bench_per_task': (v / mean_tasks) / (iter_value / args.tasks) if mean_tasks else None,
             'generation_rl_host_s': per_gen, 'train_env_steps': tm['train_env_steps'],
             'generations': len(tm['generations']), 'mopg_s': tm['rl_s'], 'boundary_host_s': tm['host_s'],
             'init_s': tm['init_s'], 'host_share': tm['host_s'] / wall, 'vs_iteration_bench': v / iter_value,

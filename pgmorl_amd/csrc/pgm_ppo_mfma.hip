@@ -51,6 +51,11 @@ PGM_STAMP_UNIT(mfma)
 // ms against the VALU heads' 6.25 (the 32 chained MFMAs and their operand reads cost what the VALU FMAs did).
 // (Samples on the accumulator rows -- the 16-row kernel's orientation -- put 8 samples' losses on every lane: 6.72 ms.)
 #define PGM_HEADS_MFMA (PGM_EXP == 22)
+// MODE 2 global grad norm: every workgroup of a task gathers all three other half images (its partner half's and both
+// halves of the other tower) and forms the other tower's sum of squares itself, in exactly the owner's element order
+// and reduction tree, so the totals stay bitwise equal in the four workgroups and the separate norm-granule hand-off
+// (one more cross-CU round trip per Adam step) disappears.  PGM_EXP 24 (A/B): the granule hand-off.
+#define PGM_FUSED_NORM (PGM_EXP != 24)
 
 namespace pgm {
 
@@ -216,6 +221,9 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
     // (they wait at that barrier anyway) and retired by the step's last barrier, instead of at the top of the
     // step; wave 0 keeps no DMA in its queue so its polls' vmcnt waits do not include it.  PGM_EXP 32: at the top
     constexpr bool EARLY_STAGE = ONE && MODE == 2 && NBUF == 2 && PGM_EXP != 32;
+    // FUSED_NORM: the early row DMA goes out from waves 1-3 while wave 0 polls the image flags (no norm hand-off left
+    // to hide it under; measured 6.17 -> 6.10 ms against issuing it after the sum of squares, PGM_EXP 26)
+    constexpr bool DMA_POLL = PGM_FUSED_NORM && PGM_EXP != 26;
     constexpr int CR = RS / 4;                         // 16-B chunks per packed row
     constexpr int NDT = (SBk * RSL) / 256;             // LDS-DMA wave instructions per pass (1 KiB each)
     static_assert(NDT * 256 == SBk * RSL, "staging split");
@@ -842,15 +850,28 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
                 lds_sync_m();
                 PGM_STAMP(10);
-                if (t == 0) {
-                    unsigned long long* flag_mine = a.xb + (size_t)slot_mine * a.xslot + a.xslot - 1;
-                    const unsigned long long* flag_other = a.xb + (size_t)slot_other * a.xslot + a.xslot - 1;
-                    __hip_atomic_store(flag_mine, ((unsigned long long)tag << 32) | __float_as_uint(lsum_wg),
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    dbg_delay(a.dbg, nstep, 1);
+                if constexpr (EARLY_STAGE && DMA_POLL) {  // next pass: rows by waves 1-3 while wave 0 polls
+                    if (w != 0) {
+                        if (gp < npass) issue_rows_n(gp & 1, gp & 1, w - 1, ic<3>{});
+                        if (gp + 1 < npass) issue_idx(gp + 1, (gp + 1) & 1, w - 1, 3);
+                    }
+                }
+                // the other tower's half slots (FUSED_NORM: their images are gathered too)
+                const int slot_t0 = ((p * 2 + (1 - m)) * 2 + 0) * 2 + par;
+                const int off_t0 = slot_t0 * a.xslot * 8, off_t1 = (slot_t0 + 2) * a.xslot * 8;
+                constexpr int NPOLL = PGM_FUSED_NORM ? 3 : 1;
+                if (t < NPOLL) {  // lane 0: the partner half; FUSED_NORM lanes 1, 2: the other tower's halves
+                    if (t == 0) {
+                        unsigned long long* flag_mine = a.xb + (size_t)slot_mine * a.xslot + a.xslot - 1;
+                        __hip_atomic_store(flag_mine, ((unsigned long long)tag << 32) | __float_as_uint(lsum_wg),
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                    dbg_delay(a.dbg, nstep, t == 0 ? 1 : 2);
+                    const int pslot = t == 0 ? slot_other : slot_t0 + 2 * (t - 1);
+                    const unsigned long long* flag_p = a.xb + (size_t)pslot * a.xslot + a.xslot - 1;
                     unsigned long long x = 0;
                     for (unsigned spins = 0;; ++spins) {
-                        x = __hip_atomic_load(flag_other, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        x = __hip_atomic_load(flag_p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         if ((unsigned)(x >> 32) == tag) break;
                         if (spins > (1u << 26)) {  // partner never arrived: flag the launch as failed
                             __hip_atomic_store(a.ws + 2 * a.P, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -859,33 +880,75 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
                         }
                         __builtin_amdgcn_s_sleep(1);
                     }
-                    const float lo = __uint_as_float((unsigned)x);
-                    S.red[12] = hs == 0 ? lsum_wg + lo : lo + lsum_wg;
+                    if (t == 0) {
+                        const float lo = __uint_as_float((unsigned)x);
+                        S.red[12] = hs == 0 ? lsum_wg + lo : lo + lsum_wg;
+                    }
                 }
-                lds_sync_m();  // the polling lane matched: every wave may load the partner's image
-                // g = half0 + half1 of this thread's float4 groups i = t + k*MT stays in registers (no LDS
-                // round trip); the sum of squares is fused in, and the Adam operands of the same groups are
-                // read from LDS right away so their latency hides under the norm hand-off below
+                lds_sync_m();  // the polling lanes matched: every wave may load the partners' images
+                // every image load of this thread first (the partner half's; FUSED_NORM: both halves of the other
+                // tower).  (Issuing the next pass's row DMA right behind them, all four waves: 6.16 -> 6.25 ms.)
+                u32x4 vo[NG4];
+#pragma unroll
+                for (int k = 0; k < NG4; ++k)
+                    vo[k] = __builtin_amdgcn_raw_buffer_load_b128(xr, off_other + 16 * min(t + k * MT, NV4 - 1), 0, SC1);
+                float ovt = 0.f;
+                if (t < TAIL)
+                    ovt = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, off_other + 16 * NV4 + 4 * t, 0, SC1));
+#if PGM_FUSED_NORM
+                u32x4 o0[NG4], o1[NG4];
 #pragma unroll
                 for (int k = 0; k < NG4; ++k) {
                     const int i = min(t + k * MT, NV4 - 1);
-                    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(xr, off_other + 16 * i, 0, SC1);
+                    o0[k] = __builtin_amdgcn_raw_buffer_load_b128(xr, off_t0 + 16 * i, 0, SC1);
+                    o1[k] = __builtin_amdgcn_raw_buffer_load_b128(xr, off_t1 + 16 * i, 0, SC1);
+                }
+                float ot0 = 0.f, ot1 = 0.f;
+                if (t < TAIL) {
+                    ot0 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, off_t0 + 16 * NV4 + 4 * t, 0, SC1));
+                    ot1 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, off_t1 + 16 * NV4 + 4 * t, 0, SC1));
+                }
+#endif
+                // g = half0 + half1 of this thread's float4 groups i = t + k*MT stays in registers (no LDS
+                // round trip); the sum of squares is fused in
+#pragma unroll
+                for (int k = 0; k < NG4; ++k) {
+                    const int i = min(t + k * MT, NV4 - 1);
                     const float4 mine = *reinterpret_cast<const float4*>(&G0[4 * i]);
                     const float mv[4] = {mine.x, mine.y, mine.z, mine.w};
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
-                        const float ov = __uint_as_float(v[q]);
+                        const float ov = __uint_as_float(vo[k][q]);
                         ag[k][q] = hs == 0 ? mv[q] + ov : ov + mv[q];
                         if (t + k * MT < NV4) sq2 = fmaf(ag[k][q], ag[k][q], sq2);
                     }
                 }
                 if (t < TAIL) {
-                    const float ov = __uint_as_float(
-                        __builtin_amdgcn_raw_buffer_load_b32(xr, off_other + 16 * NV4 + 4 * t, 0, SC1));
                     const float mine = G0[4 * NV4 + t];
-                    agt = hs == 0 ? mine + ov : ov + mine;
+                    agt = hs == 0 ? mine + ovt : ovt + mine;
                     sq2 = fmaf(agt, agt, sq2);
                 }
+#if PGM_FUSED_NORM
+                // the other tower's g = half0 + half1 and its sum of squares, element by element in the owner's order
+                // (the owner forms the same sums from its own half and this very slot pair)
+                {
+                    float sqo = 0.f;
+#pragma unroll
+                    for (int k = 0; k < NG4; ++k)
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            const float g = __uint_as_float(o0[k][q]) + __uint_as_float(o1[k][q]);
+                            if (t + k * MT < NV4) sqo = fmaf(g, g, sqo);
+                        }
+                    if (t < TAIL) {
+                        const float g = ot0 + ot1;
+                        sqo = fmaf(g, g, sqo);
+                    }
+                    sqo = wave_sum64(sqo);
+                    if (l == 0) S.red[4 + w] = sqo;
+                }
+#endif
+                // the Adam operands of the same groups
 #pragma unroll
                 for (int k = 0; k < NG4; ++k) {
                     const int i = min(t + k * MT, NV4 - 1);
@@ -913,13 +976,16 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
             lds_sync_m();
             PGM_STAMP(8);
             float total = (S.red[0] + S.red[1]) + (S.red[2] + S.red[3]);
-            if constexpr (EARLY_STAGE) {  // next pass: rows by waves 1-3 (retired by the step's last barrier)
+            if constexpr (EARLY_STAGE && !DMA_POLL) {  // next pass: rows by waves 1-3 (retired by the step's last barrier)
                 if (w != 0) {
                     if (gp < npass) issue_rows_n(gp & 1, gp & 1, w - 1, ic<3>{});
                     if (gp + 1 < npass) issue_idx(gp + 1, (gp + 1) & 1, w - 1, 3);
                 }
             }
-            if constexpr (SPLIT) {  // tagged 8-byte granule hand-off with the other tower's workgroup
+            if constexpr (SPLIT && NS == 2 && PGM_FUSED_NORM) {  // the other tower's total, formed here
+                const float other = (S.red[4] + S.red[5]) + (S.red[6] + S.red[7]);
+                total = m == 0 ? total + other : other + total;  // critic + actor in all four workgroups
+            } else if constexpr (SPLIT) {  // tagged 8-byte granule hand-off with the other tower's workgroup
                 if (t == 0) {
                     const unsigned tag = (unsigned)(nstep + 1);
                     unsigned long long* ws = a.ws + ppo_norm_granule(a.P, p, 0, hs, nstep & 1);

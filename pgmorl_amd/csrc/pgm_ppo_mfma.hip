@@ -1046,10 +1046,7 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
                     float* v4 = &av[k].x;
                     float* p4 = &ap[k].x;
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        adam1(g4[q], m4[q], v4[q], p4[q]);
-                        if (m == 1 && 4 * i + q >= oLs && 4 * i + q < oLs + A) S.aiv[4 * i + q - oLs] = expf(-2.f * p4[q]);
-                    }
+                    for (int q = 0; q < 4; ++q) adam1(g4[q], m4[q], v4[q], p4[q]);
                     *reinterpret_cast<float4*>(&S.MV[4 * i]) = am[k];
                     *reinterpret_cast<float4*>(&S.MV[IMG + 4 * i]) = av[k];
                     *reinterpret_cast<float4*>(&Pf[4 * i]) = ap[k];
@@ -1061,7 +1058,21 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
                     S.MV[i] = mm;
                     S.MV[IMG + i] = vv;
                     Pf[i] = pp;
-                    if (m == 1 && i >= oLs && i < oLs + A) S.aiv[i - oLs] = expf(-2.f * pp);
+                }
+                // exp(-2 logstd) of the new actor logstd, by the compile-time owners of elements oLs .. oLs + A - 1
+                // (inside the element loop it put a branch + exp on every element of those groups)
+                if (m == 1) {
+#pragma unroll
+                    for (int j = 0; j < A; ++j) {
+                        constexpr int e0 = oLs;
+                        const int e = e0 + j;
+                        if (e < 4 * NV4) {
+                            const int i4 = e >> 2, k = i4 / MT;
+                            if (t == i4 - k * MT) S.aiv[j] = expf(-2.f * (&ap[k].x)[e & 3]);
+                        } else if (t == e - 4 * NV4) {
+                            S.aiv[j] = expf(-2.f * Pf[e]);
+                        }
+                    }
                 }
             } else if constexpr (SPLIT) {
                 // batches of 4 elements per thread: every LDS read of a batch before any write
@@ -1830,6 +1841,11 @@ PGM_UNROLL(ONE ? PGM_U16 : 4)
 #pragma unroll
             for (int i = 0; i < W; ++i) total += S.red[i];
             PGM_STAMP(8);
+            // this step's Adam scalars (fp64 bias corrections) while the norm granule travels
+            const double b1n = b1p * (double)b1c, b2n = b2p * (double)b2c;
+            float step_size = (float)(lr / (1.0 - b1n));
+            float inv_bc2s = 1.f / (float)sqrt(1.0 - b2n);
+            asm volatile("" : "+v"(step_size), "+v"(inv_bc2s));  // formed HERE (the compiler would sink them)
             if constexpr (EARLY_STAGE) {  // next pass (gp after the pass loop): rows by waves 1..W-1
                 if (w != 0) {
                     if (gp < npass) issue_rows_n(gp & 1, gp & 1, w - 1, ic<W - 1>{});
@@ -1868,12 +1884,8 @@ PGM_UNROLL(ONE ? PGM_U16 : 4)
             }
             // ---- Adam from registers (padding: g = m = v = 0 keeps p = 0)
             ++nstep;
-            b1p *= (double)b1c;
-            b2p *= (double)b2c;
-            const double bc1 = 1.0 - b1p;
-            const double bc2 = 1.0 - b2p;
-            const float step_size = (float)(lr / bc1);
-            const float inv_bc2s = 1.f / (float)sqrt(bc2);
+            b1p = b1n;
+            b2p = b2n;
             auto adam1 = [&](float gg, float& mm, float& vv, float& pp) {
                 const float gc = gg * coef;
                 mm = mm + (1.f - b1c) * (gc - mm);
@@ -1892,7 +1904,6 @@ PGM_UNROLL(ONE ? PGM_U16 : 4)
                     am[k][q] = mm;
                     av[k][q] = vv;
                     ap[k][q] = pp;
-                    if (m == 1 && 4 * i + q >= oLs && 4 * i + q < oLs + A) S.aiv[4 * i + q - oLs] = expf(-2.f * pp);
                 }
                 *reinterpret_cast<float4*>(&S.MV[4 * i]) = make_float4(am[k][0], am[k][1], am[k][2], am[k][3]);
                 *reinterpret_cast<float4*>(&S.MV[IMG + 4 * i]) = make_float4(av[k][0], av[k][1], av[k][2], av[k][3]);
@@ -1905,7 +1916,18 @@ PGM_UNROLL(ONE ? PGM_U16 : 4)
                 S.MV[i] = mm;
                 S.MV[IMG + i] = vv;
                 Pf[i] = pp;
-                if (m == 1 && i >= oLs && i < oLs + A) S.aiv[i - oLs] = expf(-2.f * pp);
+            }
+            if (m == 1) {  // exp(-2 logstd) of the new actor logstd by the compile-time owners of its elements
+#pragma unroll
+                for (int j = 0; j < A; ++j) {
+                    const int e = oLs + j;
+                    if (e < 4 * NV4) {
+                        const int i4 = e >> 2, k = i4 / NT;
+                        if (t == i4 - k * NT) S.aiv[j] = expf(-2.f * ap[k][e & 3]);
+                    } else if (t == e - 4 * NV4) {
+                        S.aiv[j] = expf(-2.f * Pf[e]);
+                    }
+                }
             }
             if constexpr (EARLY_STAGE) dma_sync_m();  // + the next pass's rows landed
             else lds_sync_m();  // parameters updated before the next minibatch; GA region reused as scr

@@ -26,6 +26,7 @@
 //   evaluation()                           morl/mopg.py:25-46
 #include "pgm_dispatch.hpp"
 #include "pgm_rollout.hpp"
+#include <utility>
 
 PGM_STAMP_UNIT(lanes)
 
@@ -39,6 +40,85 @@ constexpr bool lanes_fit() { return O <= 48 && O + K + 1 <= 64; }
 #ifndef PGM_ROLL_L2_LDS
 #define PGM_ROLL_L2_LDS 0  // 1: layer-2 inputs through the per-wave LDS row (A/B)
 #endif
+#ifndef PGM_EXP
+#define PGM_EXP 0
+#endif
+// Policy forward with both layers' inputs broadcast by DPP from registers (row_copies + row_newbcast) instead of
+// the LDS input row (layer 1) and 64 v_readlane (layer 2).  PGM_EXP 40 (A/B): the LDS / readlane forward.
+#define PGM_ROLL_DPP (PGM_EXP != 40)
+
+template <class F, int... I>
+__device__ __forceinline__ void static_for_impl(F& f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// NR row-broadcast copies of v: copy j holds, in EVERY 16-lane row, row j of v (lane 16 r + i <- lane 16 j + i).
+// One v_permlane32_swap (rows [0 1 0 1] / [2 3 2 3]) and one v_permlane16_swap per pair of copies.
+template <int NR>
+__device__ __forceinline__ void row_copies(float v, float (&V)[NR]) {
+    static_assert(NR >= 1 && NR <= 4, "1..4 rows");
+    const unsigned u = __float_as_uint(v);
+    const auto p = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+    const auto q0 = __builtin_amdgcn_permlane16_swap(p[0], p[0], false, false);
+    V[0] = __uint_as_float(q0[0]);
+    if constexpr (NR > 1) V[1] = __uint_as_float(q0[1]);
+    if constexpr (NR > 2) {
+        const auto q1 = __builtin_amdgcn_permlane16_swap(p[1], p[1], false, false);
+        V[2] = __uint_as_float(q1[0]);
+        if constexpr (NR > 3) V[3] = __uint_as_float(q1[1]);
+    }
+}
+// acc[i & 3] += (lane i of this lane's 16-lane row of v) * w[i], i = 0..NK-1: v_fmac_f32 with a DPP row_newbcast:i
+// source operand (gfx90a+; the compiler's DPP combiner does not fold a row_newbcast mov into fmac).  The leading
+// s_nop covers the VALU-write -> DPP-read hazard on v (the asm hides the DPP read from the hazard recognizer).
+template <int I, int NK>
+__device__ __forceinline__ void fmac_one(float (&acc)[4], float v, const float (&wv)[16]) {
+    if constexpr (I < NK) {
+        if constexpr (I == 0)
+            asm("s_nop 1\n\tv_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                : "+v"(acc[I & 3]) : "v"(v), "v"(wv[I]), "i"(I));
+        else
+            asm("v_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                : "+v"(acc[I & 3]) : "v"(v), "v"(wv[I]), "i"(I));
+        fmac_one<I + 1, NK>(acc, v, wv);
+    }
+}
+template <int NK>
+__device__ __forceinline__ void fmac_row_bcast(float (&acc)[4], float v, const float* w) {
+    static_assert(NK >= 1 && NK <= 16, "1..16 lanes");
+    float wv[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) wv[i] = i < NK ? w[i] : 0.f;
+    if constexpr (NK == 16) {
+        asm("s_nop 1\n\t"
+            "v_fmac_f32_dpp %0, %4, %5 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+            "v_fmac_f32_dpp %1, %4, %6 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+            "v_fmac_f32_dpp %2, %4, %7 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+            "v_fmac_f32_dpp %3, %4, %8 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+            "v_fmac_f32_dpp %0, %4, %9 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+            "v_fmac_f32_dpp %1, %4, %10 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+            "v_fmac_f32_dpp %2, %4, %11 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+            "v_fmac_f32_dpp %3, %4, %12 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+            "v_fmac_f32_dpp %0, %4, %13 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+            "v_fmac_f32_dpp %1, %4, %14 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+            "v_fmac_f32_dpp %2, %4, %15 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+            "v_fmac_f32_dpp %3, %4, %16 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+            "v_fmac_f32_dpp %0, %4, %17 row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+            "v_fmac_f32_dpp %1, %4, %18 row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
+            "v_fmac_f32_dpp %2, %4, %19 row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
+            "v_fmac_f32_dpp %3, %4, %20 row_newbcast:15 row_mask:0xf bank_mask:0xf"
+            : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3])
+            : "v"(v), "v"(wv[0]), "v"(wv[1]), "v"(wv[2]), "v"(wv[3]), "v"(wv[4]), "v"(wv[5]), "v"(wv[6]), "v"(wv[7]),
+              "v"(wv[8]), "v"(wv[9]), "v"(wv[10]), "v"(wv[11]), "v"(wv[12]), "v"(wv[13]), "v"(wv[14]), "v"(wv[15]));
+    } else {
+        // partial row (the last input row of layer 1): one asm per lane, the first behind the hazard nop
+        fmac_one<0, NK>(acc, v, wv);
+    }
+}
 
 // per-lane actor tower: unit l of both layers, every head row of unit l (weights constant in a launch)
 template <int O, int A>
@@ -115,6 +195,32 @@ struct ActorLane {
 #if PGM_ROLL_L2_LDS
         wave_lds_fence_r();  // every lane's h1 reads done before the row is rewritten
 #endif
+    }
+    // the same action mean from registers: lane k < O holds input feature k (other lanes: anything).  Every input
+    // reaches every lane by a row copy + row_newbcast DPP operand of the FMA (no LDS round trip, no v_readlane);
+    // four accumulator chains per layer.
+    __device__ void forward_reg(float xv, int l, float (&mu)[A]) const {
+        constexpr int R1 = (O + 15) / 16;
+        float X[R1];
+        row_copies<R1>(xv, X);
+        float z[4] = {b1, 0.f, 0.f, 0.f};
+        static_for<R1>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            fmac_row_bcast<(O - 16 * j < 16 ? O - 16 * j : 16)>(z, X[j], &w1[16 * j]);
+        });
+        const float hl = tanh_fast((z[0] + z[1]) + (z[2] + z[3]));
+        float Hc[4];
+        row_copies<4>(hl, Hc);
+        float y[4] = {b2, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fmac_row_bcast<16>(y, Hc[j], &w2[16 * j]);
+        const float h2 = tanh_fast((y[0] + y[1]) + (y[2] + y[3]));
+        float pr[A];
+#pragma unroll
+        for (int j = 0; j < A; ++j) pr[j] = h2 * wm[j];
+        wave_sum64_multi<A>(pr, mu);
+#pragma unroll
+        for (int j = 0; j < A; ++j) mu[j] += bm[j];
     }
 };
 
@@ -337,14 +443,17 @@ __global__ __launch_bounds__(512) void rollout_lane_kernel(RolloutArgs a) {
         const bool upd0 = role == 0 && nc.use_ob;
 
         // ---- slot 0: after_update() carry (storage.py:71-75) and the first policy input
+        float xr[NE];  // PGM_ROLL_DPP: normalised input feature l of env slot e (lanes < O), else S.x
 #pragma unroll
         for (int e = 0; e < NE; ++e) {
+            xr[e] = 0.f;
             const int n = w + 4 * e;
             if (n >= NN) break;
             if (fl) {
                 float v = obs[(size_t)(a.carry ? T : 0) * NN * O + n * O + l];
                 if (a.carry) obs[n * O + l] = v;
-                S.x[n][l] = v;
+                if (PGM_ROLL_DPP) xr[e] = v;
+                else S.x[n][l] = v;
             }
             if (a.carry && l == 0) {
                 masks[n] = masks[(size_t)T * NN + n];
@@ -395,25 +504,42 @@ __global__ __launch_bounds__(512) void rollout_lane_kernel(RolloutArgs a) {
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): preamble loads retired where the compiler sees it
         if (NCH < T) load_eps(1);
         wave_lds_fence_r();
+        // this step's noise comes from registers loaded one step ahead (ejn), so no LDS latency sits between the
+        // forward and the Gaussian draw; chunk c + 1 is staged at the last step of chunk c for that read.  (Not
+        // where the extra registers would spill: two env slots per wave or A > 6 read it in the step.)
+        constexpr bool PREF = NE == 1 && A <= 6;
+        float ejn[1][A];
+#pragma unroll
+        for (int j = 0; j < A; ++j) ejn[0][j] = PREF ? S.eps[0][min(w, NN - 1)][j] : 0.f;
 
         for (int step = 0; step < T; ++step) {
             const int buf = step & 1;
-            const int cs = step % NCH, cb = (step / NCH) & 1;
-            if (cs == 0 && step > 0) {  // chunk step / NCH (loaded a chunk ago) into LDS; load the next one
-                store_eps(cb);
-                if (step + NCH < T) load_eps(step / NCH + 1);
+            const int cs = step % NCH;
+            if (cs == NCH - 1 && step + 1 < T) {  // chunk (step+1) / NCH (loaded a chunk ago) into LDS; load the next
+                store_eps(((step + 1) / NCH) & 1);
+                if (step + 1 + NCH < T) load_eps((step + 1) / NCH + 1);
                 wave_lds_fence_r();
+            }
+            float ejc[A];  // PREF: this step's noise of env slot 0 (from ejn); the next step's goes into ejn
+            if constexpr (PREF) {
+                const int n = min(w, NN - 1), s1 = step + 1 < T ? step + 1 : step;
+#pragma unroll
+                for (int j = 0; j < A; ++j) {
+                    ejc[j] = ejn[0][j];
+                    ejn[0][j] = S.eps[(s1 / NCH) & 1][n][(s1 % NCH) * A + j];
+                }
             }
             PGM_STAMP(0);
 #pragma unroll
             for (int e = 0; e < NE; ++e) {
                 const int n = w + 4 * e;
                 if (n >= NN) break;
-                float ej[A];  // this step's noise, read before the forward so its LDS latency hides there
+                float ej[A];
 #pragma unroll
-                for (int j = 0; j < A; ++j) ej[j] = S.eps[cb][n][cs * A + j];
+                for (int j = 0; j < A; ++j) ej[j] = PREF ? ejc[j] : S.eps[(step / NCH) & 1][n][cs * A + j];
                 float mu[A];
-                pol.forward(S.x[n], S.h1[w], l, mu);
+                if constexpr (PGM_ROLL_DPP) pol.forward_reg(xr[e], l, mu);
+                else pol.forward(S.x[n], S.h1[w], l, mu);
                 PGM_STAMP(1);
                 // Gaussian draw (torch.normal(mean, std) = eps * std + mean), log-prob and clipped action, all
                 // wave-uniform; lanes 0..A-1 store the action row, lane 0 its log-prob
@@ -465,10 +591,11 @@ __global__ __launch_bounds__(512) void rollout_lane_kernel(RolloutArgs a) {
                 double v = s_o[e];
                 if (nc.use_ob) v = clipd_s((v - mean) * inv, -nc.clipob, nc.clipob);
                 const float f = (float)v;  // VecPyTorch .float() (envs.py:192)
-                if (role == 0) S.x[n][l] = f;
+                if constexpr (PGM_ROLL_DPP) xr[e] = f;
+                else if (role == 0) S.x[n][l] = f;
                 store_lane(r_obs, role == 0 ? (uint32_t)(((size_t)(step + 1) * NN + n) * O + l) * 4 : OOB_OFF, f);
             }
-            wave_lds_fence_r();
+            if constexpr (!PGM_ROLL_DPP) wave_lds_fence_r();
             PGM_STAMP(5);
         }
         lds_sync();  // the objective waves' drain merge
@@ -707,14 +834,20 @@ __global__ __launch_bounds__(64 * EVAL_MAX_WAVES) void eval_wave_kernel(EvalArgs
 #pragma unroll
         for (int k = 0; k < K; ++k) acc[k] = 0.0;
         for (int st = 0; st < maxs; ++st) {  // SynthMO episodes end at the time limit
-            if (fl) {
-                double v = s;
-                if (a.use_ob) v = clipd((v - mean) * inv, -10.0, 10.0);
-                S.x[w][l] = (float)v;
-            }
-            wave_lds_fence_r();
             float mu[A];
-            pol.forward(S.x[w], S.h1[w], l, mu);
+            if constexpr (PGM_ROLL_DPP) {
+                double v = s;  // (lanes >= O: ignored by the broadcast)
+                if (a.use_ob) v = clipd((v - mean) * inv, -10.0, 10.0);
+                pol.forward_reg((float)v, l, mu);
+            } else {
+                if (fl) {
+                    double v = s;
+                    if (a.use_ob) v = clipd((v - mean) * inv, -10.0, 10.0);
+                    S.x[w][l] = (float)v;
+                }
+                wave_lds_fence_r();
+                pol.forward(S.x[w], S.h1[w], l, mu);
+            }
             double ac[A], sq[A];
 #pragma unroll
             for (int j = 0; j < A; ++j) {  // deterministic action = mean, clipped by the env

@@ -75,25 +75,28 @@ __device__ __forceinline__ void row_copies(float v, float (&V)[NR]) {
 // acc[i & 3] += (lane i of this lane's 16-lane row of v) * w[i], i = 0..NK-1: v_fmac_f32 with a DPP row_newbcast:i
 // source operand (gfx90a+; the compiler's DPP combiner does not fold a row_newbcast mov into fmac).  The leading
 // s_nop covers the VALU-write -> DPP-read hazard on v (the asm hides the DPP read from the hazard recognizer).
-template <int I, int NK>
-__device__ __forceinline__ void fmac_one(float (&acc)[4], float v, const float (&wv)[16]) {
+template <int I, int NK, int NA>
+__device__ __forceinline__ void fmac_one(float (&acc)[NA], float v, const float (&wv)[16]) {
     if constexpr (I < NK) {
         if constexpr (I == 0)
             asm("s_nop 1\n\tv_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
-                : "+v"(acc[I & 3]) : "v"(v), "v"(wv[I]), "i"(I));
+                : "+v"(acc[I % NA]) : "v"(v), "v"(wv[I]), "i"(I));
         else
             asm("v_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
-                : "+v"(acc[I & 3]) : "v"(v), "v"(wv[I]), "i"(I));
-        fmac_one<I + 1, NK>(acc, v, wv);
+                : "+v"(acc[I % NA]) : "v"(v), "v"(wv[I]), "i"(I));
+        fmac_one<I + 1, NK, NA>(acc, v, wv);
     }
 }
-template <int NK>
-__device__ __forceinline__ void fmac_row_bcast(float (&acc)[4], float v, const float* w) {
+// acc[i % NA] += (lane i of this lane's 16-lane row of v) * w[i], i = 0..NK-1: v_fmac_f32 with a DPP row_newbcast:i
+// source operand (gfx90a+; the compiler's DPP combiner does not fold a row_newbcast mov into fmac).  The leading
+// s_nop covers the VALU-write -> DPP-read hazard on v (the asm hides the DPP read from the hazard recognizer).
+template <int NK, int NA>
+__device__ __forceinline__ void fmac_row_bcast(float (&acc)[NA], float v, const float* w) {
     static_assert(NK >= 1 && NK <= 16, "1..16 lanes");
     float wv[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) wv[i] = i < NK ? w[i] : 0.f;
-    if constexpr (NK == 16) {
+    if constexpr (NK == 16 && NA == 4) {
         asm("s_nop 1\n\t"
             "v_fmac_f32_dpp %0, %4, %5 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
             "v_fmac_f32_dpp %1, %4, %6 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
@@ -115,8 +118,8 @@ __device__ __forceinline__ void fmac_row_bcast(float (&acc)[4], float v, const f
             : "v"(v), "v"(wv[0]), "v"(wv[1]), "v"(wv[2]), "v"(wv[3]), "v"(wv[4]), "v"(wv[5]), "v"(wv[6]), "v"(wv[7]),
               "v"(wv[8]), "v"(wv[9]), "v"(wv[10]), "v"(wv[11]), "v"(wv[12]), "v"(wv[13]), "v"(wv[14]), "v"(wv[15]));
     } else {
-        // partial row (the last input row of layer 1): one asm per lane, the first behind the hazard nop
-        fmac_one<0, NK>(acc, v, wv);
+        // one asm per lane (partial rows, or NA != 4: the compiler schedules them), the first behind the hazard nop
+        fmac_one<0, NK, NA>(acc, v, wv);
     }
 }
 
@@ -206,14 +209,20 @@ struct ActorLane {
         float z[4] = {b1, 0.f, 0.f, 0.f};
         static_for<R1>([&](auto jc) {
             constexpr int j = decltype(jc)::value;
-            fmac_row_bcast<(O - 16 * j < 16 ? O - 16 * j : 16)>(z, X[j], &w1[16 * j]);
+            fmac_row_bcast<(O - 16 * j < 16 ? O - 16 * j : 16), 4>(z, X[j], &w1[16 * j]);
         });
         const float hl = tanh_fast((z[0] + z[1]) + (z[2] + z[3]));
         float Hc[4];
         row_copies<4>(hl, Hc);
-        float y[4] = {b2, 0.f, 0.f, 0.f};
+        constexpr int NA2 = PGM_EXP == 41 ? 8 : 4;  // layer-2 accumulator chains (A/B)
+        float y[NA2];
+        y[0] = b2;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) fmac_row_bcast<16>(y, Hc[j], &w2[16 * j]);
+        for (int i = 1; i < NA2; ++i) y[i] = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fmac_row_bcast<16, NA2>(y, Hc[j], &w2[16 * j]);
+#pragma unroll
+        for (int i = 4; i < NA2; ++i) y[i - 4] += y[i];
         const float h2 = tanh_fast((y[0] + y[1]) + (y[2] + y[3]));
         float pr[A];
 #pragma unroll

@@ -388,17 +388,18 @@ __global__ __launch_bounds__(512) void rollout_lane_kernel(RolloutArgs a) {
     // statistics merge of this lane's role (counts from before the merge; numpy's mean / var divide by N,
     // exact for N a power of two); prep_merge() ran since the last merge
     auto merge = [&](int buf, bool active) {
-        double v[NN], sum = 0.0;
+        double v[NN];
 #pragma unroll
-        for (int n = 0; n < NN; ++n) {
-            v[n] = S.sr[buf][n][l];
-            sum += v[n];
-        }
+        for (int n = 0; n < NN; ++n) v[n] = S.sr[buf][n][l];
+        double sum = v[0];  // numpy's add.reduce order over the env axis
+#pragma unroll
+        for (int n = 1; n < NN; ++n) sum += v[n];
         constexpr double rn = 1.0 / NN;
         const double bm = sum * rn;
-        double sq = 0.0;
+        double d2[NN];
 #pragma unroll
-        for (int n = 0; n < NN; ++n) sq = fma(v[n] - bm, v[n] - bm, sq);
+        for (int n = 0; n < NN; ++n) d2[n] = (v[n] - bm) * (v[n] - bm);
+        const double sq = tree_sum(d2);  // (squared deviations summed pairwise: half the dependent adds)
         if (upd && active) {
             const double delta = bm - mean;
             mean = mean + delta * (double)NN * itot;
@@ -413,6 +414,9 @@ __global__ __launch_bounds__(512) void rollout_lane_kernel(RolloutArgs a) {
 
     if (chain) {
         // =========================================================== chain waves
+        // issue priority over the objective waves that share their SIMDs (those only fill the chain's stalls).
+        // PGM_EXP 42 (A/B): equal priority
+        if constexpr (PGM_EXP != 42) __builtin_amdgcn_s_setprio(3);
         const float* prm = a.params + (size_t)p * L.total;
         float* act = a.rb.actions + (size_t)p * T * NN * A;
         float* logp = a.rb.logp + (size_t)p * T * NN;
@@ -564,6 +568,9 @@ __global__ __launch_bounds__(512) void rollout_lane_kernel(RolloutArgs a) {
                     sq[j] = ac[j] * ac[j];
                     pu[j] = U[j] * ac[j];
                 }
+                // |clip(a)|^2 for the objective side, formed here (beside the tanh chain, not behind it)
+                double e2v = tree_sum(sq);
+                asm volatile("" : "+v"(e2v));
                 // dynamics (fp64, lane = feature): s' = tanh(d s + U clip(a) + c)
                 const double sn = tanh_d3(dd * s_o[e] + tree_sum(pu) + cc, S.t2);
                 const float lp = tree_sum(lpt);
@@ -579,7 +586,7 @@ __global__ __launch_bounds__(512) void rollout_lane_kernel(RolloutArgs a) {
                 if (role == 0) S.sr[buf][n][l] = s_o[e];  // lanes O.. of the row belong to the objective waves
                 S.sn[buf][n][l] = sn;
                 if (l == 0) {
-                    S.e2[buf][n] = tree_sum(sq);
+                    S.e2[buf][n] = e2v;
                     S.dn[buf][n] = dn;
                 }
                 const uint32_t moff = (uint32_t)((size_t)(step + 1) * NN + n) * 4;

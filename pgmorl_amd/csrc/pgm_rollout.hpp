@@ -88,14 +88,27 @@ __device__ __forceinline__ V tree_sum(const V (&x)[M]) {
     }
 }
 
-// 1 / sqrt(x) in fp64: hardware estimate + two Newton steps (~1 ulp; the IEEE sqrt + divide pair is a
+// Newton steps after the hardware fp64 rcp / rsq estimates on the rollout's step chain.  Measured on gfx950
+// (tests/hip/f64_rcp_rsq_probe.hip, profiles/r03d_f64_rcp_rsq_probe.txt): the estimates are good to ~5e-8, one
+// step to <= 2.2e-15 (rcp) / 4.3e-15 (rsq) relative, two steps to <= 1.2 ulp.  Two steps: one step measured no
+// faster (Walker P = 40 iteration 8.036 vs 8.028 ms, profiles/r03e_*), so the chain keeps full fp64 precision.
+// PGM_EXP 43 (A/B): one step.
+#ifndef PGM_EXP
+#define PGM_EXP 0
+#endif
+#define PGM_FP64_NEWTON (PGM_EXP == 43 ? 1 : 2)
+
+// 1 / sqrt(x) in fp64: hardware estimate + PGM_FP64_NEWTON Newton steps (the IEEE sqrt + divide pair is a
 // ~25-instruction dependent chain on the per-step critical path)
 __device__ __forceinline__ double rsqrt_d(double x) {
     double r = __builtin_amdgcn_rsq(x);
     double e = fma(-x * r, r, 1.0);
     r = fma(r * e, 0.5, r);
-    e = fma(-x * r, r, 1.0);
-    return fma(r * e, 0.5, r);
+    if constexpr (PGM_FP64_NEWTON > 1) {
+        e = fma(-x * r, r, 1.0);
+        r = fma(r * e, 0.5, r);
+    }
+    return r;
 }
 
 // fp64 tanh for the SynthMO dynamics: 1 - 2 / (exp(2|y|) + 1) with the sign restored; exp through
@@ -112,8 +125,8 @@ __device__ __forceinline__ double tanh_d2(double y) {
 
 // fp64 tanh with a table-driven exp: exp(x) = 2^m 2^(j/32) p(r), x = (32 m + j) ln2/32 + r, |r| <= ln2/64,
 // p = the degree-6 Taylor polynomial (error < 4e-18) in Estrin form (4 dependent steps); t2[j] = 2^(j/32)
-// from LDS.  Max |error| vs the IEEE tanh ~3e-16 (host-checked over [-25, 25]); about half the dependent
-// fp64 chain of tanh_d2.
+// from LDS.  Max |error| vs the IEEE tanh ~3e-16 (host-checked over [-25, 25]) with two Newton steps on the
+// reciprocal (~4e-15 with one); about half the dependent fp64 chain of tanh_d2.
 __device__ __forceinline__ double tanh_d3(double y, const double* t2) {
     const double x = 2.0 * fmin(fabs(y), 20.0);
     const double kf = __builtin_rint(x * 46.16624130844683);  // 32 / ln 2
@@ -126,7 +139,7 @@ __device__ __forceinline__ double tanh_d3(double y, const double* t2) {
     const double e = __builtin_ldexp(tj * p, k >> 5) + 1.0;
     double q = __builtin_amdgcn_rcp(e);
     q = fma(q, fma(-e, q, 1.0), q);
-    q = fma(q, fma(-e, q, 1.0), q);
+    if constexpr (PGM_FP64_NEWTON > 1) q = fma(q, fma(-e, q, 1.0), q);
     return copysign(fma(-2.0, q, 1.0), y);
 }
 

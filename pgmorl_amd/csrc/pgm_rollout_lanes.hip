@@ -202,7 +202,7 @@ struct ActorLane {
     // the same action mean from registers: lane k < O holds input feature k (other lanes: anything).  Every input
     // reaches every lane by a row copy + row_newbcast DPP operand of the FMA (no LDS round trip, no v_readlane);
     // four accumulator chains per layer.
-    __device__ void forward_reg(float xv, int l, float (&mu)[A]) const {
+    __device__ void forward_reg(float xv, int l, float (&mu)[A], float* h1row = nullptr) const {
         constexpr int R1 = (O + 15) / 16;
         float X[R1];
         row_copies<R1>(xv, X);
@@ -212,18 +212,45 @@ struct ActorLane {
             fmac_row_bcast<(O - 16 * j < 16 ? O - 16 * j : 16), 4>(z, X[j], &w1[16 * j]);
         });
         const float hl = tanh_fast((z[0] + z[1]) + (z[2] + z[3]));
-        float Hc[4];
-        row_copies<4>(hl, Hc);
-        constexpr int NA2 = PGM_EXP == 41 ? 8 : 4;  // layer-2 accumulator chains (A/B)
-        float y[NA2];
-        y[0] = b2;
+        float h2;
+        if constexpr (PGM_EXP == 44 || PGM_EXP == 45) {
+            // A/B: layer-2 inputs by an LDS row broadcast (44) or v_readlane (45) into packed FMAs
+            f2 a01 = f2{b2, 0.f}, a23 = f2{0.f, 0.f};
+            if constexpr (PGM_EXP == 44) {
+                h1row[l] = hl;
+                wave_lds_fence_r();
+            }
 #pragma unroll
-        for (int i = 1; i < NA2; ++i) y[i] = 0.f;
+            for (int k = 0; k < H; k += 4) {
+                float4 h;
+                if constexpr (PGM_EXP == 44) {
+                    h = *reinterpret_cast<const float4*>(h1row + k);
+                } else {
+                    const int hi = __float_as_int(hl);
+                    h = make_float4(__int_as_float(__builtin_amdgcn_readlane(hi, k)),
+                                    __int_as_float(__builtin_amdgcn_readlane(hi, k + 1)),
+                                    __int_as_float(__builtin_amdgcn_readlane(hi, k + 2)),
+                                    __int_as_float(__builtin_amdgcn_readlane(hi, k + 3)));
+                }
+                a01 = __builtin_elementwise_fma(f2{h.x, h.y}, f2{w2[k], w2[k + 1]}, a01);
+                a23 = __builtin_elementwise_fma(f2{h.z, h.w}, f2{w2[k + 2], w2[k + 3]}, a23);
+            }
+            if constexpr (PGM_EXP == 44) wave_lds_fence_r();
+            h2 = tanh_fast((a01.x + a01.y) + (a23.x + a23.y));
+        } else {
+            float Hc[4];
+            row_copies<4>(hl, Hc);
+            constexpr int NA2 = PGM_EXP == 41 ? 8 : 4;  // layer-2 accumulator chains (A/B)
+            float y[NA2];
+            y[0] = b2;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) fmac_row_bcast<16, NA2>(y, Hc[j], &w2[16 * j]);
+            for (int i = 1; i < NA2; ++i) y[i] = 0.f;
 #pragma unroll
-        for (int i = 4; i < NA2; ++i) y[i - 4] += y[i];
-        const float h2 = tanh_fast((y[0] + y[1]) + (y[2] + y[3]));
+            for (int j = 0; j < 4; ++j) fmac_row_bcast<16, NA2>(y, Hc[j], &w2[16 * j]);
+#pragma unroll
+            for (int i = 4; i < NA2; ++i) y[i - 4] += y[i];
+            h2 = tanh_fast((y[0] + y[1]) + (y[2] + y[3]));
+        }
         float pr[A];
 #pragma unroll
         for (int j = 0; j < A; ++j) pr[j] = h2 * wm[j];
@@ -551,7 +578,7 @@ __global__ __launch_bounds__(512) void rollout_lane_kernel(RolloutArgs a) {
 #pragma unroll
                 for (int j = 0; j < A; ++j) ej[j] = PREF ? ejc[j] : S.eps[(step / NCH) & 1][n][cs * A + j];
                 float mu[A];
-                if constexpr (PGM_ROLL_DPP) pol.forward_reg(xr[e], l, mu);
+                if constexpr (PGM_ROLL_DPP) pol.forward_reg(xr[e], l, mu, S.h1[w]);
                 else pol.forward(S.x[n], S.h1[w], l, mu);
                 PGM_STAMP(1);
                 // Gaussian draw (torch.normal(mean, std) = eps * std + mean), log-prob and clipped action, all
@@ -854,7 +881,7 @@ __global__ __launch_bounds__(64 * EVAL_MAX_WAVES) void eval_wave_kernel(EvalArgs
             if constexpr (PGM_ROLL_DPP) {
                 double v = s;  // (lanes >= O: ignored by the broadcast)
                 if (a.use_ob) v = clipd((v - mean) * inv, -10.0, 10.0);
-                pol.forward_reg((float)v, l, mu);
+                pol.forward_reg((float)v, l, mu, S.h1[w]);
             } else {
                 if (fl) {
                     double v = s;

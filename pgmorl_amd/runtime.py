@@ -106,8 +106,9 @@ class TaskBatch:
         z('bad_masks', T + 1, N, fill=1.0)
         z('stats', 3)
         z('objs', K, dt=F64)
-        z('_eval_mean', O, dt=F64)
-        z('_eval_var', O, dt=F64)
+        # the overlapped evaluation's copy of ob_rms: mean | var of every slot, one copy of the adjacent stats64
+        # segments ob_mean, ob_var (STAT_SEGMENTS order)
+        self._eval_ob = torch.zeros(2, Pc, O, dtype=F64, device=self.dev)
         self.perms = torch.zeros(ppo_epoch, T * N, dtype=I32, device=self.dev)
         self.noise = torch.zeros(T, N, A, dtype=F32, device=self.dev)
         self.hp = PPOHParams(clip_param=clip_param, value_loss_coef=value_loss_coef, entropy_coef=entropy_coef,
@@ -134,6 +135,9 @@ class TaskBatch:
         for name, off, w, vec in self._seg:
             v = self._stats64[off:off + self.capacity * w]
             setattr(self, name, (v.view(self.capacity, w) if vec else v)[:P])
+            if name == 'ob_mean':
+                self._ob_src = self._stats64[off:off + 2 * self.capacity * w].view(2, self.capacity, w)
+        self._eval_mean, self._eval_var = self._eval_ob[0, :P], self._eval_ob[1, :P]
         self._build_structs()
 
     @property
@@ -311,33 +315,40 @@ class TaskBatch:
         parameters); the next PPO update (which writes them) waits for it.  It normalises with a copy of
         this iteration's ob_rms (the next rollout advances the live one) and writes objs_out (default
         self.objs), readable after wait_eval() or from work queued on eval_stream."""
-        self.lr.fill_(float(lr))
         if noise is None:  # perf mode: the counter stream of iteration j, drawn by one wide kernel up front
             check(lib().pgm_normal_noise(self.noise.numel(), C.c_uint64(j), _ptr(self.noise), _stream()),
                   'pgm_normal_noise')
             noise = self.noise
         perm_ready = None
-        if perms is None and overlap_eval:  # the permutations only feed the update: drawn beside the rollout
+        if perms is None and overlap_eval:  # the permutations (and lr) only feed the update: set beside the rollout
             side = self.eval_stream  # (behind the previous evaluation, itself behind the previous update)
             side.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(side):
+                self.lr.fill_(float(lr))
                 self.make_perms(j)
                 perm_ready = torch.cuda.Event()
                 perm_ready.record(side)
+        else:
+            self.lr.fill_(float(lr))
         self.rollout(j, noise=noise, carry=carry)
         self.gae()
         self.adv_normalize()
-        if perms is None and perm_ready is None:
-            self.make_perms(j)
-        self.wait_eval()  # the previous overlapped evaluation still reads the parameters
         if perm_ready is not None:
+            # one wait: the side stream ran the previous evaluation (which still reads the parameters) first
             torch.cuda.current_stream().wait_event(perm_ready)
+        else:
+            if perms is None:
+                self.make_perms(j)
+            self.wait_eval()  # the previous overlapped evaluation still reads the parameters
         self.ppo_update(perms)
         if not overlap_eval:
             self.evaluate(out=objs_out)
             return
-        self._eval_mean.copy_(self.ob_mean)
-        self._eval_var.copy_(self.ob_var)
+        if self.P == self.capacity:
+            self._eval_ob.copy_(self._ob_src)  # ob_mean | ob_var in one copy
+        else:
+            self._eval_mean.copy_(self.ob_mean)
+            self._eval_var.copy_(self.ob_var)
         ready = torch.cuda.Event()
         ready.record()
         side = self.eval_stream

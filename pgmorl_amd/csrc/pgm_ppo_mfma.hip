@@ -1059,6 +1059,7 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
                     S.MV[IMG + i] = vv;
                     Pf[i] = pp;
                 }
+                PGM_STAMP(19);
                 // exp(-2 logstd) of the new actor logstd, by the compile-time owners of elements oLs .. oLs + A - 1
                 // (inside the element loop it put a branch + exp on every element of those groups)
                 if (m == 1) {

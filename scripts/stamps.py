@@ -34,7 +34,7 @@ mnames = {0: 'stage rows', 1: 'pass end sync', 2: 'grad image rounds', 3: 'Adam'
           10: 'half image publish + drain', 11: 'flag hand-off + image gather',
           4: 'tile: L1 + L2 fwd', 5: 'tile: heads + loss', 6: 'tile: gWh, dH2, gW2', 7: 'tile: dH1, gW1',
           12: 'image: lane sums', 13: 'image: stage 0 work', 14: 'image: stage 1 work', 15: 'image: stage 0 barrier',
-          16: 'tile: heads (VALU)', 17: 'tile: loss + dO tile', 18: 'tile: dO fence', 5: 'tile: head column sums'}
+          16: 'tile: heads (VALU)', 17: 'tile: loss + dO tile', 18: 'tile: dO fence', 5: 'tile: head column sums', 19: 'Adam math (MODE 2)'}
 lnames = {0: 'loop/top', 1: 'actor fwd', 6: 'sample', 7: 'dynamics', 2: 'accumulators + row', 3: 'barrier',
           4: 'stats', 5: 'emit'}
 wnames = {0: 'noise + layer-1 slices', 1: 'barrier A', 2: 'L1 sum, L2, head, draw', 3: 'barrier C',

@@ -4,8 +4,9 @@
  * Every entry point is batched over P tasks (policies), takes CALLER-OWNED device buffers
  * (plain pointers; no allocation inside), is ordered on the passed hipStream_t and returns
  * an int status (PGM_OK or a negative PGM_E_*).  pgm_last_error() returns a thread-local
- * message for the last failure.  No global mutable state besides that string: calls on
- * distinct streams are independent.  One host thread per device.
+ * message for the last failure.  No global mutable state besides that string and the
+ * pre-zeroed-workspace marks of pgm_ppo_update_reset: calls on distinct streams are independent.  One host
+ * thread per device.
  *
  * Reference seams replaced (albo437/PGMORL; paths relative to the reference tree):
  *   pgm_act_forward       Policy.act / get_value            a2c_ppo_acktr/model.py:57-73
@@ -22,6 +23,7 @@
  *                          + WeightedSumScalarization        morl/scalarization_methods.py:28-29
  *   pgm_ppo_update        PPO.update epochs x minibatches   a2c_ppo_acktr/algo/ppo.py:58-115
  *                          (+ feed_forward_generator storage.py:118-154, clip_grad_norm_, Adam)
+ *                          (pgm_ppo_update_reset: its workspace reset, issued ahead on another stream)
  *   pgm_eval              evaluation()                       morl/mopg.py:25-46
  *   pgm_randperm          SubsetRandomSampler's randperm     (perf-mode RNG replacement)
  *   pgm_normal_noise      Normal.sample's torch.normal draw  (perf-mode RNG replacement)
@@ -173,9 +175,9 @@ int pgm_adv_normalize(const pgm_dims* d, const pgm_rollout_buf* rb, const double
  * perms[e][b*mb:(b+1)*mb].  params/adam_m/adam_v [P][L] updated in place, adam_step [P] int32
  * incremented per step, lr [P].  stats [P][3] = mean (value_loss, action_loss, dist_entropy).
  * workspace: caller-owned device bytes (pgm_ppo_update_workspace_bytes), required (PGM_E_INVALID_ARG
- * when NULL), reset inside the call on `stream`.  The critic and actor towers of a task run on separate
- * CUs that exchange the squared gradient norm per minibatch step; each tower is further split over four
- * CUs (a quarter of the minibatch rows each, gradient images added through the workspace) while
+ * when NULL), reset inside the call on `stream` unless pgm_ppo_update_reset did it since the last call.
+ * The critic and actor towers of a task run on separate CUs that exchange the squared gradient norm per
+ * minibatch step; each tower is further split over four CUs (a quarter of the minibatch rows each, gradient images added through the workspace) while
  * 32 * ceil(P/4) <= CU count, else over two CUs while 16 * ceil(P/4) <= CU count.  obs_dim <= 32: tower
  * images LDS-resident (falls back to 2 CUs per task, then 1, as P grows); obs_dim > 32 (Humanoid): layer
  * 1 streamed from L2, needs 2P <= CU count (PGM_E_UNSUPPORTED otherwise: shard the tasks over more
@@ -186,6 +188,10 @@ int pgm_ppo_update(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params, 
                    float* adam_v, int32_t* adam_step, const float* lr, const int32_t* perms,
                    const pgm_rollout_buf* rb, float* stats, void* workspace, pgm_stream_t stream);
 size_t pgm_ppo_update_workspace_bytes(const pgm_dims* d);
+/* Zero, on `stream`, the part of the workspace the next pgm_ppo_update for dims d would reset inside the call,
+ * and let that call skip its own reset (the caller orders this stream before the update's stream and after
+ * every read of the previous update's timeout word).  Lets a caller take the reset off the update's stream. */
+int pgm_ppo_update_reset(const pgm_dims* d, void* workspace, pgm_stream_t stream);
 
 /* evaluation(): eval_num deterministic episodes per task from s0_eval [eval_num][O], obs normalised
  * with the snapshot ob_mean/ob_var [P][O] (use_ob_rms), objs_out [P][K] fp64 (discounted by gamma

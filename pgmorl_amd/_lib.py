@@ -69,6 +69,7 @@ _SIGS = {
     'pgm_ppo_update': (C.c_int, [C.POINTER(Dims), C.POINTER(PPOHParams), P_, P_, P_, P_, P_, P_,
                                  C.POINTER(RolloutBuf), P_, P_, P_]),
     'pgm_ppo_update_workspace_bytes': (C.c_size_t, [C.POINTER(Dims)]),
+    'pgm_ppo_update_reset': (C.c_int, [C.POINTER(Dims), P_, P_]),
     'pgm_eval': (C.c_int, [C.POINTER(Dims), P_, C.POINTER(EnvSpec), P_, P_, P_, I32, I32, I32, F64, P_, P_]),
     'pgm_randperm': (C.c_int, [I32, I32, C.c_uint64, P_, P_]),
     'pgm_normal_noise': (C.c_int, [C.c_int64, C.c_uint64, P_, P_]),

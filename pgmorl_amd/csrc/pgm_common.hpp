@@ -51,6 +51,13 @@ int wide_xslot_words(int O, int A, int K);  // pgm_ppo_wide.hip: small image + d
 inline size_t wide_xbuf_bytes(const pgm_dims* d) {
     return (size_t)d->P * 2 * PGM_NS_MAX * 2 * wide_xslot_words(d->O, d->A, d->K) * 8;
 }
+// the part of the workspace a launch expects zeroed: flags + exchange slots (every mode's, sized for PGM_NS_MAX)
+inline size_t ppo_reset_bytes(const pgm_dims* d) {
+    return ppo_flag_bytes(d->P) + (d->O > 32 ? wide_xbuf_bytes(d) : ppo_xbuf_bytes(d));
+}
+// pgm_ppo_update_reset marks a workspace as zeroed (up to n bytes, ordered by the caller's streams); a launch
+// needing <= n zeroed bytes consumes the mark instead of issuing its own reset (pgm_ppo_update.hip)
+bool ws_take_zeroed(const void* ws, size_t need);
 // obs_dim > 32 (wide kernel): flags, exchange slots [P][2 towers][NS parts][2 parities], parts 1..NS-1's
 // private [P][NS-1][L] parameter copies (sized for PGM_NS_MAX parts)
 inline size_t ppo_workspace_bytes(const pgm_dims* d) {

@@ -1969,8 +1969,11 @@ static int launch_t16_k(const pgm_dims* d, const MArgs& a, hipStream_t stream) {
     if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update");
     const int grid = 8 * NS * ((d->P + 3) / 4);
     if (int rc = check_coresident((const void*)kern, 64 * W, smem, grid, "pgm_ppo_update")) return rc;
-    e = hipMemsetAsync(a.ws, 0, ppo_flag_bytes(d->P) + ppo_xbuf_bytes(d, NS), stream);
-    if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update (workspace reset)");
+    const size_t zb = ppo_flag_bytes(d->P) + ppo_xbuf_bytes(d, NS);
+    if (!ws_take_zeroed(a.ws, zb)) {
+        e = hipMemsetAsync(a.ws, 0, zb, stream);
+        if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update (workspace reset)");
+    }
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * W), smem, stream, a);
     return launch_status("pgm_ppo_update");
 }
@@ -2001,8 +2004,11 @@ int launch_mode_k(const pgm_dims* d, const MArgs& a, hipStream_t stream) {
     if constexpr (SPLIT) {  // workgroups exchange through spin-waits: all of them must be resident together
         if (int rc = check_coresident((const void*)kern, MT, smem, grid, "pgm_ppo_update")) return rc;
     }
-    e = hipMemsetAsync(a.ws, 0, ppo_flag_bytes(d->P) + (MODE == 2 ? ppo_xbuf_bytes(d) : 0), stream);
-    if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update (workspace reset)");
+    const size_t zb = ppo_flag_bytes(d->P) + (MODE == 2 ? ppo_xbuf_bytes(d) : 0);
+    if (!ws_take_zeroed(a.ws, zb)) {
+        e = hipMemsetAsync(a.ws, 0, zb, stream);
+        if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update (workspace reset)");
+    }
     hipLaunchKernelGGL(kern, dim3(grid), dim3(MT), smem, stream, a);
     return launch_status("pgm_ppo_update");
 }

@@ -14,6 +14,9 @@
 // torch.min / torch.max / clamp backward (ties split the gradient in half) are reproduced exactly.
 #include <stdlib.h>
 
+#include <mutex>
+#include <unordered_map>
+
 #include "pgm_dispatch.hpp"
 
 PGM_STAMP_UNIT(update)
@@ -519,6 +522,33 @@ using namespace pgm;
 
 extern "C" size_t pgm_ppo_update_workspace_bytes(const pgm_dims* d) { return d ? ppo_workspace_bytes(d) : 0; }
 
+// workspaces zeroed ahead of their next launch by pgm_ppo_update_reset: pointer -> zeroed bytes
+static std::mutex g_zeroed_mu;
+static std::unordered_map<const void*, size_t> g_zeroed;
+
+bool pgm::ws_take_zeroed(const void* ws, size_t need) {
+    std::lock_guard<std::mutex> lk(g_zeroed_mu);
+    auto it = g_zeroed.find(ws);
+    if (it == g_zeroed.end()) return false;
+    const bool ok = it->second >= need;
+    g_zeroed.erase(it);  // consumed either way: the next launch reuses the workspace
+    return ok;
+}
+
+extern "C" int pgm_ppo_update_reset(const pgm_dims* d, void* workspace, pgm_stream_t stream) {
+    if (int rc = check_dims(d, "pgm_ppo_update_reset")) return rc;
+    if (!workspace) {
+        set_error("pgm_ppo_update_reset: null workspace");
+        return PGM_E_INVALID_ARG;
+    }
+    const size_t n = ppo_reset_bytes(d);
+    hipError_t e = hipMemsetAsync(workspace, 0, n, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update_reset");
+    std::lock_guard<std::mutex> lk(g_zeroed_mu);
+    g_zeroed[workspace] = n;
+    return PGM_OK;
+}
+
 extern "C" int pgm_ppo_update(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params, float* adam_m,
                               float* adam_v, int32_t* adam_step, const float* lr, const int32_t* perms,
                               const pgm_rollout_buf* rb, float* stats, void* workspace, pgm_stream_t stream) {
@@ -567,7 +597,8 @@ extern "C" int pgm_ppo_update(const pgm_dims* d, const pgm_ppo_hparams* hp, floa
             auto kern = ppo_update_kernel<O, A, K>;
             hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
             if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update");
-            if (workspace) {  // no exchange in this kernel: the timeout word (2P) reads 0 for this call
+            if (workspace && !ws_take_zeroed(workspace, ppo_flag_bytes(d->P))) {
+                // no exchange in this kernel: the timeout word (2P) reads 0 for this call
                 e = hipMemsetAsync(workspace, 0, ppo_flag_bytes(d->P), (hipStream_t)stream);
                 if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update (workspace reset)");
             }

@@ -906,8 +906,11 @@ int ppo_update_wide(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params,
     WArgs a{d->N, d->T, d->P, L, *hp, params, adam_m, adam_v, copies, adam_step, lr, perms,
             rb->obs, rb->actions, rb->logp, rb->adv, rb->values, rb->returns, stats, (unsigned long long*)ws,
             (unsigned long long*)(ws + flags), xslot, (int)xbytes};
-    hipError_t e = hipMemsetAsync(workspace, 0, flags + (ns > 1 ? xbytes : 0), stream);
-    if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update (workspace reset)");
+    hipError_t e = hipSuccess;
+    if (!ws_take_zeroed(workspace, flags + (ns > 1 ? xbytes : 0))) {
+        e = hipMemsetAsync(workspace, 0, flags + (ns > 1 ? xbytes : 0), stream);
+        if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update (workspace reset)");
+    }
     const size_t row = (size_t)L.total * sizeof(float);
     for (int hh = 1; hh < ns; ++hh) {  // parts 1..ns-1: private copies of every task's parameters
         e = hipMemcpy2DAsync(copies + (size_t)(hh - 1) * L.total, (size_t)(ns - 1) * row, params, row, row, d->P,

@@ -116,6 +116,7 @@ class TaskBatch:
                              ppo_epoch=ppo_epoch, num_mini_batch=num_mini_batch,
                              use_clipped_value_loss=int(use_clipped_value_loss))
         self._eval_stream, self._eval_done = None, None
+        self._reset_pending = False  # a pgm_ppo_update_reset queued on the side stream, not yet waited for
         nws = lib().pgm_ppo_update_workspace_bytes(C.byref(Dims(Pc, N, T, O, A, K, self.H)))
         self.update_ws = torch.zeros((nws + 7) // 8, dtype=torch.int64, device=self.dev)
         # sticky OR of every update's exchange-timeout word (workspace word 2P, include/pgm_abi.h): a launch
@@ -254,10 +255,19 @@ class TaskBatch:
         E, n = self.perms.shape
         check(lib().pgm_randperm(n, E, C.c_uint64(seed), _ptr(self.perms), _stream()), 'pgm_randperm')
 
-    def ppo_update(self, perms=None):
+    def ppo_update(self, perms=None, defer_flag=False):
+        """The update on the current stream.  The exchange-timeout word of this launch is OR-ed into the sticky
+        ``update_failed`` flag on the current stream, or (defer_flag) left to ``fold_update_flag`` on a stream that
+        runs before the next update's launch (which resets the word)."""
+        if self._reset_pending:  # the workspace reset queued on the side stream must land first
+            self.wait_eval()
         if perms is not None:
             self.perms.copy_(torch.as_tensor(np.asarray(perms), dtype=I32))
         self.ppo_update_launch()
+        if not defer_flag:
+            self.fold_update_flag()
+
+    def fold_update_flag(self):
         flag = self.update_ws[2 * self.P:2 * self.P + 1]
         torch.bitwise_or(self.update_failed, flag, out=self.update_failed)  # stream-ordered, no host sync
 
@@ -270,7 +280,9 @@ class TaskBatch:
 
     def take_update_failed(self):
         """True if any PPO update since the last call timed out in a cross-workgroup exchange (its parameters /
-        Adam state are invalid); resets the sticky flag.  Synchronises with the stream."""
+        Adam state are invalid); resets the sticky flag.  Synchronises with the stream (after the overlapped
+        evaluation, whose stream folds the last update's flag)."""
+        self.wait_eval()
         failed = int(self.update_failed.item()) != 0
         if failed:
             self.update_failed.zero_()
@@ -303,6 +315,7 @@ class TaskBatch:
         """Order the current stream after the last overlapped evaluation (its objs are then readable)."""
         if self._eval_done is not None:
             torch.cuda.current_stream().wait_event(self._eval_done)
+        self._reset_pending = False
 
     def iteration(self, j, lr, noise=None, perms=None, carry=True, overlap_eval=False, objs_out=None):
         """One MOPG iteration for every task: rollout, returns, advantages, PPO update, evaluation.
@@ -334,13 +347,15 @@ class TaskBatch:
         self.gae()
         self.adv_normalize()
         if perm_ready is not None:
-            # one wait: the side stream ran the previous evaluation (which still reads the parameters) first
+            # one wait: the side stream ran the previous evaluation (which still reads the parameters) and the
+            # workspace reset first
             torch.cuda.current_stream().wait_event(perm_ready)
+            self._reset_pending = False
         else:
             if perms is None:
                 self.make_perms(j)
             self.wait_eval()  # the previous overlapped evaluation still reads the parameters
-        self.ppo_update(perms)
+        self.ppo_update(perms, defer_flag=overlap_eval)
         if not overlap_eval:
             self.evaluate(out=objs_out)
             return
@@ -354,6 +369,12 @@ class TaskBatch:
         side = self.eval_stream
         side.wait_event(ready)
         with torch.cuda.stream(side):
+            # the timeout word of this update, folded off the main stream, then the next update's workspace reset
+            # (the next update waits for this stream: perm_ready)
+            self.fold_update_flag()
+            check(lib().pgm_ppo_update_reset(C.byref(self.dims), _ptr(self.update_ws), _stream()),
+                  'pgm_ppo_update_reset')
+            self._reset_pending = True
             out = self.evaluate(self._eval_mean, self._eval_var, out=objs_out)
             out.record_stream(side)
             self._eval_done = torch.cuda.Event()

@@ -26,6 +26,7 @@
 //   evaluation()                           morl/mopg.py:25-46
 #include "pgm_dispatch.hpp"
 #include "pgm_rollout.hpp"
+#include "pgm_mfma.hpp"
 #include <utility>
 
 PGM_STAMP_UNIT(lanes)
@@ -843,6 +844,120 @@ __global__ __launch_bounds__(256) void value_kernel(ValueArgs a) {
     for (int q = 0; q < K; ++q) a.values[((size_t)p * a.R + r) * K + q] = v[q];
 }
 
+// The same values on the f32 matrix cores (O <= 32), persistent: grid (CUs / P, P), each workgroup stages its
+// task's critic tower in LDS ONCE and its 4 waves loop over 32-row tiles (samples on the MFMA accumulator rows, as
+// in the update kernel's forward), the next tile's observation rows prefetched into registers during the current
+// one.  Layer 1 from a per-wave LDS copy of the tile's rows, layer 2 through a [32][65] transpose tile, the K value
+// outputs on the VALU (lane = sample, half h = units 32h..32h+31).  fp32 and tanh_fast as value_kernel, a different
+// summation order.  PGM_EXP 46 (A/B): value_kernel.
+template <int O, int K>
+struct CriticMSmem {
+    static constexpr int XS = O | 1;  // odd row stride: the tile's column reads are conflict-free
+    float W1t[O][H];
+    float W2t[H][H];
+    float Wv[K][H];
+    float b1[H], b2[H], bv[K];
+    float x[4][32 * XS];
+    float scr[4][32 * SCR];
+};
+
+template <int O, int K>
+__global__ __launch_bounds__(256) void value_mfma_kernel(ValueArgs a) {
+    static_assert(O <= 32, "one 32-input block");
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    using Sm = CriticMSmem<O, K>;
+    constexpr int XS = Sm::XS, KS1 = (O + 1) / 2, XL = (32 * O + 63) / 64;  // floats per lane of a tile's rows
+    auto& S = *reinterpret_cast<Sm*>(smem_raw);
+    const int p = blockIdx.y, t = threadIdx.x, w = t >> 6, l = t & 63, h = l >> 5, c = l & 31;
+    const Layout& L = a.L;
+    const float* prm = a.params + (size_t)p * L.total;
+    for (int i = t; i < O * H; i += 256) (&S.W1t[0][0])[i] = prm[L.off[PGM_P_CRITIC_W1] + i];
+    for (int i = t; i < H * H; i += 256) (&S.W2t[0][0])[i] = prm[L.off[PGM_P_CRITIC_W2] + i];
+    for (int i = t; i < K * H; i += 256) S.Wv[i / H][i % H] = prm[L.off[PGM_P_VALUE_W] + (i % H) * K + i / H];
+    if (t < H) {
+        S.b1[t] = prm[L.off[PGM_P_CRITIC_B1] + t];
+        S.b2[t] = prm[L.off[PGM_P_CRITIC_B2] + t];
+    }
+    if (t < K) S.bv[t] = prm[L.off[PGM_P_VALUE_B] + t];
+    const int ntile = (a.R + 31) / 32, stride = gridDim.x * 4;
+    const float* xg = a.obs + (size_t)p * a.R * O;
+    float xr[XL];  // this lane's share of a tile's rows (contiguous in HBM), rows past R as zeros
+    auto load_tile = [&](int tile) {
+        const int nv = tile < ntile ? min(32, a.R - tile * 32) * O : 0;
+#pragma unroll
+        for (int j = 0; j < XL; ++j) {
+            const int i = l + 64 * j;
+            xr[j] = i < nv ? xg[(size_t)tile * 32 * O + i] : 0.f;
+        }
+    };
+    int tile = blockIdx.x * 4 + w;
+    load_tile(tile);
+    __syncthreads();
+    float* xs = S.x[w];
+    float* scr = S.scr[w];
+    for (; tile < ntile; tile += stride) {
+#pragma unroll
+        for (int j = 0; j < XL; ++j) {
+            const int i = l + 64 * j;
+            if (i < 32 * O) xs[(i / O) * XS + (i % O)] = xr[j];
+        }
+        wave_lds_fence();
+        load_tile(tile + stride);  // next tile's rows in flight during this one
+        f32x16 z[2] = {f32x16{0}, f32x16{0}};
+#pragma unroll
+        for (int ks = 0; ks < KS1; ++ks) {
+            const int k = 2 * ks + h;
+            const float av = k < O ? xs[c * XS + k] : 0.f;
+#pragma unroll
+            for (int hb = 0; hb < 2; ++hb) z[hb] = mfma(av, k < O ? S.W1t[k < O ? k : 0][hb * TS + c] : 0.f, z[hb]);
+        }
+#pragma unroll
+        for (int hb = 0; hb < 2; ++hb) {
+            const float bias = S.b1[hb * TS + c];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) scr[rowof(r, h) * SCR + hb * TS + c] = tanh_fast(z[hb][r] + bias);
+        }
+        wave_lds_fence();
+        z[0] = z[1] = f32x16{0};
+#pragma unroll 16
+        for (int ks = 0; ks < H / 2; ++ks) {
+            const int k = 2 * ks + h;
+            const float av = scr[c * SCR + k];
+#pragma unroll
+            for (int ob = 0; ob < 2; ++ob) z[ob] = mfma(av, S.W2t[k][ob * TS + c], z[ob]);
+        }
+        f32x16 h2[2];
+#pragma unroll
+        for (int ob = 0; ob < 2; ++ob) {
+            const float bias = S.b2[ob * TS + c];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) h2[ob][r] = tanh_fast(z[ob][r] + bias);
+        }
+        wave_lds_fence();  // every lane finished reading the H1 tile
+#pragma unroll
+        for (int ob = 0; ob < 2; ++ob)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) scr[rowof(r, h) * SCR + ob * TS + c] = h2[ob][r];
+        wave_lds_fence();
+        float v[K];
+#pragma unroll
+        for (int q = 0; q < K; ++q) v[q] = 0.f;
+#pragma unroll 8
+        for (int u = 0; u < TS; ++u) {
+            const float hv = scr[c * SCR + h * TS + u];
+#pragma unroll
+            for (int q = 0; q < K; ++q) v[q] = fmaf(hv, S.Wv[q][h * TS + u], v[q]);
+        }
+        const int r = tile * 32 + c;
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+            const float vq = half_sum(v[q]) + S.bv[q];
+            if (h == 0 && r < a.R) a.values[((size_t)p * a.R + r) * K + q] = vq;
+        }
+        wave_lds_fence();  // the head's tile reads done before the next tile's x / scr writes
+    }
+}
+
 // ------------------------------------------------------------------------------------------ evaluation
 template <int O>
 struct EvalSmem {
@@ -950,6 +1065,14 @@ int launch_critic_values(const pgm_dims* d, const RolloutArgs& a, hipStream_t s)
         constexpr int O = decltype(o)::value, K = decltype(k)::value;
         const int R = (d->T + 1) * d->N;
         ValueArgs va{R, a.L, a.params, a.rb.obs, a.rb.values};
+        if constexpr (O <= 32 && PGM_EXP != 46) {
+            // persistent workgroups: VM_PER_CU per CU over the tasks (>= 1 per task), at most one per 4 tiles.
+            // PGM_EXP 47 (A/B): two per CU (two waves per SIMD)
+            constexpr int VM_PER_CU = PGM_EXP == 47 ? 2 : 1;
+            const int wg = max(1, min(VM_PER_CU * device_cu_count() / d->P, (R + 127) / 128));
+            return launch_k(value_mfma_kernel<O, K>, dim3(wg, d->P), dim3(256), sizeof(CriticMSmem<O, K>), s, va,
+                            "pgm_rollout (critic values)");
+        }
         return launch_k(value_kernel<O, K>, dim3((R + 255) / 256, d->P), dim3(256), sizeof(CriticSmem<O, K>), s, va,
                         "pgm_rollout (critic values)");
     });

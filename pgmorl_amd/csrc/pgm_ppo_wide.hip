@@ -39,6 +39,10 @@ PGM_STAMP_UNIT(wupd)
 #define PGM_UNROLL_W(n) PGM_PRAGMA_W(unroll n)
 #define PGM_UW_L2 (PGM_EXP == 7 || PGM_EXP == 9 ? 32 : 8)
 #define PGM_UW_HEAD (PGM_EXP == 8 || PGM_EXP == 9 ? 32 : 4)
+// block map: the two towers of a row part on one XCD (they read the same observation rows in the same phase, so the
+// second read hits that XCD's L2): Humanoid P = 20 update 31.1 -> 30.4 ms, 56.2 -> 47.8 GB per launch
+// (profiles/r03o_*).  PGM_EXP 50 (A/B): the round-2 map (the NS parts of one tower on one XCD)
+#define PGM_WIDE_COLOC (PGM_EXP != 50)
 
 namespace pgm {
 
@@ -152,15 +156,25 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
     constexpr int NKW = (NKT + 3) / 4;      // tiles owned per wave: kt = w + 4j
     constexpr int oWh = H * SCR, oB1 = oWh + Q * H, oB2 = oB1 + H, oBh = oB2 + H, oLs = oBh + Q;
     const int t = threadIdx.x, w = t >> 6, l = t & 63, h = l >> 5, c = l & 31;
-    // block map (NS > 1): in each group of 8 NS blocks, block r holds part r >> 3 of tower r & 1 of task
-    // 4g + ((r & 7) >> 1): the parts of a tower are blocks b, b + 8, ... (one XCD under round-robin
-    // dispatch: speed only)
+    // block map (NS > 1), groups of 8 NS blocks for 4 tasks; blocks b, b + 8, ... share an XCD under round-robin
+    // dispatch (speed only: every hand-off is correct under any placement)
     const int bx = (int)blockIdx.x;
     const int r8 = bx % (8 * NS);
+#if PGM_WIDE_COLOC
+    // co-located map (NS > 1): XCD slot x = r8 & 7 holds task 4g + (x >> 1) and BOTH towers of its parts
+    // (NS = 4: parts 2 (x & 1), 2 (x & 1) + 1; NS = 2: part x & 1), so the critic and actor workgroups of a row part --
+    // which read the same observation rows in the same phase, kept in step by the per-step norm hand-off -- share one L2
+    const int x8 = r8 & 7, j8 = r8 >> 3;
+    const int p = NS > 1 ? 4 * (bx / (8 * NS)) + (x8 >> 1) : (bx >> 1);
+    const int hs = NS == 4 ? 2 * (x8 & 1) + (j8 >> 1) : NS == 2 ? (x8 & 1) : 0;
+    if (p >= a.P) return;
+    const int m = NS > 1 ? (j8 & 1) : (bx & 1);
+#else  // block r holds part r >> 3 of tower r & 1 of task 4g + ((r & 7) >> 1): a tower's parts on one XCD
     const int p = NS > 1 ? 4 * (bx / (8 * NS)) + ((r8 & 7) >> 1) : (bx >> 1);
     const int hs = NS > 1 ? r8 >> 3 : 0;
     if (p >= a.P) return;
     const int m = bx & 1;
+#endif
     const int NQ = m == 0 ? K : A;
     const int N = a.N, T = a.T, B = T * N;
     const int E = a.hp.ppo_epoch, M = a.hp.num_mini_batch;

@@ -66,19 +66,19 @@ def parse():
 
 def update_kernel_name(obs_dim, P):
     """The pgm_ppo_update variant the launcher selects (pgm_ppo_mfma.hip launch_ppo_update_mfma and
-    pgm_ppo_wide.hip): 16-row tiles on 8 CUs per task while 32 ceil(P/4) <= CUs, else MODE 2 (4 CUs per task)
-    while 16 ceil(P/4) <= CUs; PGM_UPDATE_SPLIT caps it."""
+    pgm_ppo_wide.hip): 16-row tiles on 8 CUs per task while their grid (64 blocks per group of 8 tasks) fits the
+    CUs, else MODE 2 (4 CUs per task, 32 blocks per group of 8 tasks); PGM_UPDATE_SPLIT caps it."""
     if obs_dim > 32:
         return 'ppo_update_wide_kernel'
     cus = torch.cuda.get_device_properties(0).multi_processor_count
     cap = os.environ.get('PGM_UPDATE_SPLIT', '4')[:1]
     cap = int(cap) if cap.isdigit() and int(cap) <= 4 else 4
-    groups = (P + 3) // 4
-    if cap >= 4 and 32 * groups <= cus:
+    groups8 = (P + 7) // 8  # mode2_grid / t16_grid in pgm_ppo_mfma.hip
+    if cap >= 4 and 64 * groups8 <= cus:
         return 'ppo_update_t16_kernel (NS=4, W=4)'
-    if cap == 3 and 16 * groups <= cus:
+    if cap == 3 and 32 * groups8 <= cus:
         return 'ppo_update_t16_kernel (NS=2, W=8)'
-    mode = 2 if cap >= 2 and 16 * groups <= cus else 1 if cap >= 1 and 2 * P <= cus else 0
+    mode = 2 if cap >= 2 and 32 * groups8 <= cus else 1 if cap >= 1 and 2 * P <= cus else 0
     return f'ppo_update_mfma_kernel (MODE {mode})'
 
 

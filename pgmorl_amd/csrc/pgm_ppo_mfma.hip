@@ -56,6 +56,17 @@ PGM_STAMP_UNIT(mfma)
 // and reduction tree, so the totals stay bitwise equal in the four workgroups and the separate norm-granule hand-off
 // (one more cross-CU round trip per Adam step) disappears.  PGM_EXP 24 (A/B): the granule hand-off.
 #define PGM_FUSED_NORM (PGM_EXP != 24)
+// block maps of the split launches: every workgroup of a task on ONE XCD (groups of 8 tasks; blocks b, b + 8, ... share
+// an XCD under round-robin dispatch), so the per-step image hand-offs stay inside one L2: MODE 2 Walker P = 40 5.90 ->
+// 5.85-5.89 ms, t16 HalfCheetah P = 20 4.95 -> 4.88-4.90 ms, Walker P = 5 4.90 -> 4.85-4.87 ms (profiles/r03p_*).
+// PGM_EXP 48 / 49 (A/B): the round-2 maps (groups of 4 tasks, a tower's parts on one XCD, the towers on two)
+#define PGM_MODE2_XCD4 (PGM_EXP != 48)
+#define PGM_T16_XCD8 (PGM_EXP != 49)
+namespace pgm {
+// grids of the split launches (padding blocks of a partial group of tasks exit at once)
+inline int mode2_grid(int P) { return PGM_MODE2_XCD4 ? 32 * ((P + 7) / 8) : 16 * ((P + 3) / 4); }
+inline int t16_grid(int P, int NS) { return PGM_T16_XCD8 ? 16 * NS * ((P + 7) / 8) : 8 * NS * ((P + 3) / 4); }
+}  // namespace pgm
 
 namespace pgm {
 
@@ -230,14 +241,21 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
     constexpr int oW2 = O * H, oWh = oW2 + H * SCR, oB1 = oWh + Q * H, oB2 = oB1 + H, oBh = oB2 + H, oLs = oBh + Q;
     constexpr int NWT = SPLIT ? 4 : 2;  // waves per tower
     const int t = threadIdx.x, w = t >> 6, l = t & 63, h = l >> 5, c = l & 31;
-    // MODE 2 block map: in each group of 16 blocks, block r holds half r >> 3 of tower (r & 7) & 1 of task
-    // 4g + ((r & 7) >> 1): the two halves of a tower are blocks b and b + 8 (one XCD under round-robin
-    // placement -- speed only, the hand-off is correct anywhere)
+    // MODE 2 block map (speed only: the hand-off is correct under any placement; blocks b, b + 8, ... share an XCD
+    // under round-robin dispatch)
     const int bx = (int)blockIdx.x;
+#if PGM_MODE2_XCD4
+    // groups of 32 blocks for 8 tasks: block r holds half (r >> 4) & 1 of tower (r >> 3) & 1 of task 8g + (r & 7)
+    const int p = MODE == 2 ? 8 * (bx >> 5) + (bx & 7) : SPLIT ? (bx >> 1) : bx;
+    const int hs = MODE == 2 ? (bx >> 4) & 1 : 0;
+    if (p >= a.P) return;
+    const int m = MODE == 2 ? (bx >> 3) & 1 : SPLIT ? (bx & 1) : (w & 1);
+#else  // groups of 16 blocks for 4 tasks: block r holds half r >> 3 of tower r & 1 of task 4g + ((r & 7) >> 1)
     const int p = MODE == 2 ? 4 * (bx >> 4) + ((bx & 7) >> 1) : SPLIT ? (bx >> 1) : bx;
     const int hs = MODE == 2 ? (bx >> 3) & 1 : 0;  // half of the minibatch rows
     if (p >= a.P) return;
     const int m = MODE == 2 ? (bx & 1) : SPLIT ? (bx & 1) : (w & 1);  // tower of this wave
+#endif
     const int sh = SPLIT ? w : (w >> 1);                      // wave index within the tower
     const int NQ = m == 0 ? K : A;
     const int N = a.N, T = a.T, B = T * N;
@@ -1234,12 +1252,19 @@ __global__ __launch_bounds__(64 * W) void ppo_update_t16_kernel(MArgs a) {
     constexpr int oW2 = O * H, oWh = oW2 + H * SCR, oB1 = oWh + Q * H, oB2 = oB1 + H, oBh = oB2 + H, oLs = oBh + Q;
     const int t = threadIdx.x, l = t & 63, g = l >> 4, c = l & 15;
     const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-    // block map: in each group of 8 NS blocks, block r holds row part r >> 3 of tower r & 1 of task
-    // 4 G + ((r & 7) >> 1): the NS parts of a tower are blocks b, b + 8, b + 16, ... (one XCD under round-robin
-    // placement -- speed only, the hand-off is correct anywhere)
-    const int bx = (int)blockIdx.x, r8 = bx % (8 * NS);
+    // block map (speed only: the hand-offs are correct under any placement; blocks b, b + 8, ... share an XCD under
+    // round-robin dispatch)
+    const int bx = (int)blockIdx.x;
+#if PGM_T16_XCD8
+    // groups of 16 NS blocks for 8 tasks: block r holds part (r >> 4) % NS of tower (r >> 3) & 1 of task 8 G + (r & 7)
+    const int j16 = (bx >> 3) % (2 * NS);
+    const int p = 8 * (bx / (16 * NS)) + (bx & 7);
+    const int hs = j16 >> 1, m = j16 & 1;
+#else  // groups of 8 NS blocks for 4 tasks: block r holds part r >> 3 of tower r & 1 of task 4 G + ((r & 7) >> 1)
+    const int r8 = bx % (8 * NS);
     const int p = 4 * (bx / (8 * NS)) + ((r8 & 7) >> 1);
     const int hs = r8 >> 3, m = r8 & 1;
+#endif
     if (p >= a.P) return;
     const int NQ = m == 0 ? K : A;
     const int N = a.N, T = a.T, B = T * N;
@@ -1967,7 +1992,7 @@ static int launch_t16_k(const pgm_dims* d, const MArgs& a, hipStream_t stream) {
     auto kern = ppo_update_t16_kernel<O, A, K, NS, W, ONE>;
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update");
-    const int grid = 8 * NS * ((d->P + 3) / 4);
+    const int grid = t16_grid(d->P, NS);
     if (int rc = check_coresident((const void*)kern, 64 * W, smem, grid, "pgm_ppo_update")) return rc;
     const size_t zb = ppo_flag_bytes(d->P) + ppo_xbuf_bytes(d, NS);
     if (!ws_take_zeroed(a.ws, zb)) {
@@ -2000,7 +2025,7 @@ int launch_mode_k(const pgm_dims* d, const MArgs& a, hipStream_t stream) {
     if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update");
     // norm granules, timeout flag (and MODE 2: the exchange slots) start at tag 0; MODE 0 resets the flag
     // word too, so word 2P always reports THIS call
-    const int grid = MODE == 2 ? 16 * ((d->P + 3) / 4) : SPLIT ? 2 * d->P : d->P;
+    const int grid = MODE == 2 ? mode2_grid(d->P) : SPLIT ? 2 * d->P : d->P;
     if constexpr (SPLIT) {  // workgroups exchange through spin-waits: all of them must be resident together
         if (int rc = check_coresident((const void*)kern, MT, smem, grid, "pgm_ppo_update")) return rc;
     }
@@ -2045,10 +2070,9 @@ int launch_ppo_update_mfma(const pgm_dims* d, const MArgs& a, const pgm_rollout_
     const char* sel = getenv("PGM_UPDATE_SPLIT");
     const int cap = sel && sel[0] >= '0' && sel[0] <= '4' ? sel[0] - '0' : 4;
     const int cus = device_cus();
-    const int groups = (d->P + 3) / 4;
-    if (cap >= 4 && 32 * groups <= cus) return launch_t16<O, A, K, 4, 4>(d, a, stream);
-    if (cap == 3 && 16 * groups <= cus) return launch_t16<O, A, K, 2, 8>(d, a, stream);
-    if (cap >= 2 && 16 * groups <= cus) return launch_mode<O, A, K, 2>(d, a, stream);
+    if (cap >= 4 && t16_grid(d->P, 4) <= cus) return launch_t16<O, A, K, 4, 4>(d, a, stream);
+    if (cap == 3 && t16_grid(d->P, 2) <= cus) return launch_t16<O, A, K, 2, 8>(d, a, stream);
+    if (cap >= 2 && mode2_grid(d->P) <= cus) return launch_mode<O, A, K, 2>(d, a, stream);
     if (cap >= 1 && 2 * d->P <= cus) return launch_mode<O, A, K, 1>(d, a, stream);
     return launch_mode<O, A, K, 0>(d, a, stream);
 }

@@ -43,6 +43,10 @@ PGM_STAMP_UNIT(wupd)
 // second read hits that XCD's L2): Humanoid P = 20 update 31.1 -> 30.4 ms, 56.2 -> 47.8 GB per launch
 // (profiles/r03o_*).  PGM_EXP 50 (A/B): the round-2 map (the NS parts of one tower on one XCD)
 #define PGM_WIDE_COLOC (PGM_EXP != 50)
+// (all 2 NS workgroups of a task on one XCD, groups of 8 tasks: 30.4 -> 30.6-30.7 ms, kept out)
+namespace pgm {
+inline int wide_grid(int P, int NS) { return NS == 1 ? 2 * P : 8 * NS * ((P + 3) / 4); }
+}  // namespace pgm
 
 namespace pgm {
 
@@ -904,8 +908,7 @@ int ppo_update_wide(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params,
     const char* sel = getenv("PGM_UPDATE_SPLIT");
     const int cap = sel && sel[0] >= '0' && sel[0] <= '4' ? sel[0] - '0' : 4;
     const int cus = device_cu_count();
-    const int groups = (d->P + 3) / 4;
-    const int ns = cap >= 4 && 32 * groups <= cus ? 4 : cap >= 2 && 16 * groups <= cus ? 2 : 1;
+    const int ns = cap >= 4 && wide_grid(d->P, 4) <= cus ? 4 : cap >= 2 && wide_grid(d->P, 2) <= cus ? 2 : 1;
     if (ns == 1 && 2 * d->P > cus) {
         set_error("pgm_ppo_update: the wide update needs 2P <= CUs (P=%d); shard the tasks over more GPUs", d->P);
         return PGM_E_UNSUPPORTED;
@@ -952,9 +955,9 @@ int ppo_update_wide(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params,
                 return launch_status("pgm_ppo_update");
             };
             const int mb = d->T * d->N / hp->num_mini_batch;
-            if (ns == 4 && mb == 4 * 4 * TS) return launch(ppo_update_wide_kernel<O, A, K, 4, true>, 32 * groups);
-            if (ns == 4) return launch(ppo_update_wide_kernel<O, A, K, 4, false>, 32 * groups);
-            if (ns == 2) return launch(ppo_update_wide_kernel<O, A, K, 2, false>, 16 * groups);
+            if (ns == 4 && mb == 4 * 4 * TS) return launch(ppo_update_wide_kernel<O, A, K, 4, true>, wide_grid(d->P, 4));
+            if (ns == 4) return launch(ppo_update_wide_kernel<O, A, K, 4, false>, wide_grid(d->P, 4));
+            if (ns == 2) return launch(ppo_update_wide_kernel<O, A, K, 2, false>, wide_grid(d->P, 2));
             return launch(ppo_update_wide_kernel<O, A, K, 1, false>, 2 * d->P);
         }
     });

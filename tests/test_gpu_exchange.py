@@ -79,10 +79,11 @@ def test_coresidency_check_refuses_an_oversized_grid(gpu, monkeypatch):
     """The launcher refuses (PGM_E_UNSUPPORTED -> PGMError) a grid whose workgroups cannot all be resident:
     PGM_TEST_RESIDENT_CUS pretends the device has fewer CUs than the grid's workgroups (one per CU)."""
     monkeypatch.setenv('PGM_UPDATE_SPLIT', '2')
-    monkeypatch.setenv('PGM_TEST_RESIDENT_CUS', '8')  # MODE 2 for 2 tasks = 16 workgroups
+    # MODE 2 grid for 2 tasks: one group of 8 tasks' blocks (32 workgroups, 8 of them live; padding exits at once)
+    monkeypatch.setenv('PGM_TEST_RESIDENT_CUS', '16')
     args, spec, tb, pols, data, perms = _update_setup('MO-Walker2d-v2', 2, 64, 4, 1, 1, seed=3)
     with pytest.raises(PGMError, match='co-resident'):
         tb.ppo_update(torch.stack(perms).numpy())
-    monkeypatch.setenv('PGM_TEST_RESIDENT_CUS', '16')  # exactly fits: runs
+    monkeypatch.setenv('PGM_TEST_RESIDENT_CUS', '32')  # exactly fits: runs
     tb.ppo_update(torch.stack(perms).numpy())
     tb.check_update()

@@ -13,11 +13,11 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
 
 out = sys.argv[1] if len(sys.argv) > 1 else 'gpurun_out/prof_whole.txt'
-args = argparse.Namespace(whole_run_steps=5e6)
-bench.whole_run(args, 1.0)  # warm: library load, allocator, first compilation of nothing (all AOT)
+args = argparse.Namespace(whole_run_steps=5e6, tasks=40, num_processes=4, num_steps=2048)
+bench.whole_run(args, 40e6)  # warm: library load, allocator, first compilation of nothing (all AOT)
 pr = cProfile.Profile()
 pr.enable()
-res = bench.whole_run(args, 1.0)
+res = bench.whole_run(args, 40e6)  # (iter_value only scales the reported ratio)
 pr.disable()
 s = io.StringIO()
 st = pstats.Stats(pr, stream=s)

@@ -70,6 +70,37 @@ inline int t16_grid(int P, int NS) { return PGM_T16_XCD8 ? 16 * NS * ((P + 7) / 
 
 namespace pgm {
 
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// PGM_EXP 29 (A/B): the tiles' elementwise tanh(z + b) and tanh' products on register PAIRS through the packed fp32
+// ALU (v_pk_add / v_pk_mul / v_pk_fma_f32; per element the same operations and roundings as tanh_fast)
+#define PGM_PK_ELEM (PGM_EXP == 29)
+template <int N, typename V>
+__device__ __forceinline__ void tanh_bias_pk(const V& z, float bias, V& out) {
+#pragma unroll
+    for (int r = 0; r < N; r += 2) {
+        const f2v x = f2v{z[r], z[r + 1]} + f2v{bias, bias};
+        const f2v y = x * f2v{2.8853900817779268f, 2.8853900817779268f};
+        const f2v e = f2v{__builtin_amdgcn_exp2f(y.x), __builtin_amdgcn_exp2f(y.y)};
+        const f2v d = e + f2v{1.f, 1.f};
+        const f2v rc = f2v{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+        const f2v o = __builtin_elementwise_fma(f2v{-2.f, -2.f}, rc, f2v{1.f, 1.f});
+        out[r] = o.x;
+        out[r + 1] = o.y;
+    }
+}
+// out = z * (1 - a * a) (tanh' chain rule), pairs
+template <int N, typename V>
+__device__ __forceinline__ void dtanh_pk(const V& z, const V& a, V& out) {
+#pragma unroll
+    for (int r = 0; r < N; r += 2) {
+        const f2v av = f2v{a[r], a[r + 1]};
+        const f2v o = f2v{z[r], z[r + 1]} * __builtin_elementwise_fma(-av, av, f2v{1.f, 1.f});
+        out[r] = o.x;
+        out[r + 1] = o.y;
+    }
+}
+
 // The image reductions add exactly ONE partial onto a stored one per element per round (store and add ordered by a
 // barrier): a read + add + write in the wave.  PGM_EXP 23 (A/B only): ds_add_f32 instead (the same two-operand sum,
 // the read-modify-write in the LDS) -- measured ~20x slower on gfx950 (MODE 2 stage 1: 2.1 K -> 40.5 K cycles per
@@ -403,11 +434,17 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
 #pragma unroll
                     for (int hb = 0; hb < 2; ++hb) {
                         const float bias = W.b1[hb * TS + c];
+#if PGM_PK_ELEM
+                        tanh_bias_pk<16>(z[hb], bias, H1[hb]);
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) scr[rowof(r, h) * SCR + hb * TS + c] = H1[hb][r];
+#else
 #pragma unroll
                         for (int r = 0; r < 16; ++r) {
                             H1[hb][r] = tanh_fast(z[hb][r] + bias);
                             scr[rowof(r, h) * SCR + hb * TS + c] = H1[hb][r];
                         }
+#endif
                     }
                     wave_lds_fence();
                     // ---- layer 2: Z2[s][o] = H1[s][:] . W2t[:][o]   (A from the transpose tile)
@@ -423,8 +460,12 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
 #pragma unroll
                     for (int ob = 0; ob < 2; ++ob) {
                         const float bias = W.b2[ob * TS + c];
+#if PGM_PK_ELEM
+                        tanh_bias_pk<16>(z[ob], bias, H2[ob]);
+#else
 #pragma unroll
                         for (int r = 0; r < 16; ++r) H2[ob][r] = tanh_fast(z[ob][r] + bias);
+#endif
                     }
                     PGM_STAMP(4);
                     wave_lds_fence();  // every lane finished reading the H1 tile
@@ -541,6 +582,23 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
 #else
                     // ---- heads on the VALU: lane = sample c, half h sums units [32h, 32h+32)
                     float outv[Q];
+#if PGM_EXP != 27
+                    // packed: v_pk_fma_f32 over unit pairs (even / odd partial sums, added at the end; Walker P = 40
+                    // 5.845 -> 5.79-5.83 ms).  PGM_EXP 27 (A/B): one scalar FMA chain per output
+                    f2v acc2[Q];
+#pragma unroll
+                    for (int q = 0; q < Q; ++q) acc2[q] = f2v{0.f, 0.f};
+PGM_UNROLL(16)
+                    for (int u2 = 0; u2 < TS / 2; ++u2) {
+                        const f2v hv = f2v{scr[c * SCR + h * TS + 2 * u2], scr[c * SCR + h * TS + 2 * u2 + 1]};
+#pragma unroll
+                        for (int q = 0; q < Q; ++q)
+                            acc2[q] = __builtin_elementwise_fma(hv, *reinterpret_cast<const f2v*>(&W.Wh[q][h * TS + 2 * u2]),
+                                                                acc2[q]);
+                    }
+#pragma unroll
+                    for (int q = 0; q < Q; ++q) outv[q] = acc2[q].x + acc2[q].y;
+#else
 #pragma unroll
                     for (int q = 0; q < Q; ++q) outv[q] = 0.f;
 PGM_UNROLL(ONE ? PGM_U_HEAD : 4)
@@ -549,6 +607,7 @@ PGM_UNROLL(ONE ? PGM_U_HEAD : 4)
 #pragma unroll
                         for (int q = 0; q < Q; ++q) outv[q] = fmaf(hv, W.Wh[q][h * TS + u], outv[q]);
                     }
+#endif
 #pragma unroll
                     for (int q = 0; q < Q; ++q) outv[q] = half_sum(outv[q]) + W.bh[q];
                     PGM_STAMP(16);
@@ -642,12 +701,19 @@ PGM_UNROLL(ONE ? PGM_U_HEAD : 4)
                     }
                     f32x16 dZ2[2];
 #pragma unroll
-                    for (int ob = 0; ob < 2; ++ob)
+                    for (int ob = 0; ob < 2; ++ob) {
+#if PGM_PK_ELEM
+                        dtanh_pk<16>(z[ob], H2[ob], dZ2[ob]);
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) gB2[ob] += dZ2[ob][r];
+#else
 #pragma unroll
                         for (int r = 0; r < 16; ++r) {
                             dZ2[ob][r] = z[ob][r] * (1.f - H2[ob][r] * H2[ob][r]);
                             gB2[ob] += dZ2[ob][r];
                         }
+#endif
+                    }
                     PGM_STAMP(6);
                     // ---- dH1 = dZ2 W2  (A = dZ2 through the transpose tile, B = W2t[in][o] column); the critical
                     // path, so its MFMAs go into the pipe first and dW2 queues behind them
@@ -681,12 +747,19 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
                     if constexpr (!GW2_FIRST) gw2();
                     f32x16 dZ1[2];
 #pragma unroll
-                    for (int ib = 0; ib < 2; ++ib)
+                    for (int ib = 0; ib < 2; ++ib) {
+#if PGM_PK_ELEM
+                        dtanh_pk<16>(z[ib], H1[ib], dZ1[ib]);
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) gB1[ib] += dZ1[ib][r];
+#else
 #pragma unroll
                         for (int r = 0; r < 16; ++r) {
                             dZ1[ib][r] = z[ib][r] * (1.f - H1[ib][r] * H1[ib][r]);
                             gB1[ib] += dZ1[ib][r];
                         }
+#endif
+                    }
                     // ---- dW1^T[k][h] += X^T dZ1  (A = X[s(r)][k = lane], B = dZ1 reg r)
 #pragma unroll
                     for (int r = 0; r < 16; ++r) {
@@ -1384,11 +1457,17 @@ __global__ __launch_bounds__(64 * W) void ppo_update_t16_kernel(MArgs a) {
 #pragma unroll
                     for (int hb = 0; hb < 4; ++hb) {
                         const float bias = Wt.b1[hb * T16 + c];
+#if PGM_PK_ELEM
+                        tanh_bias_pk<4>(z[hb], bias, H1[hb]);
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) scr[(4 * g + r) * S16 + hb * T16 + c] = H1[hb][r];
+#else
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
                             H1[hb][r] = tanh_fast(z[hb][r] + bias);
                             scr[(4 * g + r) * S16 + hb * T16 + c] = H1[hb][r];
                         }
+#endif
                     }
                     wave_lds_fence();
                     // ---- layer 2: Z2[s][o] = H1[s][:] . W2t[:][o]  (A from the transpose tile)
@@ -1405,8 +1484,12 @@ PGM_UNROLL(ONE ? PGM_U16 : 4)
 #pragma unroll
                     for (int ob = 0; ob < 4; ++ob) {
                         const float bias = Wt.b2[ob * T16 + c];
+#if PGM_PK_ELEM
+                        tanh_bias_pk<4>(z[ob], bias, H2[ob]);
+#else
 #pragma unroll
                         for (int r = 0; r < 4; ++r) H2[ob][r] = tanh_fast(z[ob][r] + bias);
+#endif
                     }
                     PGM_STAMP(4);
                     wave_lds_fence();  // every lane finished reading the H1 tile
@@ -1496,12 +1579,19 @@ PGM_UNROLL(ONE ? PGM_U16 : 4)
                     }
                     f32x4 dZ2[4];
 #pragma unroll
-                    for (int ob = 0; ob < 4; ++ob)
+                    for (int ob = 0; ob < 4; ++ob) {
+#if PGM_PK_ELEM
+                        dtanh_pk<4>(z[ob], H2[ob], dZ2[ob]);
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) gB2[ob] += dZ2[ob][r];
+#else
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
                             dZ2[ob][r] = z[ob][r] * (1.f - H2[ob][r] * H2[ob][r]);
                             gB2[ob] += dZ2[ob][r];
                         }
+#endif
+                    }
                     PGM_STAMP(6);
 #pragma unroll
                     for (int ob = 0; ob < 4; ++ob)
@@ -1533,12 +1623,19 @@ PGM_UNROLL(ONE ? PGM_U16 : 4)
                     if constexpr (!GW2_FIRST) gw2();
                     f32x4 dZ1[4];
 #pragma unroll
-                    for (int ib = 0; ib < 4; ++ib)
+                    for (int ib = 0; ib < 4; ++ib) {
+#if PGM_PK_ELEM
+                        dtanh_pk<4>(z[ib], H1[ib], dZ1[ib]);
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) gB1[ib] += dZ1[ib][r];
+#else
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
                             dZ1[ib][r] = z[ib][r] * (1.f - H1[ib][r] * H1[ib][r]);
                             gB1[ib] += dZ1[ib][r];
                         }
+#endif
+                    }
                     // ---- dW1^T[k][h] += X^T dZ1  (A = X[sample 4g + r][feature 16 kb + c], B = dZ1 register r)
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {

@@ -59,4 +59,34 @@ __device__ __forceinline__ float group4_sum(float v) {
 __device__ __forceinline__ float wmin2(float a, float b) { return a < b ? 1.f : (a == b ? 0.5f : 0.f); }
 __device__ __forceinline__ float wmax2(float a, float b) { return a > b ? 1.f : (a == b ? 0.5f : 0.f); }
 
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// Elementwise tile math on register PAIRS through the packed fp32 ALU (v_pk_add / v_pk_mul / v_pk_fma_f32); per
+// element the same operations as tanh_fast / the scalar tanh' product.
+template <int N, typename V>
+__device__ __forceinline__ void tanh_bias_pk(const V& z, float bias, V& out) {
+#pragma unroll
+    for (int r = 0; r < N; r += 2) {
+        const f2v x = f2v{z[r], z[r + 1]} + f2v{bias, bias};
+        const f2v y = x * f2v{2.8853900817779268f, 2.8853900817779268f};
+        const f2v e = f2v{__builtin_amdgcn_exp2f(y.x), __builtin_amdgcn_exp2f(y.y)};
+        const f2v d = e + f2v{1.f, 1.f};
+        const f2v rc = f2v{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+        const f2v o = __builtin_elementwise_fma(f2v{-2.f, -2.f}, rc, f2v{1.f, 1.f});
+        out[r] = o.x;
+        out[r + 1] = o.y;
+    }
+}
+// out = z * (1 - a * a) (tanh' chain rule), pairs
+template <int N, typename V>
+__device__ __forceinline__ void dtanh_pk(const V& z, const V& a, V& out) {
+#pragma unroll
+    for (int r = 0; r < N; r += 2) {
+        const f2v av = f2v{a[r], a[r + 1]};
+        const f2v o = f2v{z[r], z[r + 1]} * __builtin_elementwise_fma(-av, av, f2v{1.f, 1.f});
+        out[r] = o.x;
+        out[r + 1] = o.y;
+    }
+}
+
 }  // namespace pgm

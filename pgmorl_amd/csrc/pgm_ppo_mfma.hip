@@ -70,36 +70,10 @@ inline int t16_grid(int P, int NS) { return PGM_T16_XCD8 ? 16 * NS * ((P + 7) / 
 
 namespace pgm {
 
-typedef float f2v __attribute__((ext_vector_type(2)));
-
-// PGM_EXP 29 (A/B): the tiles' elementwise tanh(z + b) and tanh' products on register PAIRS through the packed fp32
-// ALU (v_pk_add / v_pk_mul / v_pk_fma_f32; per element the same operations and roundings as tanh_fast)
-#define PGM_PK_ELEM (PGM_EXP == 29)
-template <int N, typename V>
-__device__ __forceinline__ void tanh_bias_pk(const V& z, float bias, V& out) {
-#pragma unroll
-    for (int r = 0; r < N; r += 2) {
-        const f2v x = f2v{z[r], z[r + 1]} + f2v{bias, bias};
-        const f2v y = x * f2v{2.8853900817779268f, 2.8853900817779268f};
-        const f2v e = f2v{__builtin_amdgcn_exp2f(y.x), __builtin_amdgcn_exp2f(y.y)};
-        const f2v d = e + f2v{1.f, 1.f};
-        const f2v rc = f2v{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
-        const f2v o = __builtin_elementwise_fma(f2v{-2.f, -2.f}, rc, f2v{1.f, 1.f});
-        out[r] = o.x;
-        out[r + 1] = o.y;
-    }
-}
-// out = z * (1 - a * a) (tanh' chain rule), pairs
-template <int N, typename V>
-__device__ __forceinline__ void dtanh_pk(const V& z, const V& a, V& out) {
-#pragma unroll
-    for (int r = 0; r < N; r += 2) {
-        const f2v av = f2v{a[r], a[r + 1]};
-        const f2v o = f2v{z[r], z[r + 1]} * __builtin_elementwise_fma(-av, av, f2v{1.f, 1.f});
-        out[r] = o.x;
-        out[r + 1] = o.y;
-    }
-}
+// the tiles' elementwise tanh(z + b) and tanh' products on register PAIRS through the packed fp32 ALU (v_pk_add /
+// v_pk_mul / v_pk_fma_f32; per element the same operations as tanh_fast): MODE 2 Walker P = 40 5.80 -> 5.76-5.77 ms,
+// t16 unchanged.  PGM_EXP 29 (A/B): one element per instruction.  (MODE 2's Adam on element pairs: no change, 5.76.)
+#define PGM_PK_ELEM (PGM_EXP != 29)
 
 // The image reductions add exactly ONE partial onto a stored one per element per round (store and add ordered by a
 // barrier): a read + add + write in the wave.  PGM_EXP 23 (A/B only): ds_add_f32 instead (the same two-operand sum,

@@ -43,6 +43,8 @@ PGM_STAMP_UNIT(wupd)
 // second read hits that XCD's L2): Humanoid P = 20 update 31.1 -> 30.4 ms, 56.2 -> 47.8 GB per launch
 // (profiles/r03o_*).  PGM_EXP 50 (A/B): the round-2 map (the NS parts of one tower on one XCD)
 #define PGM_WIDE_COLOC (PGM_EXP != 50)
+// (the VALU heads and elementwise tanh on register pairs through the packed fp32 ALU, as in the narrow kernels, made
+// this kernel slower: 30.4 -> 33.3 ms at Humanoid P = 20, it already runs at the 512-register limit)
 // (all 2 NS workgroups of a task on one XCD, groups of 8 tasks: 30.4 -> 30.6-30.7 ms, kept out)
 namespace pgm {
 inline int wide_grid(int P, int NS) { return NS == 1 ? 2 * P : 8 * NS * ((P + 3) / 4); }

@@ -651,14 +651,27 @@ PGM_UNROLL(ONE ? PGM_U_HEAD : 4)
                     }
 #endif
                     PGM_STAMP(5);
-                    // ---- head-weight grads (VALU, C layout): gWh[ob][q] += sum_r H2[s][u] dO[s][q]
+                    // ---- head-weight grads (VALU, C layout): gWh[ob][q] += sum_r H2[s][u] dO[s][q]; output pairs on the
+                    // packed ALU (each output still sums over r in order: the same values).  PGM_EXP 33 (A/B): scalar
+                    constexpr bool GWH_PK = Q % 2 == 0 && PGM_EXP != 33;
 #pragma unroll
                     for (int ob = 0; ob < 2; ++ob)
 #pragma unroll
                         for (int r = 0; r < 16; ++r) {
                             const int s = rowof(r, h);
+                            if constexpr (GWH_PK) {
+                                const f2v hv = f2v{H2[ob][r], H2[ob][r]};
 #pragma unroll
-                            for (int q = 0; q < Q; ++q) gWh[ob][q] = fmaf(H2[ob][r], S.dout[w][s][q], gWh[ob][q]);
+                                for (int q = 0; q < Q; q += 2) {
+                                    const f2v a2 = __builtin_elementwise_fma(
+                                        hv, *reinterpret_cast<const f2v*>(&S.dout[w][s][q]), f2v{gWh[ob][q], gWh[ob][q + 1]});
+                                    gWh[ob][q] = a2.x;
+                                    gWh[ob][q + 1] = a2.y;
+                                }
+                            } else {
+#pragma unroll
+                                for (int q = 0; q < Q; ++q) gWh[ob][q] = fmaf(H2[ob][r], S.dout[w][s][q], gWh[ob][q]);
+                            }
                         }
                     // ---- dH2 = dO . Wh  (MFMA; A = this lane's sample, k = head output) -> dZ2
                     z[0] = z[1] = f32x16{0};

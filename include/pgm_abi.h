@@ -177,8 +177,9 @@ int pgm_adv_normalize(const pgm_dims* d, const pgm_rollout_buf* rb, const double
  * workspace: caller-owned device bytes (pgm_ppo_update_workspace_bytes), required (PGM_E_INVALID_ARG
  * when NULL), reset inside the call on `stream` unless pgm_ppo_update_reset did it since the last call.
  * The critic and actor towers of a task run on separate CUs that exchange the squared gradient norm per
- * minibatch step; each tower is further split over four CUs (a quarter of the minibatch rows each, gradient images added through the workspace) while
- * 32 * ceil(P/4) <= CU count, else over two CUs while 16 * ceil(P/4) <= CU count.  obs_dim <= 32: tower
+ * minibatch step; each tower is further split over four CUs (a quarter of the minibatch rows each, gradient
+ * images added through the workspace) while 64 * ceil(P/8) <= CU count, else over two CUs while
+ * 32 * ceil(P/8) <= CU count (obs_dim > 32: 32 * ceil(P/4) / 16 * ceil(P/4)).  obs_dim <= 32: tower
  * images LDS-resident (falls back to 2 CUs per task, then 1, as P grows); obs_dim > 32 (Humanoid): layer
  * 1 streamed from L2, needs 2P <= CU count (PGM_E_UNSUPPORTED otherwise: shard the tasks over more
  * GPUs).  PGM_UPDATE_SPLIT=0/1/2/3/4 caps the split (3 = an A/B-only variant, selected only explicitly).

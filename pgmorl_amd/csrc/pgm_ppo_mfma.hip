@@ -2145,10 +2145,10 @@ int launch_ppo_update_mfma(const pgm_dims* d, const MArgs& a, const pgm_rollout_
     if (int rc = launch_status("pgm_ppo_update (pack rows)")) return rc;
     // every workgroup of a split launch must be resident at once: one per CU (LDS > 80 KiB, 512 registers
     // per lane), so the grid must fit the CU count.  PGM_UPDATE_SPLIT selects: 4 (default) = 16-row tiles
-    // on 4 workgroups per tower (8 CUs per task, while 32 ceil(P / 4) <= CUs; Walker P = 20: 6.4 ms vs
+    // on 4 workgroups per tower (8 CUs per task, while t16_grid(P, 4) <= CUs; Walker P = 20: 6.4 ms vs
     // MODE 2's 7.1 ms), 3 = 16-row tiles on 2 workgroups of 8 waves per tower (A/B only: it spills and is
     // slower than MODE 2, so only an explicit 3 selects it), 2 = 32-row tiles on 2 workgroups per tower
-    // (4 CUs per task, while 16 ceil(P / 4) <= CUs), 1 = one workgroup per tower (2P <= CUs), 0 = one
+    // (4 CUs per task, while mode2_grid(P) <= CUs), 1 = one workgroup per tower (2P <= CUs), 0 = one
     // workgroup per task; each falls back to the next one down when its grid does not fit.
     static_assert(sizeof(MSmem<O, A, K, true>) > 80 * 1024, "split residency argument needs > 80 KiB LDS");
     const char* sel = getenv("PGM_UPDATE_SPLIT");

@@ -8,8 +8,11 @@ objective merge (RCCL all-gather of the per-task objective vectors when N > 1).
 Counted env-steps = tasks x num_processes x num_steps per step (eval steps are not counted,
 like the reference's FPS print, morl/mopg.py:159).
 
-    python bench.py [--gpus N --steps K --warmup W]
+    python bench.py [--gpus N --steps K --warmup W]       # N > 1: starts the N ranks itself
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+At N > 1 the headline line is weak scaling (--tasks per GPU) and carries a second timed leg, `strong`: the
+fixed population --strong-tasks (40) split over the ranks in task blocks (40 -> 20 / 10 / 5 per GPU).
 """
 import argparse
 import glob
@@ -33,7 +36,9 @@ PEAK_HBM_GBS = 8000.0
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--gpus', type=int, default=None,
+                    help='ranks (GPUs); without a launcher (WORLD_SIZE unset) bench.py starts them itself; under '
+                         'torch.distributed.run it must equal WORLD_SIZE (default: WORLD_SIZE, else 1)')
     ap.add_argument('--steps', type=int, default=5)
     ap.add_argument('--warmup', type=int, default=2)
     ap.add_argument('--env-name', default='MO-Walker2d-v2')
@@ -61,6 +66,10 @@ def parse():
     ap.add_argument('--traffic-file', default=None,
                     help='PMC summary (scripts/pmc_summary.py) to quote as roofline.traffic; default: the newest '
                          'profiles/r0*_pmc_*.json whose workload matches this run')
+    ap.add_argument('--strong-tasks', type=int, default=40,
+                    help='global population of the strong-scaling leg (split over the ranks in task blocks)')
+    ap.add_argument('--no-strong', action='store_true', help='skip the strong-scaling leg at N > 1')
+    ap.add_argument('--stub-cpu', action='store_true', help=argparse.SUPPRESS)  # launcher tests (gloo, no GPU)
     return ap.parse_args()
 
 
@@ -275,61 +284,117 @@ def whole_run(args, iter_value):
                       f'num_env_steps {int(args.whole_run_steps)}, N=4, T=2048, E=10, M=32, device RNG, seed 0'}
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
-    dev = torch.device('cuda', local)
-    torch.cuda.set_device(dev)
+def pmc_traffic(args, workload, kernel):
+    """roofline.traffic: HBM-side bytes per launch of the update kernel from the committed PMC summary of THIS
+    workload at HEAD (profiles/pmc_head.json: one entry per workload, the kernel family checked against the one
+    the launcher picks; A/B files are not listed there).  (None, reason) when none matches."""
+    if args.traffic_file:
+        try:
+            d = json.load(open(args.traffic_file))
+        except Exception as e:
+            return None, f'{args.traffic_file}: {e!r}'
+        ent = {'kernel': d.get('kernel'), 'hbm_bytes_per_launch': d.get('hbm_bytes_per_launch'),
+               'source': args.traffic_file} if d.get('workload') == workload else None
+    else:
+        try:
+            ent = json.load(open(os.path.join(ROOT, 'profiles', 'pmc_head.json')))['entries'].get(workload)
+        except Exception as e:
+            return None, f'profiles/pmc_head.json: {e!r}'
+    if not ent:
+        return None, f'no PMC summary for {workload}'
+    fam = (kernel or '').split(' ')[0]
+    if not fam or fam not in (ent.get('kernel') or ''):
+        return None, f"PMC summary {ent['source']} is for {ent.get('kernel')}, not {kernel}"
+    return ent['hbm_bytes_per_launch'], ent['source']
 
-    from pgmorl_amd import envspec
+
+def launch_ranks(n):
+    """``python bench.py --gpus N`` with no launcher around it: start N rank processes of this script, one per GPU,
+    with the environment torch.distributed.run would give them (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR =
+    127.0.0.1 / MASTER_PORT), and return the first failing rank's exit code (0 when all succeed).  This parent never
+    touches the GPU (no HIP call, no exec): each child selects its device before its first HIP call.  Only rank 0
+    prints the JSON line; a rank that fails ends the others (SIGTERM, then SIGKILL after 30 s)."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK='0', MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, '-u', os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    rc, t_fail, live = 0, None, list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc, t_fail = (c if c > 0 else 1), time.time()
+                print(f'bench.py: rank {procs.index(p)} exited with {c}; stopping the other ranks', file=sys.stderr)
+                for q in live:
+                    q.terminate()
+        if t_fail is not None and time.time() - t_fail > 30:
+            for q in live:
+                q.kill()
+        time.sleep(0.1)
+    return rc
+
+
+def _gather_ints(x, dev):
+    """All-gather one int per rank (list form: works on gloo and RCCL)."""
+    t = torch.tensor([x], dtype=torch.int64, device=dev)
+    parts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, t)
+    return [int(p.item()) for p in parts]
+
+
+def leg_gpu(args, spec, dev, rank, world, blocks, tag):
+    """Time one population layout: rank r trains tasks blocks[r] = [lo, hi) of a population of blocks[-1][1].
+    W warm-up iterations, then exactly K timed ones between a barrier + synchronize on both sides; returns
+    {dt (max over ranks), upd_ms (max over ranks), history of gathered objective vectors, kernel}."""
     from pgmorl_amd.policy import new_policy
     from pgmorl_amd.runtime import TaskBatch
-    from pgmorl_amd.shard import allreduce_max, task_block
-    spec = envspec.make_spec(args.env_name)
+    from pgmorl_amd.shard import allreduce_max
     N, T, E, M = args.num_processes, args.num_steps, args.ppo_epoch, args.num_mini_batch
-    if args.scaling == 'strong':
-        G = args.tasks  # global population, rank r trains its contiguous block
-        lo, hi = task_block(G, rank, world)
-    else:
-        G = args.tasks * world
-        lo, hi = rank * args.tasks, (rank + 1) * args.tasks
+    G = blocks[-1][1]
+    lo, hi = blocks[rank]
     P = hi - lo
-    if P <= 0:
-        raise SystemExit(f'rank {rank}: no tasks (global {G} over {world} ranks)')
-    tb = TaskBatch(args.env_name, P, num_processes=N, num_steps=T, ppo_epoch=E, num_mini_batch=M, device=dev)
-    torch.manual_seed(rank * 1000)
-    w = np.linspace(0, 1, G)[lo:hi]
-    for p in range(P):
-        pol = new_policy(spec['obs_dim'], spec['act_dim'], spec['obj_num'])
-        tb.set_task(p, pol.state_dict(), {}, None, [w[p], 1 - w[p]] if spec['obj_num'] == 2 else
-                    np.ones(spec['obj_num']) / spec['obj_num'])
-    tb.env_reset()
-    per = -(-G // world)  # all-gather rows per rank (blocks padded to the largest)
+    per = max(b - a for a, b in blocks)  # all-gather rows per rank (blocks padded to the largest)
     gathered = torch.zeros(world * per, spec['obj_num'], dtype=torch.float64, device=dev)
     mine = torch.zeros(per, spec['obj_num'], dtype=torch.float64, device=dev)
+    tb = None
+    if P > 0:
+        tb = TaskBatch(args.env_name, P, num_processes=N, num_steps=T, ppo_epoch=E, num_mini_batch=M, device=dev)
+        torch.manual_seed(rank * 1000)
+        w = np.linspace(0, 1, G)[lo:hi]
+        for p in range(P):
+            pol = new_policy(spec['obs_dim'], spec['act_dim'], spec['obj_num'])
+            tb.set_task(p, pol.state_dict(), {}, None, [w[p], 1 - w[p]] if spec['obj_num'] == 2 else
+                        np.ones(spec['obj_num']) / spec['obj_num'])
+        tb.env_reset()
     total_updates = 5_000_000 // T // N
-
     history = []  # every iteration's gathered objective vectors (the offspring the EP is built from)
+    overlap = not args.no_overlap_eval and tb is not None
 
     def step(j):
         # the evaluation of iteration j runs on the side stream beside iteration j+1's rollout; the objective
         # vectors are gathered on that stream behind it
-        tb.iteration(j, 3e-4 * (1 - j / total_updates), carry=True, overlap_eval=not args.no_overlap_eval)
-        side = tb.eval_stream if not args.no_overlap_eval else torch.cuda.current_stream()
+        if tb is not None:
+            tb.iteration(j, 3e-4 * (1 - j / total_updates), carry=True, overlap_eval=overlap)
+        side = tb.eval_stream if overlap else torch.cuda.current_stream()
         with torch.cuda.stream(side):
             if world > 1:
-                mine[:P].copy_(tb.objs)
+                if tb is not None:
+                    mine[:P].copy_(tb.objs)
                 dist.all_gather_into_tensor(gathered, mine)
+                history.append(torch.cat([gathered[r * per:r * per + b - a] for r, (a, b) in enumerate(blocks)]))
             else:
                 gathered.copy_(tb.objs)
-            history.append(torch.cat([gathered[r * per:r * per + task_block(G, r, world)[1] - task_block(G, r, world)[0]]
-                                      for r in range(world)]) if args.scaling == 'strong' else gathered.clone())
-            if not args.no_overlap_eval:
+                history.append(gathered.clone())
+            if overlap:
                 # the next PPO update waits on this event: the RCCL gather never runs beside the update's
                 # co-resident exchange workgroups
                 tb._eval_done = torch.cuda.Event()
@@ -344,16 +409,17 @@ def main():
         dist.barrier()
     # per-launch duration of the dominant kernel (ppo_update) with events on the launch stream
     ev = []
-    orig_update = tb.ppo_update_launch
+    if tb is not None:
+        orig_update = tb.ppo_update_launch
 
-    def timed_update():
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-        orig_update()
-        e.record()
-        ev.append((s, e))
+        def timed_update():
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            orig_update()
+            e.record()
+            ev.append((s, e))
 
-    tb.ppo_update_launch = timed_update
+        tb.ppo_update_launch = timed_update
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -363,56 +429,156 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    tb.ppo_update_launch = orig_update
-    tb.check_update()  # a timed-out exchange invalidates the run: raises PGMError (after the timed region)
-    upd_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    if tb is not None:
+        tb.ppo_update_launch = orig_update
+        tb.check_update()  # a timed-out exchange invalidates the run: raises PGMError (after the timed region)
+    upd_ms = float(np.mean([s.elapsed_time(e) for s, e in ev])) if ev else 0.0
     dt, upd_ms = allreduce_max([dt, upd_ms], dev)  # the slowest rank defines the step
+    kernel = update_kernel_name(spec['obs_dim'], P) if P > 0 else None
+    del tb
+    torch.cuda.empty_cache()
+    return {'dt': dt, 'upd_ms': upd_ms, 'P': P, 'history': history, 'kernel': kernel, 'tag': tag}
+
+
+def leg_stub(args, spec, dev, rank, world, blocks, tag):
+    """CPU stand-in for leg_gpu (--stub-cpu, tests only): the same rank plumbing, barriers, objective all-gather and
+    max-over-ranks timing around a fixed sleep of 0.1 ms per task, so the launcher and the JSON assembly can be
+    tested with gloo on a machine without a GPU.  Never a measurement."""
+    from pgmorl_amd.shard import allreduce_max
+    G = blocks[-1][1]
+    lo, hi = blocks[rank]
+    P = hi - lo
+    per = max(b - a for a, b in blocks)
+    history = []
+    if os.environ.get('PGM_BENCH_STUB_FAIL_RANK') == str(rank):  # launcher test: one rank dies mid-run
+        raise SystemExit(3)
+
+    def step(j):
+        time.sleep(1e-4 * P)
+        mine = torch.zeros(per, spec['obj_num'], dtype=torch.float64)
+        mine[:P] = torch.arange(lo, hi, dtype=torch.float64)[:, None] + j
+        parts = [torch.empty_like(mine) for _ in range(world)] if world > 1 else [mine]
+        if world > 1:
+            dist.all_gather(parts, mine)
+        history.append(torch.cat([parts[r][:b - a] for r, (a, b) in enumerate(blocks)]))
+
+    for j in range(args.warmup):
+        step(j)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for j in range(args.warmup, args.warmup + args.steps):
+        step(j)
+    if world > 1:
+        dist.barrier()
+    dt, upd_ms = allreduce_max([time.perf_counter() - t0, 0.0], dev)
+    assert all(h.shape[0] == G for h in history)
+    assert all(torch.equal(h[:, 0], torch.arange(G, dtype=torch.float64) + i) for i, h in enumerate(history))
+    return {'dt': dt, 'upd_ms': upd_ms, 'P': P, 'history': history, 'kernel': 'stub', 'tag': tag}
+
+
+def main():
+    args = parse()
+    env_ws = os.environ.get('WORLD_SIZE')
+    if env_ws is None:
+        if (args.gpus or 1) > 1:
+            sys.exit(launch_ranks(args.gpus))
+        world, rank, local = 1, 0, 0
+    else:
+        world, rank, local = int(env_ws), int(os.environ.get('RANK', '0')), int(os.environ.get('LOCAL_RANK', '0'))
+        if args.gpus is not None and args.gpus != world:
+            sys.exit(f'bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks; run '
+                     f'`python bench.py --gpus N` (it starts the N ranks itself) or torch.distributed.run with '
+                     f'--nproc-per-node equal to --gpus')
+    if args.stub_cpu:
+        dev = torch.device('cpu')
+        if world > 1:
+            dist.init_process_group('gloo')
+        leg = leg_stub
+    else:
+        if world > 1:
+            torch.cuda.set_device(local)
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        dev = torch.device('cuda', local)
+        torch.cuda.set_device(dev)
+        leg = leg_gpu
+    n_gpus = 1
+    if world > 1:  # the rank count the collectives actually see
+        seen = _gather_ints(rank, dev)
+        if sorted(seen) != list(range(world)):
+            raise SystemExit(f'bench.py: ranks seen {seen} != range({world})')
+        n_gpus = len(seen)
+
+    from pgmorl_amd import envspec
+    from pgmorl_amd.shard import task_block
+    spec = envspec.make_spec(args.env_name)
+    N, T, E, M = args.num_processes, args.num_steps, args.ppo_epoch, args.num_mini_batch
+    if args.scaling == 'strong':  # a global population of --tasks, rank r trains its contiguous block
+        blocks = [task_block(args.tasks, r, world) for r in range(world)]
+    else:  # --tasks on every rank
+        blocks = [(r * args.tasks, (r + 1) * args.tasks) for r in range(world)]
+    if blocks[rank][1] <= blocks[rank][0] and args.scaling == 'weak':
+        raise SystemExit(f'rank {rank}: no tasks')
+    G = blocks[-1][1]
+    main_leg = leg(args, spec, dev, rank, world, blocks, args.scaling)
+    P = main_leg['P']
+    dt, upd_ms = main_leg['dt'], main_leg['upd_ms']
     env_steps = G * N * T * args.steps  # every rank's tasks (the max-over-ranks time covers them all)
     value = env_steps / dt
+    # the fixed population split over the ranks (SURVEY §8(e): pop 40 -> 40 / 20 / 10 / 5 per GPU), measured in the
+    # same run: the strong-scaling curve the north star targets (>= 6x at 1 -> 8), beside the weak headline
+    strong = None
+    if not args.no_strong and args.scaling == 'weak':
+        sblocks = [task_block(args.strong_tasks, r, world) for r in range(world)]
+        sl = main_leg if sblocks == blocks else leg(args, spec, dev, rank, world, sblocks, 'strong')
+        strong = {'global_tasks': args.strong_tasks, 'tasks_per_rank': [b - a for a, b in sblocks],
+                  'value': args.strong_tasks * N * T * args.steps / sl['dt'], 'unit': 'env steps/sec',
+                  'ms_per_step': sl['dt'] / args.steps * 1e3, 'update_ms': sl['upd_ms'],
+                  'update_kernel_rank0': sl['kernel'], 'scaling': 'strong',
+                  'note': 'same workload as the headline line' if sl is main_leg else
+                          'second timed leg of this run (same steps / warm-up), max over ranks'}
+        del sl
     mf = mflops_per_row(spec['obs_dim'], spec['act_dim'], spec['obj_num'])
     upd_flop = P * T * N * E * 6 * mf          # fwd (2 M_f) + bwd (4 M_f) per row per epoch, one launch
-    achieved = upd_flop / (upd_ms * 1e-3) / 1e12
-    traffic = None
-    wl = f'{args.env_name}/P{P}/N{N}/T{T}/E{E}/M{M}'
-    cands = [args.traffic_file] if args.traffic_file else sorted(glob.glob(os.path.join(ROOT, 'profiles', 'r0*_pmc_*.json')) +
-                                                               [os.path.join(ROOT, 'profiles', 'r01_ppo_update_pmc.json')], reverse=True)
-    for f in cands:
-        try:
-            tr = json.load(open(f))
-        except Exception:
-            continue
-        if tr.get('workload') == wl and tr.get('hbm_bytes_per_launch'):
-            traffic = tr['hbm_bytes_per_launch']
-            break
+    achieved = upd_flop / (upd_ms * 1e-3) / 1e12 if upd_ms > 0 else 0.0
+    kernel = main_leg['kernel']
+    traffic, traffic_src = pmc_traffic(args, f'{args.env_name}/P{P}/N{N}/T{T}/E{E}/M{M}', kernel)
+    alg_bytes = P * T * N * E * 4 * (spec['obs_dim'] + spec['act_dim'] + 2 * spec['obj_num'] + 2)
     out = {
-        'metric': METRIC, 'value': value, 'unit': 'env steps/sec', 'n_gpus': world, 'steps': args.steps,
+        'metric': METRIC, 'value': value, 'unit': 'env steps/sec', 'n_gpus': n_gpus, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': dt / args.steps * 1e3, 'higher_is_better': True, 'scaling': args.scaling,
         'vs_baseline': None, 'dtype': 'fp32', 'data': f"synthetic (SynthMO-{args.env_name.split('-')[1]} env, reference-order random init)",
         'config': {'workload': f'{args.env_name} (SynthMO) pop={G} ({args.scaling} scaling, {P} tasks on rank 0), '
                                f'N={N}, T={T}, ppo_epoch={E}, num_mini_batch={M}, eval_num=1, perf-mode device RNG',
                    'env': args.env_name, 'tasks_per_gpu': P, 'global_tasks': G, 'num_processes': N,
-                   'num_steps': T, 'ppo_epoch': E, 'num_mini_batch': M, 'parallelism': f'task-sharded x{world}'},
-        'roofline': {'bound': 'mfma', 'kernel': update_kernel_name(spec['obs_dim'], P), 'achieved': achieved,
+                   'num_steps': T, 'ppo_epoch': E, 'num_mini_batch': M, 'parallelism': f'task-sharded x{n_gpus}'},
+        'roofline': {'bound': 'mfma', 'kernel': kernel, 'achieved': achieved,
                      'peak': PEAK_FP32_TFLOPS, 'unit': 'TFLOP/s', 'frac': achieved / PEAK_FP32_TFLOPS,
-                     'traffic': traffic, 'avg_launch_ms': upd_ms, 'flop_per_launch': upd_flop,
-                     'algorithmic_bytes_per_launch': P * T * N * E * 4 * (spec['obs_dim'] + spec['act_dim'] +
-                                                                          2 * spec['obj_num'] + 2)},
+                     'traffic': traffic, 'traffic_source': traffic_src,
+                     'traffic_vs_algorithmic': traffic / alg_bytes if traffic else None,
+                     'avg_launch_ms': upd_ms, 'flop_per_launch': upd_flop, 'algorithmic_bytes_per_launch': alg_bytes},
         # whole-iteration view (SURVEY.md §8(d)): env-steps/s x algorithmic FLOP (or bytes) per env-step vs peak
         'path_roofline': {'flop_per_env_step': 2 * mf * (1 + 3 * E),
-                          'compute_frac': value * 2 * mf * (1 + 3 * E) / (world * PEAK_FP32_TFLOPS * 1e12),
+                          'compute_frac': value * 2 * mf * (1 + 3 * E) / (n_gpus * PEAK_FP32_TFLOPS * 1e12),
                           'bytes_per_env_step': bytes_per_env_step(spec['obs_dim'], spec['act_dim'],
                                                                    spec['obj_num'], E),
                           'hbm_frac': value * bytes_per_env_step(spec['obs_dim'], spec['act_dim'], spec['obj_num'],
-                                                                 E) / (world * PEAK_HBM_GBS * 1e9)},
+                                                                 E) / (n_gpus * PEAK_HBM_GBS * 1e9)},
     }
-    out['hypervolume'] = hypervolume(args, history, G * N * T * len(history))
+    if strong is not None:
+        out['strong'] = strong
+    if args.stub_cpu:
+        out['data'] = 'STUB (--stub-cpu: launcher / rank plumbing test, not a measurement)'
+    else:
+        out['hypervolume'] = hypervolume(args, main_leg['history'], G * N * T * len(main_leg['history']))
+    del main_leg
     if args.whole_run is None:
-        args.whole_run = world == 1 and args.env_name == 'MO-Walker2d-v2' and args.scaling == 'weak'
+        args.whole_run = world == 1 and args.env_name == 'MO-Walker2d-v2' and args.scaling == 'weak' \
+            and not args.stub_cpu
     if args.whole_run:
-        del tb, history
         torch.cuda.empty_cache()
         out['whole_run'] = whole_run(args, value)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.stub_cpu:
         out['cpu_baseline'] = cb = cpu_baseline(args, spec, G)
         out['vs_96vcpu_extrapolated'] = value / cb['extrapolated_96vcpu']
     if rank == 0:

@@ -20,7 +20,7 @@ import numpy as np
 import torch
 
 from .runtime import TaskBatch
-from .sample import DeviceSnapshot, RunningMeanStd, Sample
+from .sample import DeviceSnapshot, RowStore, RunningMeanStd, Sample
 from .shard import allgather_rows, move_rows, owner_of, task_block, world
 
 
@@ -149,20 +149,22 @@ class MOPGPopulation:
         """Collective: gather the snapshots of ``samples`` onto rank ``dst`` (final/EP_policy_*.pt)."""
         return self.place(samples, [dst] * len(samples))
 
-    def check_generation(self, tb):
+    def check_generation(self, tb, step_mismatch=None):
         """Collective (every rank, also one without tasks): PGMError on EVERY rank when any rank's update timed
-        out in a cross-workgroup exchange this generation, before anyone enters the record all-gather (a rank
-        raising alone would leave the others blocked in that collective)."""
+        out in a cross-workgroup exchange this generation, and RuntimeError on every rank when any rank's Adam
+        step counts are not the expected ones (``step_mismatch``: that rank's message), before anyone enters the
+        record all-gather (a rank raising alone would leave the others blocked in that collective)."""
         from ._lib import PGMError
         from .runtime import UPDATE_TIMEOUT_MSG
-        from .shard import any_rank
+        from .shard import allreduce_max
         failed = bool(tb.take_update_failed()) if tb is not None else False
         rank, ws = world()
-        if ws > 1:
-            if any_rank(failed, self.device):
-                raise PGMError(UPDATE_TIMEOUT_MSG + ('' if failed else ' (on another rank)'))
-        elif failed:
-            raise PGMError(UPDATE_TIMEOUT_MSG)
+        any_failed, any_mismatch = (allreduce_max([float(failed), float(step_mismatch is not None)], self.device)
+                                    if ws > 1 else (float(failed), float(step_mismatch is not None)))
+        if any_failed:
+            raise PGMError(UPDATE_TIMEOUT_MSG + ('' if failed else ' (on another rank)'))
+        if any_mismatch:
+            raise RuntimeError(step_mismatch or 'Adam step counts differ from the expected ones on another rank')
 
     def run(self, task_batch, iteration, num_updates, start_time=None, log=print):
         """Every task's MOPG iterations [iteration, iteration + num_updates) -> all_offspring_batch.
@@ -197,6 +199,7 @@ class MOPGPopulation:
             step0 = [t.sample.snapshot.adam_step for t in task_batch[lo:hi]]
             tb.env_reset()  # envs are re-created and reset every generation (mopg.py:67-82)
             arena = torch.empty(I, 3, Pl, L, dtype=torch.float32, device=self.device)
+            store = RowStore(arena, 'arena')
             rec = torch.empty(I, tb._stats64.numel(), dtype=torch.float64, device=self.device)
             objs_ar = torch.empty(I, Pl, tb.K, dtype=torch.float64, device=self.device)  # written by the evals
             for i, j in enumerate(its):
@@ -216,16 +219,19 @@ class MOPGPopulation:
             if os.environ.get('PGM_DEBUG_TASKS'):
                 print(f'[debug] generation at iteration {iteration}: P={P} local={Pl} iters={I} '
                       f'failed={int(tb.update_failed.item())}', flush=True)
-        self.check_generation(tb)  # a timed-out exchange never becomes an offspring (PGMError on every rank)
-        probe = tb if tb is not None else None
-        O, K = (probe.O, probe.K) if probe is not None else (layout.O, layout.K)
+        mismatch = None
+        B = a.num_steps * a.num_processes
+        per_iter = a.ppo_epoch * (B // (B // a.num_mini_batch))  # Adam steps of one iteration
         if tb is not None:
-            B = a.num_steps * a.num_processes
-            per_iter = a.ppo_epoch * (B // (B // a.num_mini_batch))  # Adam steps of one iteration
             got = tb.adam_step.cpu().numpy()
             want = np.asarray(step0) + I * per_iter
             if not np.array_equal(got, want):
-                raise RuntimeError(f'Adam step counts {got} != expected {want}')
+                mismatch = f'rank {rank}: Adam step counts {got} != expected {want}'
+        # a timed-out exchange or a lost Adam step never becomes an offspring (raised on every rank together)
+        self.check_generation(tb, mismatch)
+        probe = tb if tb is not None else None
+        O, K = (probe.O, probe.K) if probe is not None else (layout.O, layout.K)
+        if tb is not None:
             host_rec = rec.cpu().numpy()
             host_objs = objs_ar.cpu().numpy()
             stv = [tb.stat_views(host_rec[i], Pl) for i in range(I)]
@@ -247,12 +253,11 @@ class MOPGPopulation:
             for i in range(I):
                 if ws == 1 or own == rank:
                     step = step0[q] + (i + 1) * per_iter
-                    snap = DeviceSnapshot.in_arena(layout, arena, i, q, step, owner=rank if ws > 1 else None)
+                    snap = DeviceSnapshot.in_arena(layout, store, i, q, step, owner=rank if ws > 1 else None)
                     objs = host_objs[i, q].copy()
                     fn = (lambda st=stv[i], q=q: self._env_params(st, q, O, K))
                 else:
-                    B = a.num_steps * a.num_processes
-                    step = int(steps_all[p]) + (i + 1) * a.ppo_epoch * (B // (B // a.num_mini_batch))
+                    step = int(steps_all[p]) + (i + 1) * per_iter
                     snap = DeviceSnapshot.remote(layout, step, own)
                     r = allr[p, i]
                     objs = r[:K].copy()

@@ -23,7 +23,7 @@ from .mopg import MOPGPopulation
 from .pareto import EP, OptGraph, weight_grid
 from .policy import new_policy
 from .population import make_population
-from .sample import DeviceSnapshot, RunningMeanStd, Sample, Task, WeightedSumScalarization
+from .sample import DeviceSnapshot, RunningMeanStd, Sample, Task, WeightedSumScalarization, compact_snapshots
 from .shard import world
 
 
@@ -155,12 +155,17 @@ def run(args, device='cuda', rng='device', log=print, runtime=None):
             gen_writer.submit(generation_record(
                 args.save_dir, iteration, args.obj_num, ep, population, opt_graph, elite_batch, scalarization_batch,
                 all_offspring_batch, predicted_offspring_objs if args.selection_method == 'prediction-guided' else None))
+        # device memory follows the survivors (EP, population, next elites), not every offspring of the run: drop
+        # this generation's offspring lists and gather the live snapshots out of its arena
+        n_tasks = len(task_batch)
+        steps = n_tasks * n_its * args.num_steps * args.num_processes
+        del all_offspring_batch, all_sample_batch, offspring_batch, last_offspring_batch, task_batch
+        compact_snapshots()
         t2 = time.perf_counter()
-        steps = len(task_batch) * n_its * args.num_steps * args.num_processes
         timing['rl_s'] += t1 - t0
         timing['host_s'] += t2 - t1
         timing['train_env_steps'] += steps
-        timing['generations'].append({'iteration': iteration, 'tasks': len(task_batch), 'iters': n_its,
+        timing['generations'].append({'iteration': iteration, 'tasks': n_tasks, 'iters': n_its,
                                       'rl_s': round(t1 - t0, 4), 'host_s': round(t2 - t1, 4)})
     t_final = time.perf_counter()
     runtime.materialize(list(ep.sample_batch), dst=0)  # collective: EP snapshots onto the writing rank

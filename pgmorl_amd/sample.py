@@ -8,6 +8,7 @@ right after an iteration) and are only materialised as reference-format tensors 
 ``sample.agent.optimizer.state_dict()`` a torch Adam state_dict.
 """
 import copy
+import weakref
 
 import numpy as np
 import torch
@@ -61,13 +62,65 @@ class WeightedSumScalarization:
         return (objs * self.weights).sum(axis=-1)
 
 
+class RowStore:
+    """Device storage shared by snapshots: a generation's arena ([I][3][Pl][L], key (i, slot)) or a compact
+    buffer ([S][3][L], key k).  Tracks the snapshots that point into it (weakly), so ``compact_snapshots`` can
+    move the survivors out and let the storage go.  Every live store is in ``RowStore.live``."""
+    live = weakref.WeakSet()
+
+    def __init__(self, tensor, kind):
+        assert kind in ('arena', 'compact')
+        self.t, self.kind = tensor, kind
+        self.snaps = weakref.WeakSet()
+        RowStore.live.add(self)
+
+    @property
+    def rows(self):
+        return self.t.shape[0] * self.t.shape[2] if self.kind == 'arena' else self.t.shape[0]
+
+    def view(self, key):
+        return self.t[key[0], :, key[1]] if self.kind == 'arena' else self.t[key]
+
+
+def compact_snapshots(min_live_frac=0.5):
+    """Move the snapshots that are still alive out of every finished generation arena (and out of compact
+    buffers less than ``min_live_frac`` live) into one new compact [S][3][L] buffer per source, by one gather
+    each, and rewire them; the old storage is freed once nothing else references it.  Called at every generation
+    boundary by pgmorl_amd.morl.run after EP / population / selection, so device memory follows the surviving
+    snapshots (EP + population + elites), not every iteration of every task of the run.  Returns (stores
+    compacted, rows kept)."""
+    n_st = n_rows = 0
+    for st in list(RowStore.live):
+        snaps = [s for s in list(st.snaps) if s._store is st]
+        if not snaps:
+            continue
+        keys = sorted({s._key for s in snaps})
+        if st.kind == 'compact' and len(keys) >= min_live_frac * st.rows:
+            continue
+        if st.kind == 'arena':
+            i = torch.tensor([k[0] for k in keys], device=st.t.device)
+            q = torch.tensor([k[1] for k in keys], device=st.t.device)
+            new = st.t[i, :, q]  # advanced indexing on dims 0 and 2 -> [S][3][L], a fresh tensor
+        else:
+            new = st.t[torch.tensor(keys, device=st.t.device)]
+        ns = RowStore(new, 'compact')
+        where = {k: j for j, k in enumerate(keys)}
+        for s in snaps:
+            s._bind(ns, where[s._key])
+        st.snaps = weakref.WeakSet()
+        n_st += 1
+        n_rows += len(keys)
+    return n_st, n_rows
+
+
 class DeviceSnapshot:
     """Parameters + Adam state of one task, kept on the device of the rank that produced it.
 
     Snapshots are IMMUTABLE once taken: the per-iteration copies of a generation live in one device arena
     ([iterations][3][tasks][L], ``MOPGPopulation.run``) and a snapshot is an index into it (``in_arena``), so
     taking, cloning (Task / Sample.copy_from) and dropping snapshots moves no bytes.  Tensors are views,
-    created on first use.
+    created on first use.  At the generation boundary ``compact_snapshots`` moves the survivors into a compact
+    buffer, so an arena does not outlive its generation because one of its snapshots survived.
 
     Multi-GPU: every rank holds the same Samples (identical host state), but a snapshot's tensors live
     only on its ``owner`` rank; elsewhere it is a remote handle (no data) that ``MOPGPopulation`` moves to the
@@ -78,7 +131,7 @@ class DeviceSnapshot:
     def __init__(self, layout, params, adam_m, adam_v, adam_step, owner=None):
         self.layout = layout
         self._data = None if params is None else (params, adam_m, adam_v)
-        self._arena = None  # (arena [I][3][Pl][L], iteration, slot) -- the block view is made on demand
+        self._store, self._key = None, None  # (RowStore, key) -- the block view is made on demand
         self._blk = None
         self.adam_step = int(adam_step)
         self.owner = owner
@@ -88,22 +141,27 @@ class DeviceSnapshot:
         return cls(layout, None, None, None, adam_step, owner)
 
     @classmethod
-    def in_arena(cls, layout, arena, i, slot, adam_step, owner=None):
-        """Snapshot = row (i, :, slot) of a generation's arena (no copy)."""
+    def in_arena(cls, layout, store, i, slot, adam_step, owner=None):
+        """Snapshot = row (i, :, slot) of a generation's arena store (no copy)."""
         s = cls(layout, None, None, None, adam_step, owner)
-        s._arena = (arena, i, slot)
+        s._bind(store, (i, slot))
         return s
+
+    def _bind(self, store, key):
+        self._store, self._key = store, key
+        self._blk = self._data = None  # cached views of the previous storage
+        if store is not None:
+            store.snaps.add(self)
 
     @property
     def is_local(self):
-        return self._data is not None or self._arena is not None or self._blk is not None
+        return self._data is not None or self._store is not None or self._blk is not None
 
     def block(self):
-        """[3, L] params | exp_avg | exp_avg_sq (a view when the snapshot lives in an arena or was adopted)."""
+        """[3, L] params | exp_avg | exp_avg_sq (a view when the snapshot lives in a store or was adopted)."""
         if self._blk is None:
-            if self._arena is not None:
-                ar, i, q = self._arena
-                self._blk = ar[i, :, q]
+            if self._store is not None:
+                self._blk = self._store.view(self._key)
             elif self._data is not None:
                 self._blk = torch.stack(self._data)
             else:
@@ -112,7 +170,7 @@ class DeviceSnapshot:
 
     @property
     def data(self):
-        if self._data is None and (self._arena is not None or self._blk is not None):
+        if self._data is None and (self._store is not None or self._blk is not None):
             b = self.block()
             self._data = (b[0], b[1], b[2])
         return self._data
@@ -133,12 +191,16 @@ class DeviceSnapshot:
 
     def adopt(self, rows):
         """Materialise a remote handle from a received [3, L] block (it becomes a local replica)."""
-        self._blk, self._data, self._arena = rows, None, None
+        self._bind(None, None)
+        self._blk = rows
 
     def clone(self):
         """Snapshots are immutable: a clone shares the device storage (no copy)."""
         c = DeviceSnapshot(self.layout, None, None, None, self.adam_step, self.owner)
-        c._data, c._arena, c._blk = self._data, self._arena, self._blk
+        if self._store is not None:
+            c._bind(self._store, self._key)
+        else:
+            c._data, c._blk = self._data, self._blk
         return c
 
 

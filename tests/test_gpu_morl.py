@@ -42,6 +42,10 @@ def test_morl_run_results_tree(gpu, tmp_path, env, K, selection):
     offs = np.loadtxt(tmp_path / '2' / 'elites' / 'offsprings.txt', delimiter=',', ndmin=2)
     n_warm = len(pareto.weight_grid(K, 0.5))
     assert offs.shape == (n_warm * 2, K) and np.isfinite(offs).all()  # warm-up tasks x 2 warm-up iterations
+    # every survivor was moved out of its generation's arena (device memory follows the survivors)
+    from pgmorl_amd.sample import RowStore
+    assert all(s.snapshot._store is None or s.snapshot._store.kind == 'compact' for s in ep.sample_batch)
+    assert not [st for st in RowStore.live if st.kind == 'arena' and len(st.snaps)]
     sd = torch.load(tmp_path / 'final' / 'EP_policy_0.pt', weights_only=True)
     assert sorted(sd) == sorted(k for k, _, _ in STATE_KEYS)
     assert sd['dist.logstd._bias'].shape == (3, 1) and sd['base.actor.0.weight'].dtype == torch.float64

@@ -134,3 +134,43 @@ def test_unflatten_batch_rows_equal_unflatten():
         for (key, _, _), b in zip(STATE_KEYS, blocks):
             assert b[i].dtype == np.float64 and b[i].flags.c_contiguous
             np.testing.assert_array_equal(b[i], sd[key].numpy())
+
+
+def test_compact_snapshots_frees_arena_keeps_survivors():
+    """a surviving offspring must not keep its whole generation's arena alive.  After
+    compact_snapshots the survivors (and their clones) read the same rows from a compact buffer, the arena is
+    released, and a compact buffer that falls below half live is compacted again."""
+    import gc
+    import weakref
+
+    from pgmorl_amd.layout import ParamLayout
+    from pgmorl_amd.sample import DeviceSnapshot, RowStore, compact_snapshots
+    lay = ParamLayout(3, 2, 2)
+    I, Pl, L = 4, 5, 7
+    arena = torch.arange(I * 3 * Pl * L, dtype=torch.float32).reshape(I, 3, Pl, L)
+    ref = arena.clone()
+    st = RowStore(arena, 'arena')
+    snaps = {(i, q): DeviceSnapshot.in_arena(lay, st, i, q, 10 * i + q) for i in range(I) for q in range(Pl)}
+    keep = [snaps[(0, 1)], snaps[(3, 4)], snaps[(2, 0)]]
+    twin = keep[1].clone()
+    _ = keep[0].params  # cached views of the arena must be dropped by the rebind
+    wa = weakref.ref(arena)
+    del snaps, st, arena
+    gc.collect()
+    n_st, n_rows = compact_snapshots()
+    assert n_rows == 3
+    gc.collect()
+    assert wa() is None, 'the arena outlived its generation'
+    for s, (i, q) in zip(keep + [twin], [(0, 1), (3, 4), (2, 0), (3, 4)]):
+        assert torch.equal(s.block(), ref[i, :, q]) and torch.equal(s.params, ref[i, 0, q])
+        assert s._store.kind == 'compact' and s._store.t.shape == (3, 3, L)
+    assert twin._store is keep[1]._store and twin._key == keep[1]._key
+    # two of three rows die: the compact buffer (1/3 live) is compacted again, the survivor keeps its values
+    buf = weakref.ref(keep[0]._store.t)
+    del keep[1:], twin, s
+    gc.collect()
+    compact_snapshots()
+    gc.collect()
+    assert buf() is None and keep[0]._store.t.shape == (1, 3, L)
+    assert torch.equal(keep[0].block(), ref[0, :, 1])
+    assert compact_snapshots() == (0, 0)  # a fully live compact buffer stays put

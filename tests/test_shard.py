@@ -200,10 +200,11 @@ def test_place_moves_only_relocated_snapshots_gloo(ws, P):
     _spawn(_place_worker, ws, P)
 
 
-def _failure_worker(rank, ws, port, failing, P, errq):
-    """MOPGPopulation.check_generation over gloo: the rank(s) in ``failing`` saw an exchange timeout in their update;
-    every rank -- also one that owns no task of the generation (tb None) -- must raise PGMError together and then
-    still complete a collective (nobody is left blocked in one)."""
+def _failure_worker(rank, ws, port, failing, P, errq, kind='timeout'):
+    """MOPGPopulation.check_generation over gloo: the rank(s) in ``failing`` saw an exchange timeout in their update
+    (kind 'timeout') or wrong Adam step counts (kind 'steps'); every rank -- also one that owns no task of the
+    generation (tb None) -- must raise (PGMError / RuntimeError) together and then still complete a collective
+    (nobody is left blocked in one)."""
     try:
         import argparse
         from pgmorl_amd._lib import PGMError
@@ -213,15 +214,18 @@ def _failure_worker(rank, ws, port, failing, P, errq):
 
         class _TB:  # stands in for TaskBatch's sticky timeout flag
             def take_update_failed(self):
-                return rank in failing
+                return kind == 'timeout' and rank in failing
 
         lo, hi = task_block(P, rank, ws)
         rt = MOPGPopulation(argparse.Namespace(env_name='MO-Hopper-v2'), device='cpu')
         raised = False
+        mismatch = f'rank {rank}: steps' if kind == 'steps' and rank in failing else None
         try:
-            rt.check_generation(_TB() if hi > lo else None)
+            rt.check_generation(_TB() if hi > lo else None, mismatch)
         except PGMError:
-            raised = True
+            raised = kind == 'timeout'
+        except RuntimeError:
+            raised = kind == 'steps'
         assert raised == bool(failing), (rank, raised)
         dist.barrier()  # every rank got here: no one hangs in the check's collective
         dist.destroy_process_group()
@@ -234,12 +238,13 @@ def _failure_worker(rank, ws, port, failing, P, errq):
         raise
 
 
-@pytest.mark.parametrize('ws,failing,P', [(2, (1,), 4), (3, (0,), 2), (3, (), 5), (2, (0, 1), 2)])
-def test_update_failure_raises_on_every_rank_gloo(ws, failing, P):
+@pytest.mark.parametrize('ws,failing,P,kind', [(2, (1,), 4, 'timeout'), (3, (0,), 2, 'timeout'), (3, (), 5, 'timeout'),
+                                             (2, (0, 1), 2, 'timeout'), (2, (1,), 4, 'steps'), (3, (2,), 7, 'steps')])
+def test_update_failure_raises_on_every_rank_gloo(ws, failing, P, kind):
     ctx = mp.get_context('spawn')
     errq = ctx.SimpleQueue()
     port = _free_port()
-    procs = [ctx.Process(target=_failure_worker, args=(r, ws, port, failing, P, errq)) for r in range(ws)]
+    procs = [ctx.Process(target=_failure_worker, args=(r, ws, port, failing, P, errq, kind)) for r in range(ws)]
     for p in procs:
         p.start()
     for p in procs:

@@ -10,8 +10,8 @@ ROOT = os.path.dirname(HERE)
 LIB = os.path.join(HERE, 'libpgm.so')
 OBJDIR = os.path.join(HERE, 'build')
 SOURCES = ['pgm_abi.cpp', 'pgm_policy_env.hip', 'pgm_rollout_lanes.hip', 'pgm_rollout_wide.hip', 'pgm_misc.hip', 'pgm_ppo_update.hip',
-           'pgm_ppo_mfma.hip', 'pgm_ppo_wide.hip']
-HEADERS = ['pgm_common.hpp', 'pgm_dispatch.hpp', 'pgm_rollout.hpp', 'pgm_mfma.hpp']
+           'pgm_ppo_mfma.hip', 'pgm_ppo_fs.hip', 'pgm_ppo_wide.hip']
+HEADERS = ['pgm_common.hpp', 'pgm_dispatch.hpp', 'pgm_rollout.hpp', 'pgm_mfma.hpp', 'pgm_ppo_shared.hpp']
 ARCH = os.environ.get('PGM_OFFLOAD_ARCH', 'gfx950')
 FLAGS = ['-O3', '-std=c++17', '-fPIC', f'--offload-arch={ARCH}', '-I', os.path.join(ROOT, 'include')]
 

@@ -35,7 +35,9 @@ constexpr int ppo_img_floats(int O, int A, int K) {  // TowerImg<O, A, K> of pgm
     return O * H + H * (H + 1) + Q * H + 2 * H + Q + A;
 }
 constexpr int PGM_NS_MAX = 4;  // workgroups per tower of the row-split updates
-inline size_t ppo_flag_bytes(int P) { return ((size_t)(4 * PGM_NS_MAX * P + 1) * 8 + 255) / 256 * 256; }
+// granules: [0, 16 P + 1) the norm granules + timeout word of the MODE 2 / t16 / wide updates, then from 16 P + 8 the
+// feature-split update's image / norm / parameter granules ([3][P][2][<= 16 parts][2 parities], pgm_ppo_fs.hip)
+inline size_t ppo_flag_bytes(int P) { return ((size_t)(208 * P + 8) * 8 + 255) / 256 * 256; }
 // norm granule of (task p, tower m, row part hs, step parity par): (row part 0, parity 0) below the timeout word
 // (word 2P), the others above it.  Double-buffered by step parity like the image slots: a workgroup rewrites a
 // granule only two steps later, after every reader has matched it, so a delayed poll can never miss its tag.
@@ -58,6 +60,8 @@ inline size_t ppo_reset_bytes(const pgm_dims* d) {
 // pgm_ppo_update_reset marks a workspace as zeroed (up to n bytes, ordered by the caller's streams); a launch
 // needing <= n zeroed bytes consumes the mark instead of issuing its own reset (pgm_ppo_update.hip)
 bool ws_take_zeroed(const void* ws, size_t need);
+// feature-split update (pgm_ppo_fs.hip): its exchange payload after the sample table (0 when it cannot run)
+size_t fs_workspace_extra(const pgm_dims* d);
 // obs_dim > 32 (wide kernel): flags, exchange slots [P][2 towers][NS parts][2 parities], parts 1..NS-1's
 // private [P][NS-1][L] parameter copies (sized for PGM_NS_MAX parts)
 inline size_t ppo_workspace_bytes(const pgm_dims* d) {
@@ -65,9 +69,10 @@ inline size_t ppo_workspace_bytes(const pgm_dims* d) {
         return ppo_flag_bytes(d->P) + wide_xbuf_bytes(d) +
                (size_t)d->P * (PGM_NS_MAX - 1) * make_layout(d->O, d->A, d->K, d->H).total * sizeof(float);
     return ppo_flag_bytes(d->P) + ppo_xbuf_bytes(d) +
-           (size_t)d->P * d->T * d->N * ppo_row_stride(d->O, d->A, d->K) * sizeof(float);
+           (size_t)d->P * d->T * d->N * ppo_row_stride(d->O, d->A, d->K) * sizeof(float) + fs_workspace_extra(d);
 }
 int device_cu_count();  // CUs of the current device (cached)
+
 // Co-residency precondition of the persistent update kernels (their workgroups spin on each other's tagged
 // flags, so every workgroup of the grid must be resident at once): the occupancy query for this kernel,
 // block size and LDS must admit grid <= blocks-per-CU x CUs.  PGM_E_UNSUPPORTED (with the numbers) otherwise.

@@ -1,0 +1,722 @@
+// Feature-split PPO update with a reduce-scattered Adam (obs_dim <= 32): the latency form of the update for small
+// per-GPU populations (strong scaling: pop 40 over 8 GPUs = 5 tasks per GPU) and the alternative at every P.
+//
+// Work split.  Each tower of a task runs on NS workgroups (2 NS per task, all on one XCD under round-robin dispatch);
+// workgroup hs takes rows [hs mb / NS, (hs + 1) mb / NS) of every minibatch: R = mb / (16 NS) 16-row tiles.  Inside
+// a workgroup the FOUR WAVES SPLIT THE 64 HIDDEN FEATURES (wave w: features 16w .. 16w + 15) instead of the rows, on
+// the v_mfma_f32_16x16x4_f32 layout
+//     C/D: lane l, register r <-> (row 4(l >> 4) + r, column l & 15); A: lane l holds A[l & 15][l >> 4];
+//     B: lane l holds B[l >> 4][l & 15]
+// so a wave's gradient partials are DISJOINT blocks of the tower's gradient (no intra-workgroup image reduction):
+// dW1^T / dW2^T rows x the wave's 16 output columns, the head weights of its 16 units, its b1 / b2 entries.  The
+// feature-contracting products (Z2 = H1 W2^T, the heads, dH1 = dZ2 W2) read the other waves' activations from
+// shared LDS tiles, three workgroup barriers per minibatch step.
+//
+// Exchange (per Adam step, tags = step + 1, slots double-buffered by step parity):
+//   1. every wave publishes its gradient blocks (1 KiB "fragments" = the f32x4 C registers of 64 lanes) with
+//      16-B sc1 stores, the workgroup drains and one lane stores the tagged image flag {step, loss sum};
+//   2. REDUCE-SCATTER: block b belongs to part b mod NS, which sums it over the NS parts in part order (sc1 loads) --
+//      a sum only its owner forms, so it is deterministic without being replicated;
+//   3. the owners' squared norms meet through one tagged 8-B granule per (tower, part): every workgroup sums the
+//      2 NS granules in one fixed order (clip_grad_norm_ over both towers);
+//   4. each owner runs Adam on ITS blocks (parameters and moments of the owned blocks live in registers for the whole
+//      launch), publishes the new parameter blocks (sc1) + a tagged flag, and every workgroup gathers the other
+//      parts' blocks into its LDS parameter image.
+// Three cross-CU hops per Adam step, each moving ~1/NS of the image per reader instead of every partner's whole
+// image (pgm_ppo_mfma.hip's t16 / MODE 2), and Adam on 1/NS of the parameters per workgroup.
+//
+// Reference semantics (a2c_ppo_acktr/algo/ppo.py:58-115, storage.py:118-154, model.py:75-82, distributions.py:29-40)
+// as in pgm_ppo_mfma.hip, including torch.min/max/clamp tie gradients; entropy_coef enters once per tower.
+#include <stdlib.h>
+
+#include "pgm_dispatch.hpp"
+#include "pgm_ppo_shared.hpp"
+
+PGM_STAMP_UNIT(fs)
+
+namespace pgm {
+
+// ---------------------------------------------------------------- geometry shared by host and device
+// gradient / parameter fragments of one tower: per wave w (feature block w) K1B dW1 blocks, 4 dW2 blocks, 1 head
+// block, 1 vector block (b1, b2 and, wave 0, head bias / logstd)
+constexpr int fs_bpw(int O) { return (O + 15) / 16 + 6; }
+constexpr int fs_nb(int O) { return 4 * fs_bpw(O); }
+constexpr int fs_nown(int O, int NS) { return (fs_nb(O) + NS - 1) / NS; }  // blocks per owner (max)
+// payload: image slots [P][2][NS][2 parities][NB KiB], then parameter slots [P][2][NS][2][NOWN KiB]
+inline size_t fs_payload_bytes(int P, int O, int NS) {
+    return (size_t)P * 2 * NS * 2 * (size_t)(fs_nb(O) + fs_nown(O, NS)) * 1024;
+}
+// NS sized by the workspace: the largest power of two with 16 NS ceil(P/8) <= 256 (a 256-CU MI355X), at most 16
+inline int fs_ns_cap(int P) {
+    const int groups = (P + 7) / 8;
+    int ns = 16;
+    while (ns > 1 && 16 * ns * groups > 256) ns >>= 1;
+    return ns;
+}
+inline int fs_grid(int P, int NS) { return 16 * NS * ((P + 7) / 8); }
+// tagged granules of the exchange, in the zeroed flag region after the norm granules of the other updates:
+// kind 0 = image flag, 1 = squared-norm granule, 2 = parameter flag
+__host__ __device__ inline int fs_gran(int P, int NS, int kind, int p, int m, int hs, int par) {
+    return 16 * P + 8 + ((((kind * P + p) * 2 + m) * NS + hs) * 2 + par);
+}
+
+size_t fs_workspace_extra(const pgm_dims* d) {
+    if (d->O > 32) return 0;
+    const int ns = fs_ns_cap(d->P);
+    return ns >= 2 ? fs_payload_bytes(d->P, d->O, ns) : 0;
+}
+
+// fragment slot (block b, lane l, register r) -> tower image index (TowerImg), -1 for padding
+template <int O, int A, int K>
+__device__ __forceinline__ int frag_img(int b, int l, int r, int m) {
+    constexpr int Q = qmax<A, K>(), K1B = (O + 15) / 16, BPW = fs_bpw(O);
+    constexpr int oW2 = O * H, oWh = oW2 + H * SCR, oB1 = oWh + Q * H, oB2 = oB1 + H, oBh = oB2 + H, oLs = oBh + Q;
+    const int wb = b / BPW, k = b - wb * BPW, g = l >> 4, c = l & 15;
+    const int NQ = m == 0 ? K : A;
+    if (k < K1B) {
+        const int in = 16 * k + 4 * g + r;
+        return in < O ? in * H + 16 * wb + c : -1;
+    }
+    if (k < K1B + 4) return oW2 + (16 * (k - K1B) + 4 * g + r) * SCR + 16 * wb + c;
+    if (k == K1B + 4) return c < NQ ? oWh + c * H + 16 * wb + 4 * g + r : -1;
+    if (g != 0) return -1;
+    if (r == 0) return oB1 + 16 * wb + c;
+    if (r == 1) return oB2 + 16 * wb + c;
+    if (r == 2) return wb == 0 && c < NQ ? oBh + c : -1;
+    return wb == 0 && m == 1 && c < A ? oLs + c : -1;
+}
+
+template <int O, int A, int K, int R>
+struct FsSmem {
+    static constexpr int Q = qmax<A, K>();
+    static constexpr int RS = row_stride<O, A, K>();
+    static constexpr int RSL = RS + 4;
+    static constexpr int SB = 16 * R;                          // rows of this part per minibatch
+    static constexpr int NDT = (SB * RSL + 255) / 256;         // 1-KiB LDS-DMA pieces per staged pass
+    static constexpr int SBI = 64 * ((SB + 63) / 64);          // index slots (one 64-lane DMA per wave)
+    static constexpr bool ZA = R >= 8;                         // dZ2 tile aliases the H2 tile (LDS budget)
+    static constexpr int NDO = R >= 4 ? 1 : 4;                 // dO tiles: shared (row-split heads) or per wave
+    TowerImg<O, A, K> Pm;                                      // parameters (working copy of every part)
+    alignas(16) float RB[2][NDT * 256];                        // packed rows of this / the next minibatch
+    int32_t IB[2][SBI];                                        // sample indices of the next two minibatches
+    float H1s[SB][S16];                                        // H1 of all tiles, all 64 features
+    float H2s[SB][S16];                                        // H2 (R >= 8: then dZ2)
+    float Zs[ZA ? 1 : SB][S16];                                // dZ2
+    float dOs[NDO][SB][DQS];                                   // dL/d(head output), transposed for dH2
+    float aiv[A];                                              // actor 1 / std^2
+    float red[192];  // [0, 64) head-bias partials / poll results, [64, 128) logstd partials / norms, 128+ loss sums
+};
+template <int O, int A, int K, int R>
+constexpr size_t fs_smem_bytes() {  // > 80 KiB: one workgroup per CU (the co-residency argument of the launcher)
+    return sizeof(FsSmem<O, A, K, R>) > 81 * 1024 ? sizeof(FsSmem<O, A, K, R>) : 81 * 1024;
+}
+
+template <int O, int A, int K, int NS, int R>
+__global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
+    static_assert(O <= 32 && R >= 1 && R <= 8 && (R & (R - 1)) == 0, "fs tiles");
+    using Sm = FsSmem<O, A, K, R>;
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    auto& S = *reinterpret_cast<Sm*>(smem_raw);
+    constexpr int Q = qmax<A, K>();
+    static_assert(Q <= DQ, "head outputs beyond the dO tile");
+    constexpr int KS1 = (O + 3) / 4, K1B = (O + 15) / 16;
+    constexpr int IMG = img_floats<O, A, K>(), RS = Sm::RS, RSL = Sm::RSL, SB = Sm::SB, NDT = Sm::NDT;
+    constexpr int CR = RS / 4;
+    constexpr int BPW = fs_bpw(O), NB = fs_nb(O), NOWN = fs_nown(O, NS);
+    constexpr int OWV = (NOWN + 3) / 4;  // owned blocks per wave (block j of the part: wave j mod 4)
+    constexpr int ISB = NB * 1024, PSB = NOWN * 1024;
+    constexpr bool HSPLIT = R >= 4;      // heads: row tiles split over the waves (else every wave does all)
+    constexpr int NHT = HSPLIT ? R / 4 : R;
+    constexpr int NC = R == 1 ? 2 : 1;   // accumulator chains per tile of the 16-deep contractions
+    constexpr int oW2 = O * H, oWh = oW2 + H * SCR, oB1 = oWh + Q * H, oB2 = oB1 + H, oBh = oB2 + H, oLs = oBh + Q;
+    const int t = threadIdx.x, l = t & 63, g = l >> 4, c = l & 15;
+    const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+    // block map: groups of 16 NS blocks for 8 tasks; block r holds part (r >> 4) % NS of tower (r >> 3) & 1 of task
+    // 8 G + (r & 7), so every workgroup of a task shares blocks b, b + 8, ... (one XCD: speed only)
+    const int bx = (int)blockIdx.x;
+    const int j16 = (bx >> 3) % (2 * NS);
+    const int p = 8 * (bx / (16 * NS)) + (bx & 7);
+    const int hs = j16 >> 1, m = j16 & 1;
+    if (p >= a.P) return;
+    const int NQ = m == 0 ? K : A;
+    const int N = a.N, T = a.T, B = T * N;
+    const int E = a.hp.ppo_epoch, M = a.hp.num_mini_batch;
+    const int mb = B / M, nb = B / mb;
+    const int r0 = hs * mb / NS;
+    const int npass = E * nb;
+    const float clip = a.hp.clip_param;
+    const Layout& L = a.L;
+    float* __restrict__ P = a.params + (size_t)p * L.total;
+    float* __restrict__ Mo = a.m + (size_t)p * L.total;
+    float* __restrict__ Vo = a.v + (size_t)p * L.total;
+    const float* rows = a.rows + (size_t)p * B * RS;
+    const int fsbytes = (int)((size_t)a.P * 2 * NS * 2 * (ISB + PSB));
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(a.fsp, 0, fsbytes, 0x00020000);
+    constexpr int SC1 = 16;
+    auto islot = [&](int h, int par) { return ((((p * 2 + m) * NS + h) * 2 + par)) * ISB; };
+    auto pslot = [&](int h, int par) { return a.P * 2 * NS * 2 * ISB + ((((p * 2 + m) * NS + h) * 2 + par)) * PSB; };
+    auto gran = [&](int kind, int mm, int h, int par) { return a.ws + fs_gran(a.P, NS, kind, p, mm, h, par); };
+    unsigned long long* const fail_word = a.ws + 2 * a.P;
+
+    // ---- staging (as the 16-row kernel): the minibatch's permutation indices by 4-B LDS-DMA one minibatch
+    // earlier than its rows; rows by 16-B LDS-DMA (pieces past SB * RSL re-read the last row into padding)
+    auto issue_idx = [&](int gi, int buf, int wi, int nwv) {
+        const int e = gi / nb, bb = gi - e * nb;
+        const int32_t* src = a.perms + (size_t)e * B + bb * mb + r0;
+        for (int q0 = wi * 64; q0 < SB; q0 += 64 * nwv)
+            __builtin_amdgcn_global_load_lds((const void*)(src + min(q0 + l, SB - 1)), (lds_void_t*)&S.IB[buf][q0], 4,
+                                             0, 0);
+    };
+    auto issue_rows = [&](int buf, int ibuf, int wi, int nwv) {
+        float* base = &S.RB[buf][0];
+        for (int d = wi; d < NDT; d += nwv) {
+            const int pos = d * 256 + 4 * l, row = min(pos / RSL, SB - 1), chunk = (pos - (pos / RSL) * RSL) >> 2;
+            const int idx = S.IB[ibuf][row];
+            const float* src = rows + (size_t)idx * RS + (chunk < CR ? chunk : 0) * 4;
+            __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_t*)(base + d * 256), 16, 0, 0);
+        }
+    };
+
+    // ---- parameter image, owned blocks' parameters and moments (registers for the whole launch)
+    float* Pf = &S.Pm.W1t[0][0];
+    for (int i = t; i < IMG; i += 256) {
+        const int f = img_to_flat<O, A, K>(i, m, L);
+        Pf[i] = f >= 0 ? P[f] : 0.f;
+    }
+    if (t < A) S.aiv[t] = expf(-2.f * P[L.off[PGM_P_LOGSTD] + t]);
+    f32x4 op[OWV], om[OWV], ov[OWV];
+#pragma unroll
+    for (int i = 0; i < OWV; ++i) {
+        const int b = hs + NS * (w + 4 * i);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int ii = b < NB ? frag_img<O, A, K>(b, l, r, m) : -1;
+            const int f = ii >= 0 ? img_to_flat<O, A, K>(ii, m, L) : -1;
+            op[i][r] = f >= 0 ? P[f] : 0.f;
+            om[i][r] = f >= 0 ? Mo[f] : 0.f;
+            ov[i][r] = f >= 0 ? Vo[f] : 0.f;
+        }
+    }
+    issue_idx(0, 0, w, 4);
+    if (npass > 1) issue_idx(1, 1, w, 4);
+    dma_sync_m();
+    issue_rows(0, 0, w, 4);
+    dma_sync_m();
+
+    const int step0 = a.step[p];
+    const double lr = a.lr[p];
+    const float b1c = a.hp.beta1, b2c = a.hp.beta2, eps = a.hp.adam_eps;
+    const float vscale = a.hp.value_loss_coef * 0.5f / (float)(mb * K);
+    const float ascale = -1.f / (float)mb;
+    const float vstat = 0.5f / (float)(mb * K), astat = 1.f / (float)mb;
+    float st_v = 0.f, st_a = 0.f, st_e = 0.f;
+    double b1p = pow((double)b1c, (double)step0), b2p = pow((double)b2c, (double)step0);
+    auto& Wt = S.Pm;
+    const int fb = 16 * w;  // this wave's feature block
+    PGM_STAMP_DECL
+
+    for (int gp = 0; gp < npass; ++gp) {
+        const int cur = gp & 1, par = gp & 1;
+        const unsigned tag = (unsigned)(gp + 1);
+        const float* rb = &S.RB[cur][0];
+        auto rt = [&](int ti) { return rb + ti * 16 * RSL; };
+        // ================================================================ tiles
+        // ---- layer 1: Z1[s][fb + c] over the inputs (A = X rows, B = W1t, shared by the tiles)
+        f32x4 z[R][NC], H1[R];
+#pragma unroll
+        for (int ti = 0; ti < R; ++ti)
+#pragma unroll
+            for (int q = 0; q < NC; ++q) z[ti][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KS1; ++ks) {
+            const int k = 4 * ks + g;
+            const bool kv = k < O;
+            const float bw = kv ? Wt.W1t[kv ? k : 0][fb + c] : 0.f;
+#pragma unroll
+            for (int ti = 0; ti < R; ++ti) {
+                const float av = kv ? rt(ti)[c * RSL + (kv ? k : 0)] : 0.f;
+                z[ti][ks % NC] = mfma16(av, bw, z[ti][ks % NC]);
+            }
+        }
+        {
+            const float bias = Wt.b1[fb + c];
+#pragma unroll
+            for (int ti = 0; ti < R; ++ti) {
+                f32x4 zz = z[ti][0];
+                if constexpr (NC == 2) zz += z[ti][1];
+                tanh_bias_pk<4>(zz, bias, H1[ti]);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) S.H1s[16 * ti + 4 * g + r][fb + c] = H1[ti][r];
+            }
+        }
+        PGM_STAMP(0);
+        lds_sync_m();  // B1: H1 of every feature block
+        // ---- layer 2: Z2[s][fb + c] = H1[s][:] . W2t[:][fb + c]
+        f32x4 H2[R];
+#pragma unroll
+        for (int ti = 0; ti < R; ++ti)
+#pragma unroll
+            for (int q = 0; q < NC; ++q) z[ti][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < H / 4; ++ks) {
+            const int k = 4 * ks + g;
+            const float bw = Wt.W2t[k][fb + c];
+#pragma unroll
+            for (int ti = 0; ti < R; ++ti) z[ti][ks % NC] = mfma16(S.H1s[16 * ti + c][k], bw, z[ti][ks % NC]);
+        }
+        {
+            const float bias = Wt.b2[fb + c];
+#pragma unroll
+            for (int ti = 0; ti < R; ++ti) {
+                f32x4 zz = z[ti][0];
+                if constexpr (NC == 2) zz += z[ti][1];
+                tanh_bias_pk<4>(zz, bias, H2[ti]);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) S.H2s[16 * ti + 4 * g + r][fb + c] = H2[ti][r];
+            }
+        }
+        PGM_STAMP(1);
+        lds_sync_m();  // B2: H2 of every feature block
+        // ---- heads on the MFMA: out[s][q] = H2[s][:] . Wh[q][:] (q = lane column < Q), then the per-(sample,
+        // output) loss gradients dO in C layout (ppo.py:80-96)
+        const bool qv = c < Q;
+        float bh_[H / 4];
+#pragma unroll
+        for (int ks = 0; ks < H / 4; ++ks) bh_[ks] = qv ? Wt.Wh[qv ? c : 0][4 * ks + g] : 0.f;
+        const float bhb = qv ? Wt.bh[c] : 0.f;
+        float gbh = 0.f, gls = 0.f, lsum = 0.f;
+        f32x4 dOr[HSPLIT ? 1 : R];
+#pragma unroll
+        for (int hi = 0; hi < NHT; ++hi) {
+            const int ti = HSPLIT ? w + 4 * hi : hi;
+            const float* rr = rt(ti);
+            f32x4 ho[NC];
+#pragma unroll
+            for (int q = 0; q < NC; ++q) ho[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ks = 0; ks < H / 4; ++ks)
+                ho[ks % NC] = mfma16(S.H2s[16 * ti + c][4 * ks + g], bh_[ks], ho[ks % NC]);
+            if constexpr (NC == 2) ho[0] += ho[1];
+            f32x4 dO;
+            if (m == 0) {  // value loss over the K objectives
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int s = 4 * g + r;
+                    const bool ok = c < K;
+                    const float V = ho[0][r] + bhb;
+                    const float Vold = rr[s * RSL + O + A + 2 + (c < K ? c : 0)];
+                    const float Rt = rr[s * RSL + O + A + 2 + K + (c < K ? c : 0)];
+                    float gv, ls;
+                    if (a.hp.use_clipped_value_loss) {
+                        const float dv = V - Vold;
+                        const float vc = Vold + fminf(fmaxf(dv, -clip), clip);
+                        const float l1 = (V - Rt) * (V - Rt), l2 = (vc - Rt) * (vc - Rt);
+                        const float inr = (dv >= -clip && dv <= clip) ? 1.f : 0.f;
+                        gv = wmax2(l1, l2) * 2.f * (V - Rt) + wmax2(l2, l1) * 2.f * (vc - Rt) * inr;
+                        ls = fmaxf(l1, l2);
+                    } else {
+                        gv = 2.f * (V - Rt);
+                        ls = (Rt - V) * (Rt - V);
+                    }
+                    dO[r] = ok ? vscale * gv : 0.f;
+                    lsum += ok ? ls : 0.f;
+                }
+            } else {  // clipped surrogate; a sample's log-prob is a 16-lane row sum over its outputs
+                const bool av_ = c < A;
+                const float aiv = S.aiv[av_ ? c : 0], ls_c = av_ ? Wt.logstd[av_ ? c : 0] : 0.f;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int s = 4 * g + r;
+                    const float diff = av_ ? rr[s * RSL + O + (av_ ? c : 0)] - (ho[0][r] + bhb) : 0.f;
+                    const float lpe = av_ ? -0.5f * diff * diff * aiv - ls_c - LOG_SQRT_2PI : 0.f;
+                    const float lp = row_sum16(lpe);
+                    const float ratio = expf(lp - rr[s * RSL + O + A]);
+                    const float ad = rr[s * RSL + O + A + 1];
+                    const float s1 = ratio * ad;
+                    const float s2 = fminf(fmaxf(ratio, 1.f - clip), 1.f + clip) * ad;
+                    const float inr = (ratio >= 1.f - clip && ratio <= 1.f + clip) ? 1.f : 0.f;
+                    const float gr = ad * (wmin2(s1, s2) + wmin2(s2, s1) * inr);
+                    const float dlp = ascale * gr * ratio;
+                    lsum += c == 0 ? -fminf(s1, s2) : 0.f;
+                    dO[r] = av_ ? dlp * diff * aiv : 0.f;
+                    gls += av_ ? dlp * (diff * diff * aiv - 1.f) : 0.f;
+                }
+            }
+            float* dt = &S.dOs[HSPLIT ? 0 : w][0][0];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                gbh += dO[r];
+                if (c < DQ) dt[(16 * ti + 4 * g + r) * DQS + c] = dO[r];
+            }
+            if constexpr (!HSPLIT) dOr[hi] = dO;
+        }
+        gbh = group4_sum(gbh);
+        gls = group4_sum(gls);
+        lsum = wave_sum64(lsum);
+        if constexpr (HSPLIT) {  // partial head sums of this wave's row tiles: summed in wave order after B3
+            if (g == 0) {
+                S.red[16 * w + c] = gbh;
+                S.red[64 + 16 * w + c] = gls;
+            }
+        }
+        if (t == 64 * w) S.red[128 + w] = lsum;  // wave partials (row-split heads) / identical copies (else)
+        PGM_STAMP(2);
+        if constexpr (HSPLIT || Sm::ZA) lds_sync_m();  // B2b: dO tiles of every wave / H2 reads done before dZ2
+        else wave_lds_fence();
+        // ---- head-weight gradient gWh^T[u][q] += H2^T dO, dH2 = dO . Wh -> dZ2 (this wave's units)
+        f32x4 gWh = f32x4{0.f, 0.f, 0.f, 0.f}, gW2[4], gW1[K1B];
+        float gB1 = 0.f, gB2 = 0.f;
+#pragma unroll
+        for (int ib = 0; ib < 4; ++ib) gW2[ib] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kb = 0; kb < K1B; ++kb) gW1[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const float* dtl = &S.dOs[HSPLIT ? 0 : w][0][0];
+        float (*Zt)[S16] = Sm::ZA ? S.H2s : S.Zs;
+        f32x4 dZ2[R];
+#pragma unroll
+        for (int ti = 0; ti < R; ++ti) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float bo = HSPLIT ? (qv ? dtl[(16 * ti + 4 * g + r) * DQS + (qv ? c : 0)] : 0.f) : dOr[HSPLIT ? 0 : ti][r];
+                gWh = mfma16(H2[ti][r], bo, gWh);
+            }
+            f32x4 zz = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ks = 0; ks < (Q + 3) / 4; ++ks) {
+                const int q = 4 * ks + g;
+                const bool qq = q < Q;
+                const float av = qq ? dtl[(16 * ti + c) * DQS + (qq ? q : 0)] : 0.f;
+                zz = mfma16(av, qq ? Wt.Wh[qq ? q : 0][fb + c] : 0.f, zz);
+            }
+            dtanh_pk<4>(zz, H2[ti], dZ2[ti]);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                gB2 += dZ2[ti][r];
+                Zt[16 * ti + 4 * g + r][fb + c] = dZ2[ti][r];
+            }
+            // dW2^T[in][fb + c] += H1^T dZ2 (A = H1 of every feature block in C layout from its tile)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int ib = 0; ib < 4; ++ib)
+                    gW2[ib] = mfma16(S.H1s[16 * ti + 4 * g + r][16 * ib + c], dZ2[ti][r], gW2[ib]);
+        }
+        PGM_STAMP(3);
+        lds_sync_m();  // B3: dZ2 of every feature block
+        // ---- dH1 = dZ2 W2 for this wave's input block, dZ1, dW1^T[k][fb + c] += X^T dZ1
+#pragma unroll
+        for (int ti = 0; ti < R; ++ti)
+#pragma unroll
+            for (int q = 0; q < NC; ++q) z[ti][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < H / 4; ++ks) {
+            const int o = 4 * ks + g;
+            const float bw = Wt.W2t[fb + c][o];
+#pragma unroll
+            for (int ti = 0; ti < R; ++ti) z[ti][ks % NC] = mfma16(Zt[16 * ti + c][o], bw, z[ti][ks % NC]);
+        }
+#pragma unroll
+        for (int ti = 0; ti < R; ++ti) {
+            f32x4 zz = z[ti][0], dZ1;
+            if constexpr (NC == 2) zz += z[ti][1];
+            dtanh_pk<4>(zz, H1[ti], dZ1);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                gB1 += dZ1[r];
+#pragma unroll
+                for (int kb = 0; kb < K1B; ++kb) {
+                    const int k = 16 * kb + c;
+                    const float ax = k < O ? rt(ti)[(4 * g + r) * RSL + (k < O ? k : 0)] : 0.f;
+                    gW1[kb] = mfma16(ax, dZ1[r], gW1[kb]);
+                }
+            }
+        }
+        gB1 = group4_sum(gB1);
+        gB2 = group4_sum(gB2);
+        PGM_STAMP(4);
+
+        // ================================================================ exchange
+        // ---- 1. publish this wave's gradient blocks (its feature block of every tensor)
+        dbg_delay(a.dbg, gp, 0);
+        {
+            float vb2 = 0.f, vls = 0.f;
+            if (w == 0) {
+                if constexpr (HSPLIT) {  // the waves' head partial sums (written before B3), in wave order
+                    vb2 = ((S.red[c] + S.red[16 + c]) + S.red[32 + c]) + S.red[48 + c];
+                    vls = ((S.red[64 + c] + S.red[80 + c]) + S.red[96 + c]) + S.red[112 + c];
+                } else {
+                    vb2 = gbh;
+                    vls = gls;
+                }
+                // -entropy_coef * d(mean entropy)/d logstd enters once per tower (ppo.py:98): part 0
+                if (hs == 0) vls -= a.hp.entropy_coef;
+            }
+            const f32x4 vec = g == 0 ? f32x4{gB1, gB2, c < NQ ? vb2 : 0.f, m == 1 && c < A ? vls : 0.f}
+                                     : f32x4{0.f, 0.f, 0.f, 0.f};
+            const int base = islot(hs, par) + (w * BPW * 64 + l) * 16;
+            auto st = [&](int k, const f32x4& v) {
+                const u32x4 u = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
+                                 __float_as_uint(v[3])};
+                __builtin_amdgcn_raw_buffer_store_b128(u, xr, base + k * 1024, 0, SC1);
+            };
+#pragma unroll
+            for (int kb = 0; kb < K1B; ++kb) st(kb, gW1[kb]);
+#pragma unroll
+            for (int ib = 0; ib < 4; ++ib) st(K1B + ib, gW2[ib]);
+            st(K1B + 4, gWh);
+            st(K1B + 5, vec);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
+        lds_sync_m();
+        PGM_STAMP(5);
+        float lsum_wg = 0.f;
+        if constexpr (HSPLIT) lsum_wg = ((S.red[128] + S.red[129]) + S.red[130]) + S.red[131];
+        else lsum_wg = S.red[128];
+        if (t == 0)
+            __hip_atomic_store(gran(0, m, hs, par), ((unsigned long long)tag << 32) | __float_as_uint(lsum_wg),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // spin on a tagged granule (bounded; a timeout marks the launch failed and every later poll skips)
+        auto spin = [&](const unsigned long long* gr) -> unsigned long long {
+            if (__hip_atomic_load(fail_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return 0ull;
+            for (unsigned spins = 0;; ++spins) {
+                const unsigned long long x = __hip_atomic_load(gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((unsigned)(x >> 32) == tag) return x;
+                if (spins > (1u << 26)) {
+                    __hip_atomic_store(fail_word, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    return 0ull;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        };
+        if (w == 0) {
+            if (l < NS) {  // lane h polls part h's image flag (the NS - 1 polls run concurrently)
+                dbg_delay(a.dbg, gp, 1);
+                S.red[l] = l == hs ? lsum_wg : __uint_as_float((unsigned)spin(gran(0, m, l, par)));
+            }
+        } else {  // the next minibatch's rows (and the one after's indices) while wave 0 polls
+            if (gp + 1 < npass) issue_rows((gp + 1) & 1, (gp + 1) & 1, w - 1, 3);
+            if (gp + 2 < npass) issue_idx(gp + 2, gp & 1, w - 1, 3);
+        }
+        lds_sync_m();
+        float lsum_all = 0.f;
+#pragma unroll
+        for (int h = 0; h < NS; ++h) lsum_all += S.red[h];  // part order
+        PGM_STAMP(6);
+        // ---- 2. reduce-scatter: this part's blocks summed over the NS parts in part order, squared norm
+        f32x4 gr_[OWV];
+        float sq = 0.f;
+#pragma unroll
+        for (int i = 0; i < OWV; ++i) {
+            const int b = hs + NS * (w + 4 * i);
+            gr_[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (b < NB) {
+                u32x4 pl[NS];
+#pragma unroll
+                for (int h = 0; h < NS; ++h)
+                    pl[h] = __builtin_amdgcn_raw_buffer_load_b128(xr, islot(h, par) + (b * 64 + l) * 16, 0, SC1);
+#pragma unroll
+                for (int h = 0; h < NS; ++h) {
+                    const f32x4 v = f32x4{__uint_as_float(pl[h][0]), __uint_as_float(pl[h][1]),
+                                          __uint_as_float(pl[h][2]), __uint_as_float(pl[h][3])};
+                    gr_[i] = h == 0 ? v : gr_[i] + v;
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) sq = fmaf(gr_[i][r], gr_[i][r], sq);
+            }
+        }
+        sq = wave_sum64(sq);
+        if (l == 0) S.red[32 + w] = sq;
+        lds_sync_m();
+        const float sq_wg = ((S.red[32] + S.red[33]) + S.red[34]) + S.red[35];
+        PGM_STAMP(7);
+        // ---- 3. squared norms of both towers' parts: one granule each, summed in (tower, part) order
+        if (t == 0)
+            __hip_atomic_store(gran(1, m, hs, par), ((unsigned long long)tag << 32) | __float_as_uint(sq_wg),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // this step's Adam scalars (fp64 bias corrections) while the granules travel
+        const double b1n = b1p * (double)b1c, b2n = b2p * (double)b2c;
+        float step_size = (float)(lr / (1.0 - b1n));
+        float inv_bc2s = 1.f / (float)sqrt(1.0 - b2n);
+        asm volatile("" : "+v"(step_size), "+v"(inv_bc2s));
+        if (w == 0 && l < 2 * NS) {
+            dbg_delay(a.dbg, gp, 2);
+            const int mm = l / NS, hh = l - mm * NS;
+            S.red[64 + l] = mm == m && hh == hs ? sq_wg : __uint_as_float((unsigned)spin(gran(1, mm, hh, par)));
+        }
+        lds_sync_m();
+        float total = 0.f;
+#pragma unroll
+        for (int i = 0; i < 2 * NS; ++i) total += S.red[64 + i];
+        const float coef = clip_coef(a.hp.max_grad_norm, total);
+        if (t == 0) {
+            if (m == 0) st_v += lsum_all * vstat;
+            else st_a += lsum_all * astat;
+            float ent = 0.f;
+#pragma unroll
+            for (int q = 0; q < A; ++q) ent += 0.5f + LOG_SQRT_2PI + Wt.logstd[q];
+            st_e += ent;
+        }
+        b1p = b1n;
+        b2p = b2n;
+        PGM_STAMP(8);
+        // ---- 4. Adam on the owned blocks (registers), publish them, write them into this part's image
+        dbg_delay(a.dbg, gp, 3);
+#pragma unroll
+        for (int i = 0; i < OWV; ++i) {
+            const int b = hs + NS * (w + 4 * i);
+            if (b < NB) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float gc = gr_[i][r] * coef;
+                    om[i][r] = om[i][r] + (1.f - b1c) * (gc - om[i][r]);
+                    ov[i][r] = ov[i][r] * b2c + (1.f - b2c) * (gc * gc);
+                    const float den = __builtin_amdgcn_sqrtf(ov[i][r]) * inv_bc2s + eps;
+                    op[i][r] -= step_size * om[i][r] * __builtin_amdgcn_rcpf(den);
+                }
+                const u32x4 u = {__float_as_uint(op[i][0]), __float_as_uint(op[i][1]), __float_as_uint(op[i][2]),
+                                 __float_as_uint(op[i][3])};
+                __builtin_amdgcn_raw_buffer_store_b128(u, xr, pslot(hs, par) + ((w + 4 * i) * 64 + l) * 16, 0, SC1);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int ii = frag_img<O, A, K>(b, l, r, m);
+                    if (ii >= 0) Pf[ii] = op[i][r];
+                }
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        lds_sync_m();
+        if (t == 0)
+            __hip_atomic_store(gran(2, m, hs, par), (unsigned long long)tag << 32, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        if (w == 0 && l < NS && l != hs) spin(gran(2, m, l, par));
+        lds_sync_m();
+        PGM_STAMP(9);
+        // ---- the other parts' new parameter blocks into the image (block b: wave b mod 4)
+        {
+            constexpr int GPW = NB / 4;  // blocks per wave (NB is a multiple of 4)
+            u32x4 pv[GPW];
+#pragma unroll
+            for (int k = 0; k < GPW; ++k) {
+                const int b = w + 4 * k, h = b % NS, jj = b / NS;
+                if (h != hs) pv[k] = __builtin_amdgcn_raw_buffer_load_b128(xr, pslot(h, par) + (jj * 64 + l) * 16, 0, SC1);
+            }
+#pragma unroll
+            for (int k = 0; k < GPW; ++k) {
+                const int b = w + 4 * k;
+                if (b % NS != hs) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int ii = frag_img<O, A, K>(b, l, r, m);
+                        if (ii >= 0) Pf[ii] = __uint_as_float(pv[k][r]);
+                    }
+                }
+            }
+        }
+        dma_sync_m();  // image complete; this wave's row DMA retired (the barrier: every wave's)
+        if (m == 1 && t < A) S.aiv[t] = expf(-2.f * Wt.logstd[t]);  // read after the next step's B2
+        PGM_STAMP(10);
+    }
+    PGM_STAMP_FLUSH;
+    // ---- owners write their blocks' parameters and moments back; statistics and the step by part 0
+#pragma unroll
+    for (int i = 0; i < OWV; ++i) {
+        const int b = hs + NS * (w + 4 * i);
+        if (b < NB) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int ii = frag_img<O, A, K>(b, l, r, m);
+                const int f = ii >= 0 ? img_to_flat<O, A, K>(ii, m, L) : -1;
+                if (f >= 0) {
+                    P[f] = op[i][r];
+                    Mo[f] = om[i][r];
+                    Vo[f] = ov[i][r];
+                }
+            }
+        }
+    }
+    if (hs == 0 && t == 0) {
+        const float n = (float)(E * M);
+        if (m == 0) a.stats[p * 3 + 0] = st_v / n;
+        if (m == 1) {
+            a.step[p] = step0 + npass;
+            a.stats[p * 3 + 1] = st_a / n;
+            a.stats[p * 3 + 2] = st_e / n;
+        }
+    }
+}
+
+template <int O, int A, int K, int NS, int R>
+static int launch_fs_k(const pgm_dims* d, const MArgs& a, hipStream_t stream) {
+    const size_t smem = fs_smem_bytes<O, A, K, R>();
+    if (smem > 160 * 1024) {
+        set_error("pgm_ppo_update (fs): LDS %zu bytes exceeds 160 KiB", smem);
+        return PGM_E_UNSUPPORTED;
+    }
+    auto kern = ppo_update_fs_kernel<O, A, K, NS, R>;
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update (fs)");
+    const int grid = fs_grid(d->P, NS);
+    if (int rc = check_coresident((const void*)kern, 256, smem, grid, "pgm_ppo_update (fs)")) return rc;
+    const size_t zb = ppo_flag_bytes(d->P);  // norm / flag granules (the payload needs no reset: tags order it)
+    if (!ws_take_zeroed(a.ws, zb)) {
+        e = hipMemsetAsync(a.ws, 0, zb, stream);
+        if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update (workspace reset)");
+    }
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), smem, stream, a);
+    return launch_status("pgm_ppo_update (fs)");
+}
+
+// NS parts per tower for this launch: the workspace cap, the device's CUs, mb divisible into 16-row tiles of at most
+// 8 per part; 0 = the feature-split update does not apply
+int fs_choose_ns(const pgm_dims* d, int mb) {
+    if (d->O > 32) return 0;
+    const int cus = device_cu_count();
+    for (int ns = fs_ns_cap(d->P); ns >= 2; ns >>= 1) {
+        if (fs_grid(d->P, ns) > cus || mb % (16 * ns) != 0) continue;
+        const int R = mb / (16 * ns);
+        if (R >= 1 && R <= 8 && (R & (R - 1)) == 0) return ns;
+    }
+    return 0;
+}
+
+template <int O, int A, int K, int NS>
+static int launch_fs_ns(const pgm_dims* d, const MArgs& a, int R, hipStream_t stream) {
+    // minibatches of 64 / 128 / 256 / 512 rows (N = 1 / 2 / 4 / 8 at T = 2048, M = 32): 16 NS R = mb
+    auto one = [&](auto rc) -> int {
+        constexpr int RR = decltype(rc)::value, MB = 16 * NS * RR;
+        if constexpr (MB == 64 || MB == 128 || MB == 256 || MB == 512) return launch_fs_k<O, A, K, NS, RR>(d, a, stream);
+        set_error("pgm_ppo_update (fs): minibatch of %d rows unsupported", MB);
+        return PGM_E_UNSUPPORTED;
+    };
+    switch (R) {
+        case 1: return one(ic<1>{});
+        case 2: return one(ic<2>{});
+        case 4: return one(ic<4>{});
+        case 8: return one(ic<8>{});
+    }
+    set_error("pgm_ppo_update (fs): %d row tiles per part unsupported", R);
+    return PGM_E_UNSUPPORTED;
+}
+
+// called by pgm_ppo_mfma.hip's launcher after the sample table is packed
+int ppo_update_fs(const pgm_dims* d, const MArgs& a, int ns, hipStream_t stream) {
+    const int mb = d->T * d->N / a.hp.num_mini_batch;
+    const int R = mb / (16 * ns);
+    return dispatch_dims(d->O, d->A, d->K, "pgm_ppo_update (fs)", [&](auto o, auto aa, auto k) -> int {
+        constexpr int O = decltype(o)::value, A = decltype(aa)::value, K = decltype(k)::value;
+        if constexpr (O > 32) {
+            return PGM_E_UNSUPPORTED;
+        } else {
+            switch (ns) {
+                case 2: return launch_fs_ns<O, A, K, 2>(d, a, R, stream);
+                case 4: return launch_fs_ns<O, A, K, 4>(d, a, R, stream);
+                case 8: return launch_fs_ns<O, A, K, 8>(d, a, R, stream);
+                case 16: return launch_fs_ns<O, A, K, 16>(d, a, R, stream);
+            }
+            set_error("pgm_ppo_update (fs): NS=%d unsupported", ns);
+            return PGM_E_UNSUPPORTED;
+        }
+    });
+}
+
+}  // namespace pgm

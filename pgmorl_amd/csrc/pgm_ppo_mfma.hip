@@ -29,7 +29,7 @@
 #include <stdlib.h>
 
 #include "pgm_dispatch.hpp"
-#include "pgm_mfma.hpp"
+#include "pgm_ppo_shared.hpp"
 
 PGM_STAMP_UNIT(mfma)
 
@@ -88,15 +88,6 @@ __device__ __forceinline__ void lds_add(float* p, float v) {
 #endif
 }
 
-// clip_grad_norm_'s coefficient min(max_norm / (sqrt(sum of squares) + 1e-6), 1) (torch nn/utils/clip_grad.py):
-// hardware sqrt and a Newton-refined reciprocal (<= 1 ulp) instead of the IEEE expansions, off the critical path's
-// division sequences
-__device__ __forceinline__ float clip_coef(float max_norm, float sumsq) {
-    const float d = __builtin_amdgcn_sqrtf(sumsq) + 1e-6f;
-    float r = __builtin_amdgcn_rcpf(d);
-    r = fmaf(fmaf(-d, r, 1.f), r, r);
-    return fminf(max_norm * r, 1.f);
-}
 
 // ---------------------------------------------------------------- packed sample table
 struct PackArgs {
@@ -131,44 +122,6 @@ __global__ __launch_bounds__(256) void pack_rows_kernel(PackArgs a) {
     *reinterpret_cast<float4*>(a.rows + (size_t)row * RS + k0) = v;
 }
 
-// ---------------------------------------------------------------- tower images
-// One tower's parameters as an LDS image: W1^T [in][out], W2^T [in][out] with a padded row stride,
-// head weights [output][unit], biases, logstd (actor only).  Padding slots and head rows beyond the
-// tower's output count hold zeros for the whole launch (their gradient, Adam moments and update are 0).
-// The same image type holds gradients and (SPLIT) the Adam moments, so clip_grad_norm_ and Adam are
-// flat passes over images, and the working copy IS the master copy until the launch writes it back.
-template <int O, int A, int K>
-struct TowerImg {
-    static constexpr int Q = qmax<A, K>();
-    float W1t[O][H];
-    float W2t[H][SCR];
-    float Wh[Q][H];
-    float b1[H], b2[H], bh[Q], logstd[A];
-};
-template <int O, int A, int K>
-constexpr int img_floats() { return (int)(sizeof(TowerImg<O, A, K>) / sizeof(float)); }
-
-// image slot -> flat parameter index (pgm_param_layout order), -1 for padding / unused slots
-template <int O, int A, int K>
-__device__ __forceinline__ int img_to_flat(int i, int m, const Layout& L) {
-    constexpr int Q = qmax<A, K>();
-    constexpr int s1 = O * H, s2 = s1 + H * SCR, s3 = s2 + Q * H, s4 = s3 + H, s5 = s4 + H, s6 = s5 + Q, s7 = s6 + A;
-    const int NQ = m == 0 ? K : A;
-    if (i < s1) return L.off[m ? PGM_P_ACTOR_W1 : PGM_P_CRITIC_W1] + i;
-    if (i < s2) {
-        const int j = i - s1, in = j / SCR, o = j - in * SCR;
-        return o < H ? L.off[m ? PGM_P_ACTOR_W2 : PGM_P_CRITIC_W2] + in * H + o : -1;
-    }
-    if (i < s3) {  // reference head weight [NQ][H] stored transposed [H][NQ]
-        const int j = i - s2, q = j / H, u = j - q * H;
-        return q < NQ ? L.off[m ? PGM_P_MEAN_W : PGM_P_VALUE_W] + u * NQ + q : -1;
-    }
-    if (i < s4) return L.off[m ? PGM_P_ACTOR_B1 : PGM_P_CRITIC_B1] + (i - s3);
-    if (i < s5) return L.off[m ? PGM_P_ACTOR_B2 : PGM_P_CRITIC_B2] + (i - s4);
-    if (i < s6) return (i - s5) < NQ ? L.off[m ? PGM_P_MEAN_B : PGM_P_VALUE_B] + (i - s5) : -1;
-    if (i < s7) return m ? L.off[PGM_P_LOGSTD] + (i - s6) : -1;
-    return -1;
-}
 
 template <int O, int A, int K, bool SPLIT, int NBUF>
 struct MSmemT {
@@ -197,23 +150,6 @@ constexpr int nbuf() { return sizeof(MSmemT<O, A, K, SPLIT, 2>) <= 160 * 1024 ? 
 template <int O, int A, int K, bool SPLIT>
 using MSmem = MSmemT<O, A, K, SPLIT, nbuf<O, A, K, SPLIT>()>;
 
-struct MArgs {
-    int N, T;
-    Layout L;
-    pgm_ppo_hparams hp;
-    float *params, *m, *v;
-    int32_t* step;
-    const float* lr;
-    const int32_t* perms;
-    const float* rows;       // packed sample table [P][T*N][RS]
-    float* stats;
-    unsigned long long* ws;  // SPLIT: tagged norm granules + timeout flag (word 2P), zeroed before the launch
-    unsigned long long* xb;  // MODE 2: gradient-image exchange slots, zeroed before the launch
-    int xslot;               // 8-byte words per exchange slot (image payload, flag granule in the last word)
-    int xbytes;              // bytes of the exchange buffer
-    int P;
-    DbgDelay dbg;            // test-only exchange delay (PGM_TEST_DELAY; cycles 0 = off)
-};
 
 
 // MODE 0: one workgroup per task (joint towers).  MODE 1 (SPLIT): one workgroup per tower.  MODE 2: each tower
@@ -858,7 +794,7 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
                     if (half == 1) {
 #if PGM_HEADS_MFMA
                         if (l == 0 || l == 16) {  // lane 16 gq holds the sums of outputs 4 gq .. 4 gq + 3
-                            const float ec = add ? 0.f : a.hp.entropy_coef;
+                            const float ec = add || hs != 0 ? 0.f : a.hp.entropy_coef;  // once per tower: row part 0
 #pragma unroll
                             for (int r = 0; r < 4; ++r) {
                                 const int q = 4 * (l >> 4) + r;
@@ -870,7 +806,7 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
 #else
                         if (h == 0 && c < NQ) acc(oBh + c, gsm);
                         if (m == 1 && h == 1 && c < A) {  // -entropy_coef * d(mean entropy)/d logstd enters once (ppo.py:98)
-                            const float ec = add ? 0.f : a.hp.entropy_coef;
+                            const float ec = add || hs != 0 ? 0.f : a.hp.entropy_coef;  // once per tower: row part 0
                             acc(oLs + c, gsm - ec);
                         }
 #endif
@@ -1250,10 +1186,6 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
 // images of a tower are exchanged through 16-B sc1 publishes + tagged flags (every workgroup sums them in
 // row-part order h = 0..NS-1, so all NS copies of the Adam step are bitwise identical), the two towers
 // exchange their squared norms as tagged 8-byte granules, and Adam runs from registers.
-constexpr int T16 = 16;       // samples per tile
-constexpr int S16 = H + 2;    // transpose-tile row stride: conflict-free A-operand reads, 2-way (free) writes
-constexpr int DQ = 8;         // head-output columns of the dO transpose tile (Q <= 8)
-constexpr int DQS = DQ + 1;
 
 
 template <int O, int A, int K, int W, int NBUF, int NIMG_>
@@ -1714,7 +1646,7 @@ PGM_UNROLL(ONE ? PGM_U16 : 4)
                             put4([&](int r) { return c < Q ? oWh + c * H + ub * T16 + 4 * g + r : -1; }, gWh[ub]);
                     if constexpr (BV % NSL == SL) {  // vectors: lanes of group 0 (every group holds the sums)
                         // -entropy_coef * d(mean entropy)/d logstd enters once (ppo.py:98)
-                        const float lsv = m == 1 ? gls - (add ? 0.f : a.hp.entropy_coef) : 0.f;
+                        const float lsv = m == 1 ? gls - (add || hs != 0 ? 0.f : a.hp.entropy_coef) : 0.f;  // once per tower: part 0
                         put4([&](int r) { return g == 0 ? oB1 + r * T16 + c : -1; }, f32x4{gB1[0], gB1[1], gB1[2], gB1[3]});
                         put4([&](int r) { return g == 0 ? oB2 + r * T16 + c : -1; }, f32x4{gB2[0], gB2[1], gB2[2], gB2[3]});
                         put4([&](int r) { return g == 0 && r == 0 && c < Q ? oBh + c : g == 0 && r == 1 && c < A ? oLs + c : -1; },
@@ -2132,6 +2064,9 @@ int launch_mode(const pgm_dims* d, const MArgs& a, hipStream_t stream) {
     return launch_mode_k<O, A, K, MODE, false>(d, a, stream);
 }
 
+int fs_choose_ns(const pgm_dims* d, int mb);
+int ppo_update_fs(const pgm_dims* d, const MArgs& a, int ns, hipStream_t stream);
+
 template <int O, int A, int K>
 int launch_ppo_update_mfma(const pgm_dims* d, const MArgs& a, const pgm_rollout_buf* rb, hipStream_t stream) {
     // packed sample table, then the update
@@ -2151,6 +2086,13 @@ int launch_ppo_update_mfma(const pgm_dims* d, const MArgs& a, const pgm_rollout_
     // (4 CUs per task, while mode2_grid(P) <= CUs), 1 = one workgroup per tower (2P <= CUs), 0 = one
     // workgroup per task; each falls back to the next one down when its grid does not fit.
     static_assert(sizeof(MSmem<O, A, K, true>) > 80 * 1024, "split residency argument needs > 80 KiB LDS");
+    // feature-split update with the reduce-scattered Adam (pgm_ppo_fs.hip): PGM_UPDATE_KERNEL=fs selects it
+    if (const char* k = getenv("PGM_UPDATE_KERNEL")) {
+        if (k[0] == 'f' && k[1] == 's') {
+            const int ns = fs_choose_ns(d, d->T * d->N / a.hp.num_mini_batch);
+            if (ns > 0) return ppo_update_fs(d, a, ns, stream);
+        }
+    }
     const char* sel = getenv("PGM_UPDATE_SPLIT");
     const int cap = sel && sel[0] >= '0' && sel[0] <= '4' ? sel[0] - '0' : 4;
     const int cus = device_cus();
@@ -2172,7 +2114,8 @@ int ppo_update_mfma(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params,
     MArgs a{d->N, d->T, make_layout(d->O, d->A, d->K, d->H), *hp, params, adam_m, adam_v, adam_step, lr, perms,
             (const float*)(ws + ppo_flag_bytes(d->P) + ppo_xbuf_bytes(d)), stats, (unsigned long long*)ws,
             (unsigned long long*)(ws + ppo_flag_bytes(d->P)), ppo_xslot(d->O, d->A, d->K), (int)ppo_xbuf_bytes(d),
-            d->P, dbg_delay_from_env()};
+            d->P, dbg_delay_from_env(),
+            ws + ppo_flag_bytes(d->P) + ppo_xbuf_bytes(d) + (size_t)d->P * d->T * d->N * ppo_row_stride(d->O, d->A, d->K) * sizeof(float)};
     return dispatch_dims(d->O, d->A, d->K, "pgm_ppo_update", [&](auto o, auto aa, auto k) -> int {
         constexpr int O = decltype(o)::value, A = decltype(aa)::value, K = decltype(k)::value;
         if constexpr (O > 32) {

@@ -9,6 +9,7 @@ workgroup for a fixed number of cycles at one hand-off point of one step:
   where 2 -- between its tower-norm granule store and its poll: the other tower can finish this step and
              publish the NEXT step's norm before the delayed poll looks -- the order a single-buffered granule
              lost (the poll would see the next tag and spin until the timeout word).
+  where 3 -- (feature-split update only) before its Adam step and parameter publish.
 Each case must leave the exchange-timeout word clear (check_update) and the parameters equal to the oracle's.
 """
 import numpy as np
@@ -26,7 +27,10 @@ DELAY = 4_000_000  # shader cycles (~2 ms): far beyond one Adam step, far below 
 
 
 def _run_update(env, P, T, N, E, M, split, delay, monkeypatch):
-    monkeypatch.setenv('PGM_UPDATE_SPLIT', split)
+    if split == 'fs':
+        monkeypatch.setenv('PGM_UPDATE_KERNEL', 'fs')
+    else:
+        monkeypatch.setenv('PGM_UPDATE_SPLIT', split)
     if delay is not None:
         monkeypatch.setenv('PGM_TEST_DELAY', ':'.join(str(x) for x in delay))
     args, spec, tb, pols, data, perms = _update_setup(env, P, T, N, E, M, seed=17)
@@ -52,26 +56,56 @@ def _run_update(env, P, T, N, E, M, split, delay, monkeypatch):
         assert int(tb.adam_step[p]) == E * M
 
 
-# block ids: MODE 2 (split '2') groups 16 blocks per 4 tasks, block r = half r >> 3 of tower r & 1 of task
-# 4 g + ((r & 7) >> 1); t16 (split '4') groups 32, part r >> 3.  Blocks 0 / 1: task 0's critic / actor, part 0;
-# 8 / 9: part 1; 25: actor part 3 (t16 only).
-CASES = [('2', 0, 0), ('2', 9, 0), ('2', 8, 1), ('2', 1, 1), ('2', 0, 2), ('2', 9, 2),
-         ('4', 0, 0), ('4', 25, 0), ('4', 17, 1), ('4', 0, 2), ('4', 1, 2), ('4', 24, 2)]
+def block_of(kernel, task, tower, part, ns=4):
+    """blockIdx.x of (task, tower 0 = critic / 1 = actor, row part) under the HEAD block maps: every workgroup of a
+    task on blocks b, b + 8, ... (one XCD) -- MODE 2 (pgm_ppo_mfma.hip ppo_update_mfma_kernel, PGM_MODE2_XCD4): groups
+    of 32 blocks per 8 tasks, block r = half (r >> 4) & 1 of tower (r >> 3) & 1 of task 8 G + (r & 7); t16 (NS = 4)
+    and the feature-split kernel (pgm_ppo_fs.hip, NS parts): groups of 16 NS blocks per 8 tasks, block r = part
+    ((r >> 3) % 2 NS) >> 1 of tower (r >> 3) & 1 of task 8 G + (r & 7)."""
+    if kernel == '2':
+        return 32 * (task // 8) + 16 * part + 8 * tower + (task & 7)
+    return 16 * ns * (task // 8) + 8 * (2 * part + tower) + (task & 7)
 
 
-@pytest.mark.parametrize('split,block,where', CASES)
-def test_delayed_handoff_keeps_parity(gpu, split, block, where, monkeypatch):
-    # Walker, 2 tasks, mb = 256 (the single-tile specialisations of both kernels), 4 Adam steps; the stall
-    # hits step 1 (both parities are exercised before and after it)
+def test_block_of_inverts_the_kernel_maps():
+    for kernel, ns in (('2', 2), ('4', 4), ('fs', 16), ('fs', 2)):
+        seen = set()
+        for task in range(11):
+            for tower in (0, 1):
+                for part in range(ns):
+                    b = block_of(kernel, task, tower, part, ns)
+                    if kernel == '2':
+                        got = (8 * (b >> 5) + (b & 7), (b >> 3) & 1, (b >> 4) & 1)
+                    else:
+                        j = (b >> 3) % (2 * ns)
+                        got = (8 * (b // (16 * ns)) + (b & 7), j & 1, j >> 1)
+                    assert got == (task, tower, part) and b not in seen
+                    seen.add(b)
+
+
+# (kernel, task, tower, part, where): stall that workgroup at that hand-off; fs: NS = 16 parts for 2 Walker tasks,
+# where 3 = before its Adam / parameter publish
+CASES = [('2', 0, 0, 0, 0), ('2', 0, 1, 1, 0), ('2', 0, 0, 1, 1), ('2', 0, 1, 0, 1), ('2', 0, 0, 0, 2), ('2', 0, 1, 1, 2),
+         ('4', 0, 0, 0, 0), ('4', 0, 1, 3, 0), ('4', 0, 1, 2, 1), ('4', 0, 0, 0, 2), ('4', 0, 1, 0, 2), ('4', 0, 0, 3, 2),
+         ('fs', 0, 0, 0, 0), ('fs', 1, 1, 15, 0), ('fs', 0, 1, 7, 1), ('fs', 1, 0, 3, 2), ('fs', 0, 1, 0, 2),
+         ('fs', 1, 1, 9, 3), ('fs', 0, 0, 15, 3)]
+
+
+@pytest.mark.parametrize('split,task,tower,part,where', CASES)
+def test_delayed_handoff_keeps_parity(gpu, split, task, tower, part, where, monkeypatch):
+    # Walker, 2 tasks, mb = 256 (the single-tile specialisations of MODE 2 / t16; fs: 16 parts of one 16-row tile),
+    # 4 Adam steps; the stall hits step 1 (both parities are exercised before and after it)
+    block = block_of(split, task, tower, part, 16 if split == 'fs' else 4)
     _run_update('MO-Walker2d-v2', 2, 256, 4, 1, 4, split, (1, block, where, DELAY), monkeypatch)
 
 
-@pytest.mark.parametrize('split', ['2', '4'])
+@pytest.mark.parametrize('split', ['2', '4', 'fs'])
 def test_delay_on_last_step_and_ragged_grid(gpu, split, monkeypatch):
-    # Hopper-v3 (3 objectives), 5 tasks (a ragged last group of the block map), multi-pass minibatches
-    # (mb = 128 with N = 2: not the single-tile path); stall the last task's actor part 0 on the last step
+    # Hopper-v3 (3 objectives), 5 tasks (a partial group of 8 tasks in the block map), multi-pass minibatches for
+    # MODE 2 / t16 (mb = 128 with N = 2: not the single-tile path; fs: 8 parts of one tile); stall the last task's
+    # actor part 0 on the last step
     P = 5
-    block = (16 if split == '2' else 32) * (P // 4) + 2 * (P % 4 - 1) + 1
+    block = block_of(split, P - 1, 1, 0, 8 if split == 'fs' else 4)
     _run_update('MO-Hopper-v3', P, 128, 2, 1, 2, split, (1, block, 2, DELAY), monkeypatch)
 
 

@@ -115,21 +115,30 @@ def test_adam_state_roundtrip():
                                        ('MO-Humanoid-v2', 20, 8, 2048), ('MO-Humanoid-v2', 3, 8, 64)])
 def test_update_workspace_covers_every_split(env, P, N, T):
     """pgm_ppo_update_workspace_bytes covers the largest row split a launch may pick (PGM_NS_MAX = 4 parts per
-    tower): tagged norm granules (2 towers x 4 parts x 2 step parities x P + 1, 256-B padded), exchange slots [P][2 towers][4 parts][2
-    parities], and the packed sample table (obs_dim <= 32) or the parts' private parameter rows (wide)."""
+    tower): tagged granules (the row-split updates' norm granules, 2 towers x 4 parts x 2 step parities x P + 1, then
+    from granule 16 P + 8 the feature-split update's [3 kinds][P][2 towers][<= 16 parts][2 parities]; 256-B padded),
+    exchange slots [P][2 towers][4 parts][2 parities], and the packed sample table + the feature-split payload
+    (obs_dim <= 32: [P][2][NS][2] image slots of NB KiB and parameter slots of ceil(NB / NS) KiB, NS the largest
+    power of two <= 16 with 16 NS ceil(P / 8) <= 256, NB = 4 (ceil(O / 16) + 6)) or the parts' private parameter
+    rows (wide)."""
     from pgmorl_amd import envspec
     spec = envspec.make_spec(env)
     O, A, K, H = spec['obs_dim'], spec['act_dim'], spec['obj_num'], 64
     Q = max(A, K)
     d = _lib.Dims(P, N, T, O, A, K, H)
     got = _lib.lib().pgm_ppo_update_workspace_bytes(d)
-    flags = -(-(2 * 4 * 2 * P + 1) * 8 // 256) * 256
+    flags = -(-(16 * P + 8 + 3 * P * 2 * 16 * 2) * 8 // 256) * 256
     if O <= 32:
         img = O * H + H * (H + 1) + Q * H + 2 * H + Q + A
         xslot = -(-(img + 1) // 32) * 32
         n = O + A + 2 + 2 * K
         rs = 16 if n <= 16 else 32 if n <= 32 else 64 if n <= 64 else 128
-        want = flags + P * 2 * 4 * 2 * xslot * 8 + P * T * N * rs * 4
+        ns = 16
+        while ns > 1 and 16 * ns * -(-P // 8) > 256:
+            ns //= 2
+        nb = 4 * (-(-O // 16) + 6)
+        fs = P * 2 * ns * 2 * (nb + -(-nb // ns)) * 1024 if ns >= 2 else 0
+        want = flags + P * 2 * 4 * 2 * xslot * 8 + P * T * N * rs * 4 + fs
     else:
         img = H * (H + 1) + Q * H + 2 * H + Q + A
         nkt = -(-O // 32)

@@ -182,7 +182,7 @@ def cpu_baseline(args, spec, tasks):
 def hv_comparison(env_name):
     """The newest committed full-algorithm device-vs-oracle HV comparison at an equal budget for this env
     (scripts/hv_full.py: warm-up + prediction-guided generations on both sides, per seed), summarised."""
-    key = {'MO-Walker2d-v2': 'walker', 'MO-Hopper-v2': 'hopper'}.get(env_name)
+    key = {'MO-Walker2d-v2': 'walker', 'MO-Hopper-v2': 'hopper', 'MO-Hopper-v3': 'hopper3'}.get(env_name)
     if key is None:
         return None
     import re

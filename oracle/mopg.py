@@ -13,6 +13,7 @@ The MuJoCo envs are replaced by the synthetic env of oracle/vecenv.py; multiproc
 fan-out is replaced by a plain loop over tasks (tasks never interact inside a generation).
 """
 import copy
+import os
 import time
 
 import numpy as np
@@ -23,6 +24,20 @@ from .ppo import PPO, RolloutStorage, linear_lr
 from .vecenv import RunningMeanStd, SynthEnv, VecNormalizedSynth
 
 F64 = torch.float64
+# Precision arm of scripts/hv_full.py (PGM_ORACLE_NET_DTYPE=float32): the policy, its PPO losses / backward / Adam in
+# fp32 (the device's arithmetic), the envs, running statistics and returns still fp64.  Default: the fp64 reference.
+NET = torch.float32 if os.environ.get('PGM_ORACLE_NET_DTYPE') == 'float32' else F64
+
+
+def _to_net_dtype(policy, agent):
+    """Cast a sample's policy and Adam state to NET in place (no-op for fp64)."""
+    if NET == F64:
+        return
+    policy.to(NET)
+    for st in agent.optimizer.state.values():
+        for k in ('exp_avg', 'exp_avg_sq'):
+            if k in st:
+                st[k] = st[k].to(NET)
 
 
 class OracleSample:
@@ -63,7 +78,8 @@ def evaluation(args, spec, s0_eval, policy, ob_rms):
             while not done:
                 if args.ob_rms:
                     ob = np.clip((ob - ob_rms.mean) / np.sqrt(ob_rms.var + 1e-8), -10.0, 10.0)
-                _, action, _ = policy.act(torch.tensor(ob, dtype=F64).unsqueeze(0), deterministic=True)
+                _, action, _ = policy.act(torch.tensor(ob, dtype=next(policy.parameters()).dtype).unsqueeze(0),
+                                          deterministic=True)
                 ob, _, done, info = env.step(action[0].numpy())
                 objs += gamma * info['obj']
                 if not args.raw:
@@ -81,6 +97,7 @@ def mopg_worker(args, spec, s0_train, s0_eval, sample, weights, iteration, num_u
     """
     sample = OracleSample.copy_from(sample)  # Task deep-copies its elite (morl/task.py:9-10)
     policy, agent = sample.actor_critic, sample.agent
+    _to_net_dtype(policy, agent)
     T, N = args.num_steps, args.num_processes
     envs = VecNormalizedSynth(spec, s0_train, args.gamma, args.ob_rms, args.obj_rms)
     for key in ('ob_rms', 'ret_rms', 'obj_rms'):
@@ -97,14 +114,14 @@ def mopg_worker(args, spec, s0_train, s0_eval, sample, weights, iteration, num_u
             agent.set_lr(linear_lr(j, total, args.lr, args.lr_decay_ratio))
         for t in range(T):
             with torch.no_grad():
-                value, action, logp = policy.act(ro.obs[t], noise=None if noise is None else noise[t])
+                value, action, logp = policy.act(ro.obs[t].to(NET), noise=None if noise is None else noise[t])
             obs, dones, infos = envs.step(action.numpy())
             obj = torch.tensor(np.stack([i['obj'] for i in infos]), dtype=F64)
             masks = torch.tensor([[0.0] if d else [1.0] for d in dones], dtype=F64)
             bad = torch.tensor([[0.0] if 'bad_transition' in i else [1.0] for i in infos], dtype=F64)
             ro.insert(torch.from_numpy(obs).to(F64), action, logp, value, obj, masks, bad)
         with torch.no_grad():
-            next_value = policy.get_value(ro.obs[-1])
+            next_value = policy.get_value(ro.obs[-1].to(NET))
         ro.compute_returns(next_value, args.use_gae, args.gamma, args.gae_lambda, args.use_proper_time_limits)
         obj_var = envs.obj_rms.var if envs.obj_rms is not None else None
         if record is not None:

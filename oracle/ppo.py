@@ -121,6 +121,9 @@ class PPO:
 
     def minibatch_step(self, obs, act, vp, ret, old_lp, adv):
         """One clipped-PPO Adam step (ppo.py:76-103). Returns (value_loss, action_loss, entropy)."""
+        dt = next(self.actor_critic.parameters()).dtype  # fp64; fp32 in the precision arm (oracle/mopg.py NET)
+        if dt != F64:
+            obs, act, vp, ret, old_lp, adv = (x.to(dt) for x in (obs, act, vp, ret, old_lp, adv))
         values, logp, entropy = self.actor_critic.evaluate_actions(obs, act)
         ratio = torch.exp(logp - old_lp)
         surr1 = ratio * adv

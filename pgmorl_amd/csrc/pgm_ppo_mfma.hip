@@ -794,7 +794,7 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
                     if (half == 1) {
 #if PGM_HEADS_MFMA
                         if (l == 0 || l == 16) {  // lane 16 gq holds the sums of outputs 4 gq .. 4 gq + 3
-                            const float ec = add || hs != 0 ? 0.f : a.hp.entropy_coef;  // once per tower: row part 0
+                            const float ec = add || hs != 0 || (w >> 1) != 0 ? 0.f : a.hp.entropy_coef;  // once per tower: part 0, image 0
 #pragma unroll
                             for (int r = 0; r < 4; ++r) {
                                 const int q = 4 * (l >> 4) + r;
@@ -806,7 +806,7 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
 #else
                         if (h == 0 && c < NQ) acc(oBh + c, gsm);
                         if (m == 1 && h == 1 && c < A) {  // -entropy_coef * d(mean entropy)/d logstd enters once (ppo.py:98)
-                            const float ec = add || hs != 0 ? 0.f : a.hp.entropy_coef;  // once per tower: row part 0
+                            const float ec = add || hs != 0 || (w >> 1) != 0 ? 0.f : a.hp.entropy_coef;  // once per tower: part 0, image 0
                             acc(oLs + c, gsm - ec);
                         }
 #endif
@@ -1646,7 +1646,7 @@ PGM_UNROLL(ONE ? PGM_U16 : 4)
                             put4([&](int r) { return c < Q ? oWh + c * H + ub * T16 + 4 * g + r : -1; }, gWh[ub]);
                     if constexpr (BV % NSL == SL) {  // vectors: lanes of group 0 (every group holds the sums)
                         // -entropy_coef * d(mean entropy)/d logstd enters once (ppo.py:98)
-                        const float lsv = m == 1 ? gls - (add || hs != 0 ? 0.f : a.hp.entropy_coef) : 0.f;  // once per tower: part 0
+                        const float lsv = m == 1 ? gls - (add || hs != 0 || w >= WPI ? 0.f : a.hp.entropy_coef) : 0.f;  // once per tower: part 0, image A
                         put4([&](int r) { return g == 0 ? oB1 + r * T16 + c : -1; }, f32x4{gB1[0], gB1[1], gB1[2], gB1[3]});
                         put4([&](int r) { return g == 0 ? oB2 + r * T16 + c : -1; }, f32x4{gB2[0], gB2[1], gB2[2], gB2[3]});
                         put4([&](int r) { return g == 0 && r == 0 && c < Q ? oBh + c : g == 0 && r == 1 && c < A ? oLs + c : -1; },

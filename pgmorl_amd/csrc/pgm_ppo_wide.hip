@@ -563,7 +563,7 @@ PGM_UNROLL_W(PGM_UW_L2)
                     if (half == 1) {
                         if (h == 0 && c < NQ) acc(oBh + c, gsm);
                         if (m == 1 && h == 1 && c < A) {  // -entropy_coef * d(mean entropy)/d logstd enters once (ppo.py:98)
-                            const float ec = add || hs != 0 ? 0.f : a.hp.entropy_coef;  // once per tower: row part 0
+                            const float ec = add || hs != 0 || (w >> 1) != 0 ? 0.f : a.hp.entropy_coef;  // once per tower: part 0, image 0
                             acc(oLs + c, gsm - ec);
                         }
                         if (!add) {  // padding slots of a freshly written image

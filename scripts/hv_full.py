@@ -8,7 +8,9 @@ only the MOPG back end differs: MOPGPopulation on the GPU (rng='host') or Oracle
 task with the fp64 oracle MOPG_worker restatement in a process pool (one process per task, like
 morl/morl.py:84-88).  Side 'oracle32' is the noise floor: the same fp64 oracle with each offspring's
 parameters and Adam moments rounded to fp32 at the generation boundary (the device's storage precision),
-compared against the plain oracle with --ref like the device side.  Each side picks its own elites from its own offspring, so the comparison is on the
+compared against the plain oracle with --ref like the device side.  Side 'oracle_f32' is the precision arm: the
+oracle with its policy, PPO losses, backward and Adam in fp32 (PGM_ORACLE_NET_DTYPE=float32, oracle/mopg.py NET),
+envs / statistics / returns fp64 as on the device.  Each side picks its own elites from its own offspring, so the comparison is on the
 budget-level quantities (HV of the final EP vs the origin, EP size, train env-steps), as
 scripts/plot/ep_batch_visualize_2d.py:23-45 reports them.
 
@@ -39,6 +41,9 @@ from pgmorl_amd.sample import DeviceSnapshot, RunningMeanStd, Sample  # noqa: E4
 CONFIGS = {  # pop and the reference's per-env flags (scripts/*.py), iterations scaled to fit the budget
     'MO-Hopper-v2': dict(delta='0.25', tasks=5, N=1, warmup=10, update=5, gens=3, extra=[]),
     'MO-Walker2d-v2': dict(delta=str(1.0 / 39.0), tasks=40, N=4, warmup=4, update=3, gens=3, extra=[]),
+    # scripts/hopper-v3.py: 3 objectives, delta 0.25 (15 warm-up tasks), pbuffer-num 20, sparsity 1e6
+    'MO-Hopper-v3': dict(delta='0.25', tasks=15, N=4, warmup=4, update=3, gens=3,
+                         extra=['--pbuffer-num', '20', '--sparsity', '1000000.0']),
 }
 
 
@@ -190,13 +195,15 @@ def run_side(side, env, seed, procs):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument('side', choices=['oracle', 'oracle32', 'device'])
+    ap.add_argument('side', choices=['oracle', 'oracle32', 'oracle_f32', 'device'])
     ap.add_argument('--env', default='MO-Hopper-v2', choices=sorted(CONFIGS))
     ap.add_argument('--seeds', type=int, nargs='+', default=[0])
     ap.add_argument('--procs', type=int, default=7)
     ap.add_argument('--ref', help='oracle JSON (device side)')
     ap.add_argument('--out', required=True)
     a = ap.parse_args()
+    if a.side == 'oracle_f32':  # before anything imports oracle.mopg (the pool workers fork from this process)
+        os.environ['PGM_ORACLE_NET_DTYPE'] = 'float32'
     if a.ref:
         ref = json.load(open(a.ref))
         env, seeds = ref['env'], [r['seed'] for r in ref['runs']]

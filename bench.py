@@ -73,24 +73,6 @@ def parse():
     return ap.parse_args()
 
 
-def update_kernel_name(obs_dim, P):
-    """The pgm_ppo_update variant the launcher selects (pgm_ppo_mfma.hip launch_ppo_update_mfma and
-    pgm_ppo_wide.hip): 16-row tiles on 8 CUs per task while their grid (64 blocks per group of 8 tasks) fits the
-    CUs, else MODE 2 (4 CUs per task, 32 blocks per group of 8 tasks); PGM_UPDATE_SPLIT caps it."""
-    if obs_dim > 32:
-        return 'ppo_update_wide_kernel'
-    cus = torch.cuda.get_device_properties(0).multi_processor_count
-    cap = os.environ.get('PGM_UPDATE_SPLIT', '4')[:1]
-    cap = int(cap) if cap.isdigit() and int(cap) <= 4 else 4
-    groups8 = (P + 7) // 8  # mode2_grid / t16_grid in pgm_ppo_mfma.hip
-    if cap >= 4 and 64 * groups8 <= cus:
-        return 'ppo_update_t16_kernel (NS=4, W=4)'
-    if cap == 3 and 32 * groups8 <= cus:
-        return 'ppo_update_t16_kernel (NS=2, W=8)'
-    mode = 2 if cap >= 2 and 32 * groups8 <= cus else 1 if cap >= 1 and 2 * P <= cus else 0
-    return f'ppo_update_mfma_kernel (MODE {mode})'
-
-
 def mflops_per_row(O, A, K, H=64):
     """M_f = 2(O*H + H^2) + H*A + H*K multiply-adds per row forward."""
     return 2 * (O * H + H * H) + H * A + H * K
@@ -434,7 +416,7 @@ def leg_gpu(args, spec, dev, rank, world, blocks, tag):
         tb.check_update()  # a timed-out exchange invalidates the run: raises PGMError (after the timed region)
     upd_ms = float(np.mean([s.elapsed_time(e) for s, e in ev])) if ev else 0.0
     dt, upd_ms = allreduce_max([dt, upd_ms], dev)  # the slowest rank defines the step
-    kernel = update_kernel_name(spec['obs_dim'], P) if P > 0 else None
+    kernel = tb.update_variant() if tb is not None else None  # the launcher's own choice (pgm_ppo_update_variant)
     del tb
     torch.cuda.empty_cache()
     return {'dt': dt, 'upd_ms': upd_ms, 'P': P, 'history': history, 'kernel': kernel, 'tag': tag}

@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define PGM_ABI_VERSION 2
+#define PGM_ABI_VERSION 3
 
 #define PGM_OK 0
 #define PGM_E_INVALID_ARG (-1)
@@ -177,18 +177,27 @@ int pgm_adv_normalize(const pgm_dims* d, const pgm_rollout_buf* rb, const double
  * workspace: caller-owned device bytes (pgm_ppo_update_workspace_bytes), required (PGM_E_INVALID_ARG
  * when NULL), reset inside the call on `stream` unless pgm_ppo_update_reset did it since the last call.
  * The critic and actor towers of a task run on separate CUs that exchange the squared gradient norm per
- * minibatch step; each tower is further split over four CUs (a quarter of the minibatch rows each, gradient
+ * minibatch step.  obs_dim <= 32 and small per-GPU populations (>= 4 parts per tower fit: 16 NS ceil(P/8) <= CUs,
+ * minibatch rows a multiple of 16 NS): each tower on NS = 16 / 8 / 4 CUs that split the minibatch rows, the four
+ * waves of a CU split the hidden features, and the gradient is reduce-scattered over the parts before Adam (the
+ * feature-split update).  Otherwise each tower is split over four CUs (a quarter of the minibatch rows each, gradient
  * images added through the workspace) while 64 * ceil(P/8) <= CU count, else over two CUs while
  * 32 * ceil(P/8) <= CU count (obs_dim > 32: 32 * ceil(P/4) / 16 * ceil(P/4)).  obs_dim <= 32: tower
  * images LDS-resident (falls back to 2 CUs per task, then 1, as P grows); obs_dim > 32 (Humanoid): layer
  * 1 streamed from L2, needs 2P <= CU count (PGM_E_UNSUPPORTED otherwise: shard the tasks over more
- * GPUs).  PGM_UPDATE_SPLIT=0/1/2/3/4 caps the split (3 = an A/B-only variant, selected only explicitly).
+ * GPUs).  PGM_UPDATE_SPLIT=0/1/2/3/4 caps the row split (3 = an A/B-only variant, selected only explicitly);
+ * PGM_UPDATE_KERNEL=fs forces the feature-split update wherever it fits, =mfma the row-split kernels.
  * After the call, the 8-byte word at index 2P of the workspace is nonzero iff an exchange timed out
  * (the workgroups were not co-resident); the results of such a call are invalid. */
 int pgm_ppo_update(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params, float* adam_m,
                    float* adam_v, int32_t* adam_step, const float* lr, const int32_t* perms,
                    const pgm_rollout_buf* rb, float* stats, void* workspace, pgm_stream_t stream);
 size_t pgm_ppo_update_workspace_bytes(const pgm_dims* d);
+/* The update kernel pgm_ppo_update would launch for these dims and hyper-parameters on the current device (same
+ * selection rule, including the PGM_UPDATE_KERNEL / PGM_UPDATE_SPLIT / PGM_FS_HOPS overrides), as text into buf[n]
+ * (e.g. "ppo_update_fs_kernel (NS=16, R=1, 2 hops)"): what benchmarks and profiles report.  No reference
+ * counterpart (diagnostic). */
+int pgm_ppo_update_variant(const pgm_dims* d, const pgm_ppo_hparams* hp, char* buf, int n);
 /* Zero, on `stream`, the part of the workspace the next pgm_ppo_update for dims d would reset inside the call,
  * and let that call skip its own reset (the caller orders this stream before the update's stream and after
  * every read of the previous update's timeout word).  Lets a caller take the reset off the update's stream. */

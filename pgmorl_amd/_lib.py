@@ -12,7 +12,7 @@ import torch  # noqa: F401  (must precede loading libpgm.so)
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('PGM_LIB') or os.path.join(HERE, 'libpgm.so')
 
-PGM_ABI_VERSION = 2
+PGM_ABI_VERSION = 3
 PGM_OK, PGM_E_INVALID_ARG, PGM_E_SHAPE, PGM_E_HIP, PGM_E_UNSUPPORTED = 0, -1, -2, -3, -4
 PARAM_TENSORS = ['actor_w1', 'actor_b1', 'actor_w2', 'actor_b2', 'critic_w1', 'critic_b1', 'critic_w2',
                  'critic_b2', 'value_w', 'value_b', 'mean_w', 'mean_b', 'logstd']
@@ -69,6 +69,7 @@ _SIGS = {
     'pgm_ppo_update': (C.c_int, [C.POINTER(Dims), C.POINTER(PPOHParams), P_, P_, P_, P_, P_, P_,
                                  C.POINTER(RolloutBuf), P_, P_, P_]),
     'pgm_ppo_update_workspace_bytes': (C.c_size_t, [C.POINTER(Dims)]),
+    'pgm_ppo_update_variant': (C.c_int, [C.POINTER(Dims), C.c_void_p, C.c_char_p, C.c_int]),
     'pgm_ppo_update_reset': (C.c_int, [C.POINTER(Dims), P_, P_]),
     'pgm_eval': (C.c_int, [C.POINTER(Dims), P_, C.POINTER(EnvSpec), P_, P_, P_, I32, I32, I32, F64, P_, P_]),
     'pgm_randperm': (C.c_int, [I32, I32, C.c_uint64, P_, P_]),

@@ -26,6 +26,7 @@
 // a2c_ppo_acktr/storage.py:118-154 (minibatch rows), a2c_ppo_acktr/model.py:75-82,
 // a2c_ppo_acktr/distributions.py:29-40 (log_probs / entropy).  torch.min/max/clamp backward
 // (ties split the gradient in half) are reproduced exactly.
+#include <stdio.h>
 #include <stdlib.h>
 
 #include "pgm_dispatch.hpp"
@@ -2067,6 +2068,48 @@ int launch_mode(const pgm_dims* d, const MArgs& a, hipStream_t stream) {
 int fs_choose_ns(const pgm_dims* d, int mb);
 int ppo_update_fs(const pgm_dims* d, const MArgs& a, int ns, hipStream_t stream);
 
+// Which obs_dim <= 32 update runs (one rule for the launcher and pgm_ppo_update_variant):
+//   * feature-split with the reduce-scattered Adam (pgm_ppo_fs.hip) while it gets >= FS_AUTO_NS parts per tower
+//     (small per-GPU populations: the latency form), or always with PGM_UPDATE_KERNEL=fs;
+//   * else the row-split kernels, PGM_UPDATE_SPLIT capping them: 4 (default) = 16-row tiles on 4 workgroups per
+//     tower (8 CUs per task, while t16_grid(P, 4) <= CUs), 3 = 16-row tiles on 2 workgroups of 8 waves (A/B only,
+//     selected only explicitly), 2 = 32-row tiles on 2 workgroups per tower (MODE 2, while mode2_grid(P) <= CUs),
+//     1 = one workgroup per tower (2P <= CUs), 0 = one per task; each falls back to the next one down.
+// PGM_UPDATE_KERNEL other than fs / auto (e.g. "mfma", the tests' row-split A/B) or any PGM_UPDATE_SPLIT keeps the
+// row-split kernels.
+constexpr int FS_AUTO_NS = 4;
+struct UpdateChoice {
+    int kind;  // 0 = MODE (mode), 1 = t16 (ns, w), 2 = feature-split (ns)
+    int ns, w, mode;
+};
+static UpdateChoice choose_update(const pgm_dims* d, int mb) {
+    const char* ksel = getenv("PGM_UPDATE_KERNEL");
+    const char* sel = getenv("PGM_UPDATE_SPLIT");
+    const bool force_fs = ksel && ksel[0] == 'f' && ksel[1] == 's';
+    const bool auto_k = !sel && (!ksel || !ksel[0] || (ksel[0] == 'a' && ksel[1] == 'u'));
+    const int fs_ns = fs_choose_ns(d, mb);
+    if (fs_ns > 0 && (force_fs || (auto_k && fs_ns >= FS_AUTO_NS))) return {2, fs_ns, 4, 0};
+    const int cap = sel && sel[0] >= '0' && sel[0] <= '4' ? sel[0] - '0' : 4;
+    const int cus = device_cu_count();
+    if (cap >= 4 && t16_grid(d->P, 4) <= cus) return {1, 4, 4, 0};
+    if (cap == 3 && t16_grid(d->P, 2) <= cus) return {1, 2, 8, 0};
+    if (cap >= 2 && mode2_grid(d->P) <= cus) return {0, 2, 4, 2};
+    if (cap >= 1 && 2 * d->P <= cus) return {0, 1, 4, 1};
+    return {0, 1, 4, 0};
+}
+
+int describe_update_mfma(const pgm_dims* d, const pgm_ppo_hparams* hp, char* buf, int n) {
+    const int mb = d->T * d->N / hp->num_mini_batch;
+    const UpdateChoice c = choose_update(d, mb);
+    if (c.kind == 2) {
+        const char* hv = getenv("PGM_FS_HOPS");
+        return snprintf(buf, n, "ppo_update_fs_kernel (NS=%d, R=%d, %d hops)", c.ns, mb / (16 * c.ns),
+                        hv && hv[0] == '3' ? 3 : 2);
+    }
+    if (c.kind == 1) return snprintf(buf, n, "ppo_update_t16_kernel (NS=%d, W=%d)", c.ns, c.w);
+    return snprintf(buf, n, "ppo_update_mfma_kernel (MODE %d)", c.mode);
+}
+
 template <int O, int A, int K>
 int launch_ppo_update_mfma(const pgm_dims* d, const MArgs& a, const pgm_rollout_buf* rb, hipStream_t stream) {
     // packed sample table, then the update
@@ -2079,27 +2122,13 @@ int launch_ppo_update_mfma(const pgm_dims* d, const MArgs& a, const pgm_rollout_
     hipLaunchKernelGGL(pack, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, stream, pa);
     if (int rc = launch_status("pgm_ppo_update (pack rows)")) return rc;
     // every workgroup of a split launch must be resident at once: one per CU (LDS > 80 KiB, 512 registers
-    // per lane), so the grid must fit the CU count.  PGM_UPDATE_SPLIT selects: 4 (default) = 16-row tiles
-    // on 4 workgroups per tower (8 CUs per task, while t16_grid(P, 4) <= CUs; Walker P = 20: 6.4 ms vs
-    // MODE 2's 7.1 ms), 3 = 16-row tiles on 2 workgroups of 8 waves per tower (A/B only: it spills and is
-    // slower than MODE 2, so only an explicit 3 selects it), 2 = 32-row tiles on 2 workgroups per tower
-    // (4 CUs per task, while mode2_grid(P) <= CUs), 1 = one workgroup per tower (2P <= CUs), 0 = one
-    // workgroup per task; each falls back to the next one down when its grid does not fit.
+    // per lane), so the grid must fit the CU count (choose_update)
     static_assert(sizeof(MSmem<O, A, K, true>) > 80 * 1024, "split residency argument needs > 80 KiB LDS");
-    // feature-split update with the reduce-scattered Adam (pgm_ppo_fs.hip): PGM_UPDATE_KERNEL=fs selects it
-    if (const char* k = getenv("PGM_UPDATE_KERNEL")) {
-        if (k[0] == 'f' && k[1] == 's') {
-            const int ns = fs_choose_ns(d, d->T * d->N / a.hp.num_mini_batch);
-            if (ns > 0) return ppo_update_fs(d, a, ns, stream);
-        }
-    }
-    const char* sel = getenv("PGM_UPDATE_SPLIT");
-    const int cap = sel && sel[0] >= '0' && sel[0] <= '4' ? sel[0] - '0' : 4;
-    const int cus = device_cus();
-    if (cap >= 4 && t16_grid(d->P, 4) <= cus) return launch_t16<O, A, K, 4, 4>(d, a, stream);
-    if (cap == 3 && t16_grid(d->P, 2) <= cus) return launch_t16<O, A, K, 2, 8>(d, a, stream);
-    if (cap >= 2 && mode2_grid(d->P) <= cus) return launch_mode<O, A, K, 2>(d, a, stream);
-    if (cap >= 1 && 2 * d->P <= cus) return launch_mode<O, A, K, 1>(d, a, stream);
+    const UpdateChoice c = choose_update(d, d->T * d->N / a.hp.num_mini_batch);
+    if (c.kind == 2) return ppo_update_fs(d, a, c.ns, stream);
+    if (c.kind == 1) return c.ns == 4 ? launch_t16<O, A, K, 4, 4>(d, a, stream) : launch_t16<O, A, K, 2, 8>(d, a, stream);
+    if (c.mode == 2) return launch_mode<O, A, K, 2>(d, a, stream);
+    if (c.mode == 1) return launch_mode<O, A, K, 1>(d, a, stream);
     return launch_mode<O, A, K, 0>(d, a, stream);
 }
 

@@ -12,6 +12,7 @@
 //   clip_grad_norm_ (coef = max/(norm+1e-6), clamp 1)   torch.nn.utils.clip_grad
 //   Adam (lerp m, v*b2 + (1-b2) g^2, bias-corrected step, eps outside sqrt)   torch.optim.adam
 // torch.min / torch.max / clamp backward (ties split the gradient in half) are reproduced exactly.
+#include <stdio.h>
 #include <stdlib.h>
 
 #include <mutex>
@@ -521,6 +522,22 @@ int ppo_update_wide(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params,
 using namespace pgm;
 
 extern "C" size_t pgm_ppo_update_workspace_bytes(const pgm_dims* d) { return d ? ppo_workspace_bytes(d) : 0; }
+
+namespace pgm {
+int describe_update_mfma(const pgm_dims* d, const pgm_ppo_hparams* hp, char* buf, int n);
+int describe_update_wide(const pgm_dims* d, char* buf, int n);
+}
+extern "C" int pgm_ppo_update_variant(const pgm_dims* d, const pgm_ppo_hparams* hp, char* buf, int n) {
+    if (int rc = check_dims(d, "pgm_ppo_update_variant")) return rc;
+    if (!hp || !buf || n <= 0 || hp->num_mini_batch <= 0) {
+        set_error("pgm_ppo_update_variant: null pointer or empty buffer");
+        return PGM_E_INVALID_ARG;
+    }
+    const char* sel = getenv("PGM_UPDATE_KERNEL");
+    if (sel && sel[0] == 'v') return snprintf(buf, n, "ppo_update_kernel (VALU, A/B)") > 0 ? PGM_OK : PGM_E_INVALID_ARG;
+    if (d->O <= 32) return describe_update_mfma(d, hp, buf, n) > 0 ? PGM_OK : PGM_E_INVALID_ARG;
+    return describe_update_wide(d, buf, n) > 0 ? PGM_OK : PGM_E_INVALID_ARG;
+}
 
 // workspaces zeroed ahead of their next launch by pgm_ppo_update_reset: pointer -> zeroed bytes
 static std::mutex g_zeroed_mu;

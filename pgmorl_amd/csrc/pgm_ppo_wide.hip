@@ -24,6 +24,7 @@
 // sums, clips and updates only its slice of dW1 and hands the new weights to the others, which write them
 // into their own parameter copy (parts 1..NS-1 keep private parameter rows in the workspace, so no part
 // reads layer-1 weights another is rewriting; part 0 works on the caller's row).
+#include <stdio.h>
 #include <stdlib.h>
 
 #include "pgm_dispatch.hpp"
@@ -898,6 +899,17 @@ PGM_UNROLL_W(PGM_UW_L2)
 
 }  // namespace
 
+static int wide_choose_ns(const pgm_dims* d) {
+    const char* sel = getenv("PGM_UPDATE_SPLIT");
+    const int cap = sel && sel[0] >= '0' && sel[0] <= '4' ? sel[0] - '0' : 4;
+    const int cus = device_cu_count();
+    return cap >= 4 && wide_grid(d->P, 4) <= cus ? 4 : cap >= 2 && wide_grid(d->P, 2) <= cus ? 2 : 1;
+}
+
+int describe_update_wide(const pgm_dims* d, char* buf, int n) {
+    return snprintf(buf, n, "ppo_update_wide_kernel (NS=%d)", wide_choose_ns(d));
+}
+
 int ppo_update_wide(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params, float* adam_m, float* adam_v,
                     int32_t* adam_step, const float* lr, const int32_t* perms, const pgm_rollout_buf* rb, float* stats,
                     void* workspace, hipStream_t stream) {
@@ -907,10 +919,8 @@ int ppo_update_wide(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params,
     }
     // NS = 4 (each tower on four CUs) while the 32-block groups fit the CU count, else NS = 2 while the
     // 16-block groups do, else 1; PGM_UPDATE_SPLIT caps it (0/1: one workgroup per tower, 2: at most two)
-    const char* sel = getenv("PGM_UPDATE_SPLIT");
-    const int cap = sel && sel[0] >= '0' && sel[0] <= '4' ? sel[0] - '0' : 4;
     const int cus = device_cu_count();
-    const int ns = cap >= 4 && wide_grid(d->P, 4) <= cus ? 4 : cap >= 2 && wide_grid(d->P, 2) <= cus ? 2 : 1;
+    const int ns = wide_choose_ns(d);
     if (ns == 1 && 2 * d->P > cus) {
         set_error("pgm_ppo_update: the wide update needs 2P <= CUs (P=%d); shard the tasks over more GPUs", d->P);
         return PGM_E_UNSUPPORTED;

@@ -73,53 +73,80 @@ __device__ __forceinline__ void row_copies(float v, float (&V)[NR]) {
         if constexpr (NR > 3) V[3] = __uint_as_float(q1[1]);
     }
 }
-// acc[i & 3] += (lane i of this lane's 16-lane row of v) * w[i], i = 0..NK-1: v_fmac_f32 with a DPP row_newbcast:i
-// source operand (gfx90a+; the compiler's DPP combiner does not fold a row_newbcast mov into fmac).  The leading
-// s_nop covers the VALU-write -> DPP-read hazard on v (the asm hides the DPP read from the hazard recognizer).
+// acc[i % NA] += (lane i of this lane's 16-lane row of v) * w[i], i = 0..NK-1: v_fmac_f32 with a DPP row_newbcast:i
+// source operand (gfx90a+; the compiler's DPP combiner does not fold a row_newbcast mov into fmac).  NA = 4 (the
+// shipped kernels): ONE asm block per row, whose leading s_nop covers the VALU-write -> DPP-read hazard on v (the asm
+// hides the DPP read from the hazard recognizer; inside one block nothing can write v).  Other NA (A/B builds only):
+// one asm statement per lane, each behind its own s_nop.
 template <int I, int NK, int NA>
 __device__ __forceinline__ void fmac_one(float (&acc)[NA], float v, const float (&wv)[16]) {
     if constexpr (I < NK) {
-        if constexpr (I == 0)
-            asm("s_nop 1\n\tv_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
-                : "+v"(acc[I % NA]) : "v"(v), "v"(wv[I]), "i"(I));
-        else
-            asm("v_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
-                : "+v"(acc[I % NA]) : "v"(v), "v"(wv[I]), "i"(I));
+        asm("s_nop 1\n\tv_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+            : "+v"(acc[I % NA]) : "v"(v), "v"(wv[I]), "i"(I));
         fmac_one<I + 1, NK, NA>(acc, v, wv);
     }
 }
-// acc[i % NA] += (lane i of this lane's 16-lane row of v) * w[i], i = 0..NK-1: v_fmac_f32 with a DPP row_newbcast:i
-// source operand (gfx90a+; the compiler's DPP combiner does not fold a row_newbcast mov into fmac).  The leading
-// s_nop covers the VALU-write -> DPP-read hazard on v (the asm hides the DPP read from the hazard recognizer).
+#define PGM_FL0 "v_fmac_f32_dpp %0, %4, %5 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+#define PGM_FL1 "v_fmac_f32_dpp %1, %4, %6 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+#define PGM_FL2 "v_fmac_f32_dpp %2, %4, %7 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+#define PGM_FL3 "v_fmac_f32_dpp %3, %4, %8 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+#define PGM_FL4 "v_fmac_f32_dpp %0, %4, %9 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+#define PGM_FL5 "v_fmac_f32_dpp %1, %4, %10 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+#define PGM_FL6 "v_fmac_f32_dpp %2, %4, %11 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+#define PGM_FL7 "v_fmac_f32_dpp %3, %4, %12 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+#define PGM_FL8 "v_fmac_f32_dpp %0, %4, %13 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+#define PGM_FL9 "v_fmac_f32_dpp %1, %4, %14 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+#define PGM_FL10 "v_fmac_f32_dpp %2, %4, %15 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+#define PGM_FL11 "v_fmac_f32_dpp %3, %4, %16 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+#define PGM_FL12 "v_fmac_f32_dpp %0, %4, %17 row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+#define PGM_FL13 "v_fmac_f32_dpp %1, %4, %18 row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
+#define PGM_FL14 "v_fmac_f32_dpp %2, %4, %19 row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
+#define PGM_FL15 "v_fmac_f32_dpp %3, %4, %20 row_newbcast:15 row_mask:0xf bank_mask:0xf\n\t"
+#define PGM_FU1 PGM_FL0
+#define PGM_FU2 PGM_FU1 PGM_FL1
+#define PGM_FU3 PGM_FU2 PGM_FL2
+#define PGM_FU4 PGM_FU3 PGM_FL3
+#define PGM_FU5 PGM_FU4 PGM_FL4
+#define PGM_FU6 PGM_FU5 PGM_FL5
+#define PGM_FU7 PGM_FU6 PGM_FL6
+#define PGM_FU8 PGM_FU7 PGM_FL7
+#define PGM_FU9 PGM_FU8 PGM_FL8
+#define PGM_FU10 PGM_FU9 PGM_FL9
+#define PGM_FU11 PGM_FU10 PGM_FL10
+#define PGM_FU12 PGM_FU11 PGM_FL11
+#define PGM_FU13 PGM_FU12 PGM_FL12
+#define PGM_FU14 PGM_FU13 PGM_FL13
+#define PGM_FU15 PGM_FU14 PGM_FL14
+#define PGM_FU16 PGM_FU15 PGM_FL15
+#define PGM_FMAC_ASM(body)                                                                                       \
+    asm("s_nop 1\n\t" body                                                                                    \
+        : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3])                                                \
+        : "v"(v), "v"(wv[0]), "v"(wv[1]), "v"(wv[2]), "v"(wv[3]), "v"(wv[4]), "v"(wv[5]), "v"(wv[6]), "v"(wv[7]), \
+          "v"(wv[8]), "v"(wv[9]), "v"(wv[10]), "v"(wv[11]), "v"(wv[12]), "v"(wv[13]), "v"(wv[14]), "v"(wv[15]))
 template <int NK, int NA>
 __device__ __forceinline__ void fmac_row_bcast(float (&acc)[NA], float v, const float* w) {
     static_assert(NK >= 1 && NK <= 16, "1..16 lanes");
     float wv[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) wv[i] = i < NK ? w[i] : 0.f;
-    if constexpr (NK == 16 && NA == 4) {
-        asm("s_nop 1\n\t"
-            "v_fmac_f32_dpp %0, %4, %5 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-            "v_fmac_f32_dpp %1, %4, %6 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-            "v_fmac_f32_dpp %2, %4, %7 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-            "v_fmac_f32_dpp %3, %4, %8 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-            "v_fmac_f32_dpp %0, %4, %9 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-            "v_fmac_f32_dpp %1, %4, %10 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-            "v_fmac_f32_dpp %2, %4, %11 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-            "v_fmac_f32_dpp %3, %4, %12 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-            "v_fmac_f32_dpp %0, %4, %13 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-            "v_fmac_f32_dpp %1, %4, %14 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-            "v_fmac_f32_dpp %2, %4, %15 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-            "v_fmac_f32_dpp %3, %4, %16 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
-            "v_fmac_f32_dpp %0, %4, %17 row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
-            "v_fmac_f32_dpp %1, %4, %18 row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
-            "v_fmac_f32_dpp %2, %4, %19 row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
-            "v_fmac_f32_dpp %3, %4, %20 row_newbcast:15 row_mask:0xf bank_mask:0xf"
-            : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3])
-            : "v"(v), "v"(wv[0]), "v"(wv[1]), "v"(wv[2]), "v"(wv[3]), "v"(wv[4]), "v"(wv[5]), "v"(wv[6]), "v"(wv[7]),
-              "v"(wv[8]), "v"(wv[9]), "v"(wv[10]), "v"(wv[11]), "v"(wv[12]), "v"(wv[13]), "v"(wv[14]), "v"(wv[15]));
+    if constexpr (NA == 4) {
+        if constexpr (NK == 1) PGM_FMAC_ASM(PGM_FU1);
+        else if constexpr (NK == 2) PGM_FMAC_ASM(PGM_FU2);
+        else if constexpr (NK == 3) PGM_FMAC_ASM(PGM_FU3);
+        else if constexpr (NK == 4) PGM_FMAC_ASM(PGM_FU4);
+        else if constexpr (NK == 5) PGM_FMAC_ASM(PGM_FU5);
+        else if constexpr (NK == 6) PGM_FMAC_ASM(PGM_FU6);
+        else if constexpr (NK == 7) PGM_FMAC_ASM(PGM_FU7);
+        else if constexpr (NK == 8) PGM_FMAC_ASM(PGM_FU8);
+        else if constexpr (NK == 9) PGM_FMAC_ASM(PGM_FU9);
+        else if constexpr (NK == 10) PGM_FMAC_ASM(PGM_FU10);
+        else if constexpr (NK == 11) PGM_FMAC_ASM(PGM_FU11);
+        else if constexpr (NK == 12) PGM_FMAC_ASM(PGM_FU12);
+        else if constexpr (NK == 13) PGM_FMAC_ASM(PGM_FU13);
+        else if constexpr (NK == 14) PGM_FMAC_ASM(PGM_FU14);
+        else if constexpr (NK == 15) PGM_FMAC_ASM(PGM_FU15);
+        else PGM_FMAC_ASM(PGM_FU16);
     } else {
-        // one asm per lane (partial rows, or NA != 4: the compiler schedules them), the first behind the hazard nop
         fmac_one<0, NK, NA>(acc, v, wv);
     }
 }
@@ -427,7 +454,9 @@ __global__ __launch_bounds__(512) void rollout_lane_kernel(RolloutArgs a) {
         double d2[NN];
 #pragma unroll
         for (int n = 0; n < NN; ++n) d2[n] = (v[n] - bm) * (v[n] - bm);
-        const double sq = tree_sum(d2);  // (squared deviations summed pairwise: half the dependent adds)
+        double sq = d2[0];  // numpy's var(axis=0): the squared deviations also summed in env order
+#pragma unroll
+        for (int n = 1; n < NN; ++n) sq += d2[n];
         if (upd && active) {
             const double delta = bm - mean;
             mean = mean + delta * (double)NN * itot;

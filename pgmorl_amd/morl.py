@@ -276,11 +276,11 @@ def write_generation_record(r):
 
 class _StateDictWriter:
     """torch.save of many state_dicts with identical keys, shapes and dtypes (the EP policies), without re-pickling:
-    the first is saved by torch.save into memory with torch's own CRC-32 computation switched off
-    (torch.serialization.set_crc32_options(False): records carry CRC 0, as torch writes them in that mode); every
-    later file is that zip image with the tensor records' bytes replaced (torch.save stores them uncompressed, 64-B
-    aligned, one record per storage in state_dict order).  The first templated file is read back with
-    torch.load(weights_only=True) and compared; any mismatch falls back to torch.save for every file."""
+    the first is saved by torch.save into memory; every later file is that zip image with the tensor records' bytes
+    replaced (torch.save stores them uncompressed, 64-B aligned, one record per storage in state_dict order) and each
+    patched record's CRC-32 recomputed (zlib.crc32, local header and central directory), so every file is a valid zip
+    exactly like torch.save's.  The first templated file is read back with torch.load(weights_only=True) and
+    compared; any mismatch falls back to torch.save for every file."""
 
     def __init__(self, sd):
         import io
@@ -288,17 +288,7 @@ class _StateDictWriter:
         self.keys = list(sd)
         b = io.BytesIO()
         self.crc = True
-        try:
-            from torch.serialization import get_crc32_options, set_crc32_options
-            prev = get_crc32_options()
-            set_crc32_options(False)
-            try:
-                torch.save(sd, b)
-            finally:
-                set_crc32_options(prev)
-            self.crc = False
-        except ImportError:  # an older torch: CRC-32s patched per file
-            torch.save(sd, b)
+        torch.save(sd, b)
         self.tmpl = b.getvalue()
         self.ok = False
         try:

@@ -278,6 +278,12 @@ class TaskBatch:
                                    C.byref(self.c_rb), _ptr(self.stats), _ptr(self.update_ws), _stream()),
               'pgm_ppo_update')
 
+    def update_variant(self):
+        """The update kernel pgm_ppo_update launches for this batch (pgm_ppo_update_variant: the launcher's own rule)."""
+        buf = C.create_string_buffer(128)
+        check(lib().pgm_ppo_update_variant(C.byref(self.dims), C.byref(self.hp), buf, 128), 'pgm_ppo_update_variant')
+        return buf.value.decode()
+
     def take_update_failed(self):
         """True if any PPO update since the last call timed out in a cross-workgroup exchange (its parameters /
         Adam state are invalid); resets the sticky flag.  Synchronises with the stream (after the overlapped

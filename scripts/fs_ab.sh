@@ -1,5 +1,6 @@
 #!/bin/bash
-# GPU box: A/B of the update kernels per per-GPU load (default launcher choice vs PGM_UPDATE_KERNEL=fs).
+# GPU box: A/B of the update kernels per per-GPU load: the launcher's default, the feature-split update with 2 hops
+# (PGM_UPDATE_KERNEL=fs) and with 3 hops (PGM_FS_HOPS=3); then fs phase stamps (libpgm_stamps.so) at P = 5.
 # Usage: bash scripts/fs_ab.sh TAG
 set -o pipefail
 TAG=${1:-ab}
@@ -11,7 +12,11 @@ run() {  # name, env assignment ('' = default), bench args...
   python -c "import json;d=json.load(open('$OUT/ab_${TAG}_$n.json'));r=d['roofline'];print('$n', round(d['value']/1e6,3),'M/s', round(d['ms_per_step'],3),'ms/step', r['kernel'], round(r['avg_launch_ms'],3),'ms frac', round(r['frac'],3))"
 }
 for P in 5 10 20 40; do
-  run p${P}_def '' --scaling strong --tasks $P && run p${P}_fs PGM_UPDATE_KERNEL=fs --scaling strong --tasks $P || exit 1
+  run p${P}_def '' --scaling strong --tasks $P && run p${P}_fs2 PGM_UPDATE_KERNEL=fs --scaling strong --tasks $P && \
+  run p${P}_fs3 "PGM_UPDATE_KERNEL=fs PGM_FS_HOPS=3" --scaling strong --tasks $P || exit 1
 done
-run cheetah20_def '' --env-name MO-HalfCheetah-v2 --tasks 20 && run cheetah20_fs PGM_UPDATE_KERNEL=fs --env-name MO-HalfCheetah-v2 --tasks 20 && \
-run hopper2_p5_def '' --env-name MO-Hopper-v2 --tasks 5 --num-processes 1 && run hopper2_p5_fs PGM_UPDATE_KERNEL=fs --env-name MO-Hopper-v2 --tasks 5 --num-processes 1
+run hopper2_p5_def '' --env-name MO-Hopper-v2 --tasks 5 --num-processes 1 && run hopper2_p5_fs2 PGM_UPDATE_KERNEL=fs --env-name MO-Hopper-v2 --tasks 5 --num-processes 1 || exit 1
+for H in ${STAMP_HOPS:-}; do
+  PGM_UPDATE_KERNEL=fs PGM_FS_HOPS=$H P=5 STAMP_BLOCK=1 PGM_LIB=pgmorl_amd/libpgm_stamps.so timeout -k 10 120 python scripts/stamps.py > $OUT/stamps_${TAG}_fs${H}_p5.txt 2>&1 || { echo STAMPS FAILED; tail $OUT/stamps_${TAG}_fs${H}_p5.txt; exit 1; }
+  echo "=== fs hops $H P=5"; grep -A14 "== fs" $OUT/stamps_${TAG}_fs${H}_p5.txt
+done

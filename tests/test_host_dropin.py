@@ -105,7 +105,7 @@ def test_host_draws_and_lr_schedule():
 
 def test_templated_state_dict_files_load_like_torch_save(tmp_path):
     """write_final's _StateDictWriter: every EP_policy_*.pt after the first is the first file's zip image with the
-    tensor records (and their CRC-32s) replaced; torch.load(weights_only=True) must return each state_dict bit for
+    tensor records and their CRC-32s replaced; torch.load(weights_only=True) must return each state_dict bit for
     bit, with the reference keys, shapes and fp64 dtype."""
     from pgmorl_amd.morl import _StateDictWriter
     lay = ParamLayout(11, 3, 3)
@@ -123,6 +123,11 @@ def test_templated_state_dict_files_load_like_torch_save(tmp_path):
         assert list(got) == [k for k, _, _ in STATE_KEYS]
         for k in sd:
             assert got[k].dtype == torch.float64 and torch.equal(got[k], sd[k]), (i, k)
+        # a valid zip for any CRC-checking reader (torch.save's own records carry real CRC-32s)
+        import zipfile
+        with zipfile.ZipFile(str(tmp_path / f'p{i}.pt')) as z:
+            assert z.testzip() is None, i
+            assert all(zi.CRC != 0 for zi in z.infolist() if '/data/' in zi.filename), i
 
 
 def test_unflatten_batch_rows_equal_unflatten():

@@ -194,8 +194,8 @@ int pgm_ppo_update(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params, 
                    const pgm_rollout_buf* rb, float* stats, void* workspace, pgm_stream_t stream);
 size_t pgm_ppo_update_workspace_bytes(const pgm_dims* d);
 /* The update kernel pgm_ppo_update would launch for these dims and hyper-parameters on the current device (same
- * selection rule, including the PGM_UPDATE_KERNEL / PGM_UPDATE_SPLIT / PGM_FS_HOPS overrides), as text into buf[n]
- * (e.g. "ppo_update_fs_kernel (NS=16, R=1, 2 hops)"): what benchmarks and profiles report.  No reference
+ * selection rule, including the PGM_UPDATE_KERNEL / PGM_UPDATE_SPLIT overrides), as text into buf[n]
+ * (e.g. "ppo_update_fs_kernel (NS=16, R=1)"): what benchmarks and profiles report.  No reference
  * counterpart (diagnostic). */
 int pgm_ppo_update_variant(const pgm_dims* d, const pgm_ppo_hparams* hp, char* buf, int n);
 /* Zero, on `stream`, the part of the workspace the next pgm_ppo_update for dims d would reset inside the call,

@@ -23,7 +23,12 @@
 //      launch), publishes the new parameter blocks (sc1) + a tagged flag, and every workgroup gathers the other
 //      parts' blocks into its LDS parameter image.
 // Three cross-CU hops per Adam step, each moving ~1/NS of the image per reader instead of every partner's whole
-// image (pgm_ppo_mfma.hip's t16 / MODE 2), and Adam on 1/NS of the parameters per workgroup.
+// image (pgm_ppo_mfma.hip's t16 / MODE 2), and Adam on 1/NS of the parameters per workgroup.  The parameter gather of
+// step s is issued at its end and written into the image during step s + 1, each block just before its first reader
+// (every wave gathers its own feature block).  Measured and dropped: a two-hop form (owners publish the reduced
+// gradient, every workgroup gathers all of it and runs Adam on the whole tower) -- one hop fewer, but Adam on ~32
+// elements per thread plus the wider gather cost more than the hop (P = 5: 28.1 K vs 24.7 K cycles per Adam step,
+// profiles/r04c_fs2_stamps_p5.txt, r04c_fs3_stamps_p5.txt).
 //
 // Reference semantics (a2c_ppo_acktr/algo/ppo.py:58-115, storage.py:118-154, model.py:75-82, distributions.py:29-40)
 // as in pgm_ppo_mfma.hip, including torch.min/max/clamp tie gradients; entropy_coef enters once per tower.
@@ -111,12 +116,7 @@ constexpr size_t fs_smem_bytes() {  // > 80 KiB: one workgroup per CU (the co-re
     return sizeof(FsSmem<O, A, K, R>) > 81 * 1024 ? sizeof(FsSmem<O, A, K, R>) : 81 * 1024;
 }
 
-// HOPS 3: reduce-scatter, norm granules, sharded Adam + parameter all-gather (parameters and moments of a part's own
-// blocks in its registers).  HOPS 2: reduce-scatter, then the owners publish the REDUCED gradient blocks with their
-// squared norm in the same tagged granule, and every workgroup gathers the whole reduced gradient and runs Adam on
-// all of it (identical inputs and order in every part: bitwise-identical parameters; each thread keeps the moments
-// of its fixed elements in registers) -- one cross-CU hop fewer for ~4x the Adam work per workgroup.
-template <int O, int A, int K, int NS, int R, int HOPS>
+template <int O, int A, int K, int NS, int R>
 __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
     static_assert(O <= 32 && R >= 1 && R <= 8 && (R & (R - 1)) == 0, "fs tiles");
     using Sm = FsSmem<O, A, K, R>;
@@ -189,17 +189,16 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
         Pf[i] = f >= 0 ? P[f] : 0.f;
     }
     if (t < A) S.aiv[t] = expf(-2.f * P[L.off[PGM_P_LOGSTD] + t]);
-    // HOPS 3: parameters + moments of this part's own blocks; HOPS 2: moments of this wave's blocks b = w + 4k
-    constexpr int NMV = HOPS == 3 ? OWV : BPW;
-    f32x4 op[HOPS == 3 ? OWV : 1], om[NMV], ov[NMV];
+    // parameters + moments of this part's own blocks b = hs + NS j (block j of the part: wave j mod 4)
+    f32x4 op[OWV], om[OWV], ov[OWV];
 #pragma unroll
-    for (int i = 0; i < NMV; ++i) {
-        const int b = HOPS == 3 ? hs + NS * (w + 4 * i) : w + 4 * i;
+    for (int i = 0; i < OWV; ++i) {
+        const int b = hs + NS * (w + 4 * i);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int ii = b < NB ? frag_img<O, A, K>(b, l, r, m) : -1;
             const int f = ii >= 0 ? img_to_flat<O, A, K>(ii, m, L) : -1;
-            if constexpr (HOPS == 3) op[i][r] = f >= 0 ? P[f] : 0.f;
+            op[i][r] = f >= 0 ? P[f] : 0.f;
             om[i][r] = f >= 0 ? Mo[f] : 0.f;
             ov[i][r] = f >= 0 ? Vo[f] : 0.f;
         }
@@ -222,12 +221,33 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
     const int fb = 16 * w;  // this wave's feature block
     PGM_STAMP_DECL
 
+    // the other parts' new parameter blocks of THIS wave's feature block (b = BPW w + k), loaded at the end of a step
+    // and written into the image during the next one, each just before its first reader: W1 + vector block before
+    // layer 1, W2 before layer 2, the head block before B2 (heads read every wave's); the own part's blocks are
+    // written by their owners before the parameter hand-off
+    u32x4 pv[BPW];
+    auto put_block = [&](int k) {
+        const int b = BPW * w + k;
+        if (b % NS != hs) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int ii = frag_img<O, A, K>(b, l, r, m);
+                if (ii >= 0) Pf[ii] = __uint_as_float(pv[k][r]);
+            }
+        }
+    };
     for (int gp = 0; gp < npass; ++gp) {
         const int cur = gp & 1, par = gp & 1;
         const unsigned tag = (unsigned)(gp + 1);
         const float* rb = &S.RB[cur][0];
         auto rt = [&](int ti) { return rb + ti * 16 * RSL; };
         // ================================================================ tiles
+        if (gp > 0) {
+#pragma unroll
+            for (int k = 0; k < K1B; ++k) put_block(k);
+            put_block(K1B + 5);
+            if (m == 1 && w == 0 && l < A) S.aiv[l] = expf(-2.f * Wt.logstd[l]);  // read in the heads, after B2
+        }
         // ---- layer 1: Z1[s][fb + c] over the inputs (A = X rows, B = W1t, shared by the tiles)
         f32x4 z[R][NC], H1[R];
 #pragma unroll
@@ -257,7 +277,11 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
             }
         }
         PGM_STAMP(0);
-        lds_sync_m();  // B1: H1 of every feature block
+        if (gp > 0) {
+#pragma unroll
+            for (int k = K1B; k < K1B + 5; ++k) put_block(k);
+        }
+        lds_sync_m();  // B1: H1 of every feature block (and every wave's head block)
         // ---- layer 2: Z2[s][fb + c] = H1[s][:] . W2t[:][fb + c]
         f32x4 H2[R];
 #pragma unroll
@@ -536,20 +560,7 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
         lds_sync_m();
         const float sq_wg = ((S.red[32] + S.red[33]) + S.red[34]) + S.red[35];
         PGM_STAMP(7);
-        // ---- 3. squared norms of both towers' parts: one granule each, summed in (tower, part) order (HOPS 2: the
-        // granule also tells that the part's reduced blocks are published)
-        if constexpr (HOPS == 2) {
-#pragma unroll
-            for (int i = 0; i < OWV; ++i) {
-                if (hs + NS * (w + 4 * i) < NB) {
-                    const u32x4 u = {__float_as_uint(gr_[i][0]), __float_as_uint(gr_[i][1]), __float_as_uint(gr_[i][2]),
-                                     __float_as_uint(gr_[i][3])};
-                    __builtin_amdgcn_raw_buffer_store_b128(u, xr, pslot(hs, par) + ((w + 4 * i) * 64 + l) * 16, 0, SC1);
-                }
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            lds_sync_m();
-        }
+        // ---- 3. squared norms of both towers' parts: one granule each, summed in (tower, part) order
         if (t == 0)
             __hip_atomic_store(gran(1, m, hs, par), ((unsigned long long)tag << 32) | __float_as_uint(sq_wg),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -587,102 +598,61 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
             const float den = __builtin_amdgcn_sqrtf(vv_) * inv_bc2s + eps;
             pp_ -= step_size * mm_ * __builtin_amdgcn_rcpf(den);
         };
-        if constexpr (HOPS == 3) {
-            // ---- 4. Adam on the owned blocks (registers), publish them, write them into this part's image
+        // ---- 4. Adam on the owned blocks (registers), publish them, write them into this part's image
 #pragma unroll
-            for (int i = 0; i < OWV; ++i) {
-                const int b = hs + NS * (w + 4 * i);
-                if (b < NB) {
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        float mm = om[i][r], vv = ov[i][r], pp = op[i][r];
-                        adam(gr_[i][r], mm, vv, pp);
-                        om[i][r] = mm;
-                        ov[i][r] = vv;
-                        op[i][r] = pp;
-                    }
-                    const u32x4 u = {__float_as_uint(op[i][0]), __float_as_uint(op[i][1]), __float_as_uint(op[i][2]),
-                                     __float_as_uint(op[i][3])};
-                    __builtin_amdgcn_raw_buffer_store_b128(u, xr, pslot(hs, par) + ((w + 4 * i) * 64 + l) * 16, 0, SC1);
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int ii = frag_img<O, A, K>(b, l, r, m);
-                        if (ii >= 0) Pf[ii] = op[i][r];
-                    }
-                }
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            lds_sync_m();
-            if (t == 0)
-                __hip_atomic_store(gran(2, m, hs, par), (unsigned long long)tag << 32, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            if (w == 0 && l < NS && l != hs) spin(gran(2, m, l, par));
-            lds_sync_m();
-            PGM_STAMP(9);
-            // ---- the other parts' new parameter blocks into the image (block b: wave b mod 4)
-            u32x4 pv[BPW];
-#pragma unroll
-            for (int k = 0; k < BPW; ++k) {
-                const int b = w + 4 * k, h = b % NS, jj = b / NS;
-                if (h != hs) pv[k] = __builtin_amdgcn_raw_buffer_load_b128(xr, pslot(h, par) + (jj * 64 + l) * 16, 0, SC1);
-            }
-#pragma unroll
-            for (int k = 0; k < BPW; ++k) {
-                const int b = w + 4 * k;
-                if (b % NS != hs) {
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int ii = frag_img<O, A, K>(b, l, r, m);
-                        if (ii >= 0) Pf[ii] = __uint_as_float(pv[k][r]);
-                    }
-                }
-            }
-        } else {
-            // ---- 4. the whole reduced gradient (every part's blocks; this wave: b = w + 4k) and Adam on all of it
-            u32x4 pv[BPW];
-#pragma unroll
-            for (int k = 0; k < BPW; ++k) {
-                const int b = w + 4 * k;
-                pv[k] = __builtin_amdgcn_raw_buffer_load_b128(xr, pslot(b % NS, par) + ((b / NS) * 64 + l) * 16, 0, SC1);
-            }
-            PGM_STAMP(9);
-#pragma unroll
-            for (int k = 0; k < BPW; ++k) {
-                const int b = w + 4 * k;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int ii = frag_img<O, A, K>(b, l, r, m);
-                    if (ii >= 0) {
-                        float pp = Pf[ii], mm = om[k][r], vv = ov[k][r];
-                        adam(__uint_as_float(pv[k][r]), mm, vv, pp);
-                        om[k][r] = mm;
-                        ov[k][r] = vv;
-                        Pf[ii] = pp;
-                    }
-                }
-            }
-        }
-        dma_sync_m();  // image complete; this wave's row DMA retired (the barrier: every wave's)
-        if (m == 1 && t < A) S.aiv[t] = expf(-2.f * Wt.logstd[t]);  // read after the next step's B2
-        PGM_STAMP(10);
-    }
-    PGM_STAMP_FLUSH;
-    // ---- parameters and moments back to HBM (HOPS 3: each part its own blocks; HOPS 2: part 0, every element once);
-    // statistics and the step by part 0
-    if (HOPS == 3 || hs == 0) {
-#pragma unroll
-        for (int i = 0; i < NMV; ++i) {
-            const int b = HOPS == 3 ? hs + NS * (w + 4 * i) : w + 4 * i;
+        for (int i = 0; i < OWV; ++i) {
+            const int b = hs + NS * (w + 4 * i);
             if (b < NB) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
+                    float mm = om[i][r], vv = ov[i][r], pp = op[i][r];
+                    adam(gr_[i][r], mm, vv, pp);
+                    om[i][r] = mm;
+                    ov[i][r] = vv;
+                    op[i][r] = pp;
+                }
+                const u32x4 u = {__float_as_uint(op[i][0]), __float_as_uint(op[i][1]), __float_as_uint(op[i][2]),
+                                 __float_as_uint(op[i][3])};
+                __builtin_amdgcn_raw_buffer_store_b128(u, xr, pslot(hs, par) + ((w + 4 * i) * 64 + l) * 16, 0, SC1);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
                     const int ii = frag_img<O, A, K>(b, l, r, m);
-                    const int f = ii >= 0 ? img_to_flat<O, A, K>(ii, m, L) : -1;
-                    if (f >= 0) {
-                        P[f] = HOPS == 3 ? op[HOPS == 3 ? i : 0][r] : Pf[ii];
-                        Mo[f] = om[i][r];
-                        Vo[f] = ov[i][r];
-                    }
+                    if (ii >= 0) Pf[ii] = op[i][r];
+                }
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // + the row DMA issued during the image poll
+        lds_sync_m();
+        if (t == 0)
+            __hip_atomic_store(gran(2, m, hs, par), (unsigned long long)tag << 32, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        if (w == 0 && l < NS && l != hs) spin(gran(2, m, l, par));
+        lds_sync_m();  // every part's blocks published; the next minibatch's rows landed
+        PGM_STAMP(9);
+        // ---- the other parts' new blocks of this wave's feature block: loads in flight into the next step
+        if (gp + 1 < npass) {
+#pragma unroll
+            for (int k = 0; k < BPW; ++k) {
+                const int b = BPW * w + k, h = b % NS, jj = b / NS;
+                if (h != hs) pv[k] = __builtin_amdgcn_raw_buffer_load_b128(xr, pslot(h, par) + (jj * 64 + l) * 16, 0, SC1);
+            }
+        }
+        PGM_STAMP(10);
+    }
+    PGM_STAMP_FLUSH;
+    // ---- owners write their blocks' parameters and moments back; statistics and the step by part 0
+#pragma unroll
+    for (int i = 0; i < OWV; ++i) {
+        const int b = hs + NS * (w + 4 * i);
+        if (b < NB) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int ii = frag_img<O, A, K>(b, l, r, m);
+                const int f = ii >= 0 ? img_to_flat<O, A, K>(ii, m, L) : -1;
+                if (f >= 0) {
+                    P[f] = op[i][r];
+                    Mo[f] = om[i][r];
+                    Vo[f] = ov[i][r];
                 }
             }
         }
@@ -700,14 +670,12 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
 
 template <int O, int A, int K, int NS, int R>
 static int launch_fs_k(const pgm_dims* d, const MArgs& a, hipStream_t stream) {
-    const char* hv = getenv("PGM_FS_HOPS");
-    const bool three = hv && hv[0] == '3';
     const size_t smem = fs_smem_bytes<O, A, K, R>();
     if (smem > 160 * 1024) {
         set_error("pgm_ppo_update (fs): LDS %zu bytes exceeds 160 KiB", smem);
         return PGM_E_UNSUPPORTED;
     }
-    auto kern = three ? ppo_update_fs_kernel<O, A, K, NS, R, 3> : ppo_update_fs_kernel<O, A, K, NS, R, 2>;
+    auto kern = ppo_update_fs_kernel<O, A, K, NS, R>;
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update (fs)");
     const int grid = fs_grid(d->P, NS);

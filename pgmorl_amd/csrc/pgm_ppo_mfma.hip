@@ -2101,11 +2101,7 @@ static UpdateChoice choose_update(const pgm_dims* d, int mb) {
 int describe_update_mfma(const pgm_dims* d, const pgm_ppo_hparams* hp, char* buf, int n) {
     const int mb = d->T * d->N / hp->num_mini_batch;
     const UpdateChoice c = choose_update(d, mb);
-    if (c.kind == 2) {
-        const char* hv = getenv("PGM_FS_HOPS");
-        return snprintf(buf, n, "ppo_update_fs_kernel (NS=%d, R=%d, %d hops)", c.ns, mb / (16 * c.ns),
-                        hv && hv[0] == '3' ? 3 : 2);
-    }
+    if (c.kind == 2) return snprintf(buf, n, "ppo_update_fs_kernel (NS=%d, R=%d)", c.ns, mb / (16 * c.ns));
     if (c.kind == 1) return snprintf(buf, n, "ppo_update_t16_kernel (NS=%d, W=%d)", c.ns, c.w);
     return snprintf(buf, n, "ppo_update_mfma_kernel (MODE %d)", c.mode);
 }

@@ -80,6 +80,7 @@ def run(args, device='cuda', rng='device', log=print, runtime=None):
     rank, ws = world()
     writer = rank == 0  # every rank holds the same host state; one writes the results tree
     gen_writer = GenerationWriter() if writer else None
+    ep_files = EPFileCache(os.path.join(args.save_dir, 'final'), gen_writer) if writer else None
     while iteration < total_num_updates:
         if log is not None:
             log('\n------------------------------- Warm-up Stage -------------------------------' if episode == 0 else
@@ -161,6 +162,8 @@ def run(args, device='cuda', rng='device', log=print, runtime=None):
         steps = n_tasks * n_its * args.num_steps * args.num_processes
         del all_offspring_batch, all_sample_batch, offspring_batch, last_offspring_batch, task_batch
         compact_snapshots()
+        if writer:  # the EP members' final files, written ahead on the writer thread while the next generation trains
+            ep_files.update(ep)
         t2 = time.perf_counter()
         timing['rl_s'] += t1 - t0
         timing['host_s'] += t2 - t1
@@ -171,7 +174,7 @@ def run(args, device='cuda', rng='device', log=print, runtime=None):
     runtime.materialize(list(ep.sample_batch), dst=0)  # collective: EP snapshots onto the writing rank
     if writer:
         gen_writer.join()
-        write_final(args, ep)
+        write_final(args, ep, ep_files)
         timing['final_s'] = time.perf_counter() - t_final
         timing['wall_s'] = time.perf_counter() - t_start
         timing['env_steps_per_s_whole_run'] = timing['train_env_steps'] / timing['wall_s']
@@ -221,7 +224,7 @@ class GenerationWriter:
             if rec is None:
                 return
             try:
-                write_generation_record(rec)
+                rec() if callable(rec) else write_generation_record(rec)
             except BaseException as e:  # surfaced by join()
                 self._err = e
 
@@ -348,21 +351,111 @@ class _StateDictWriter:
             torch.save(sd, path)
 
 
-def write_final(args, ep):
-    """morl/morl.py:223-245: final/EP_policy_i.pt, EP_env_params_i.pkl, objs.txt, env_params.txt."""
+class EPFileCache:
+    """The final EP files (EP_policy_i.pt, EP_env_params_i.pkl, morl/morl.py:223-230) of every archive member,
+    written AHEAD: at each generation boundary the members that entered the EP get their two files under
+    final/.ep_cache/<uid>.{pt,pkl} on the background writer thread (one device->host copy of their parameters on the
+    main thread), and the files of members that left are deleted there too.  write_final then only renames each
+    final member's pair to its index (os.replace) instead of serialising thousands of policies at the end of the run.
+    Snapshots are immutable, so a member's files never go stale.  Members whose snapshot lives on another rank
+    (multi-GPU) are written by write_final after the final gather, as before."""
+
+    def __init__(self, final_dir, gen_writer):
+        import itertools
+        self.dir = os.path.join(final_dir, '.ep_cache')
+        self.writer = gen_writer
+        self.files = {}  # uid -> (pt path, pkl path), written or queued
+        self.next_uid = itertools.count()
+        self.sdw = None
+
+    def _paths(self, uid):
+        return os.path.join(self.dir, f'{uid}.pt'), os.path.join(self.dir, f'{uid}.pkl')
+
+    def update(self, ep):
+        members = list(ep.sample_batch)
+        live = set()
+        new = []
+        for smp in members:
+            uid = getattr(smp, '_ep_uid', None)
+            if uid is None:
+                uid = smp._ep_uid = next(self.next_uid)
+            live.add(uid)
+            if uid not in self.files and smp.snapshot.is_local:
+                new.append((uid, smp))
+        gone = [self.files.pop(u) for u in [u for u in self.files if u not in live]]
+        if new:
+            layout = new[0][1].snapshot.layout
+            flats = torch.stack([smp.snapshot.params for _, smp in new])
+            if self.sdw is None:
+                self.sdw = _StateDictWriter(layout.unflatten(flats[0]))
+            sdw = self.sdw
+            blocks = layout.unflatten_batch(flats) if sdw.ok else None
+            sds = None if blocks is not None else [layout.unflatten(f) for f in flats]
+            envs = [smp.env_params for _, smp in new]
+            paths = [self._paths(uid) for uid, _ in new]
+            for (uid, _), pp in zip(new, paths):
+                self.files[uid] = pp
+            first = not os.path.isdir(self.dir)
+
+            def job():
+                os.makedirs(self.dir, exist_ok=True)
+                for i, (pt, pkl) in enumerate(paths):
+                    if blocks is not None:
+                        sdw.save_records([b[i] for b in blocks], pt)
+                        if first and i == 0:
+                            sdw.verify({k: torch.from_numpy(b[0]) for k, b in zip(sdw.keys, blocks)}, pt)
+                    else:
+                        sdw.save(sds[i], pt)
+                    with open(pkl, 'wb') as fp:
+                        pickle.dump(envs[i], fp)
+            self.writer.submit(job)
+        if gone:
+            def drop():
+                for pt, pkl in gone:
+                    for f in (pt, pkl):
+                        try:
+                            os.remove(f)
+                        except FileNotFoundError:
+                            pass
+            self.writer.submit(drop)
+
+    def take(self, smp, i, final):
+        """Move a written member's pair to its final index; False when it has none (write it directly)."""
+        uid = getattr(smp, '_ep_uid', None)
+        pp = self.files.pop(uid, None) if uid is not None else None
+        if pp is None or not os.path.exists(pp[0]) or not os.path.exists(pp[1]):
+            return False
+        os.replace(pp[0], os.path.join(final, f'EP_policy_{i}.pt'))
+        os.replace(pp[1], os.path.join(final, f'EP_env_params_{i}.pkl'))
+        return True
+
+    def close(self):
+        import shutil
+        shutil.rmtree(self.dir, ignore_errors=True)
+        self.files.clear()
+
+
+def write_final(args, ep, cache=None):
+    """morl/morl.py:223-245: final/EP_policy_i.pt, EP_env_params_i.pkl, objs.txt, env_params.txt.  With ``cache``
+    (an EPFileCache whose writer thread has been joined) members written ahead are renamed into place."""
     fmt = _fmt(args.obj_num)
     final = os.path.join(args.save_dir, 'final')
     os.makedirs(final, exist_ok=True)
     samples = list(ep.sample_batch)
-    if samples:  # every EP policy's flat parameters in ONE device->host copy, then the reference state_dicts
-        snaps = [s.snapshot for s in samples]
+    if cache is not None:
+        todo = [i for i, smp in enumerate(samples) if not cache.take(smp, i, final)]
+        cache.close()
+    else:
+        todo = list(range(len(samples)))
+    if todo:  # every remaining EP policy's flat parameters in ONE device->host copy, then the reference state_dicts
+        snaps = [samples[i].snapshot for i in todo]
         flats_dev = torch.stack([sn.params for sn in snaps])
         flats = None
-        envs = [s.env_params for s in samples]
+        envs = [samples[i].env_params for i in todo]
         layout = snaps[0].layout
         sd0 = layout.unflatten(flats_dev[0])
         sdw = _StateDictWriter(sd0)
-        p0 = os.path.join(final, 'EP_policy_0.pt')
+        p0 = os.path.join(final, f'EP_policy_{todo[0]}.pt')
         sdw.save(sd0, p0)
         sdw.verify(sd0, p0)
 
@@ -372,20 +465,21 @@ def write_final(args, ep):
         if blocks is None:
             flats = flats_dev.cpu().numpy()
 
-        def save(i):
-            if i:
+        def save(j):
+            i = todo[j]
+            if j:
                 path = os.path.join(final, f'EP_policy_{i}.pt')
                 if blocks is not None:
-                    sdw.save_records([b[i] for b in blocks], path)
+                    sdw.save_records([b[j] for b in blocks], path)
                 else:
-                    sdw.save(layout.unflatten(flats[i]), path)
+                    sdw.save(layout.unflatten(flats[j]), path)
             with open(os.path.join(final, f'EP_env_params_{i}.pkl'), 'wb') as fp:
-                pickle.dump(envs[i], fp)
+                pickle.dump(envs[j], fp)
         # file creation and writes release the GIL: two writer threads overlap them with the Python work (one EP
         # can hold thousands of policies; more threads only contend for the GIL)
         from concurrent.futures import ThreadPoolExecutor
         with ThreadPoolExecutor(max_workers=2) as ex:
-            list(ex.map(save, range(len(samples))))
+            list(ex.map(save, range(len(todo))))
     with open(os.path.join(final, 'objs.txt'), 'w') as fp:
         for obj in ep.obj_batch:
             fp.write((fmt + '\n').format(*obj))

@@ -1,6 +1,7 @@
 """Host side of the drop-in on CPU: reference Sample <-> device-layout Sample round trip, Task copies,
 scalarisation, and the snapshot record packing used at the generation boundary."""
 import argparse
+import os
 
 import numpy as np
 import torch
@@ -179,3 +180,60 @@ def test_compact_snapshots_frees_arena_keeps_survivors():
     assert buf() is None and keep[0]._store.t.shape == (1, 3, L)
     assert torch.equal(keep[0].block(), ref[0, :, 1])
     assert compact_snapshots() == (0, 0)  # a fully live compact buffer stays put
+
+
+def test_ep_file_cache_matches_write_final(tmp_path):
+    """EPFileCache (whole-run overhead): EP members' final files written ahead at each generation
+    boundary on the writer thread and renamed into place by write_final give the same final/ tree as writing every
+    file at the end (morl/morl.py:223-245): same policies (torch.load, weights_only), same env_params pickles, members
+    that left the archive leave no files behind."""
+    import argparse
+    import pickle
+
+    from pgmorl_amd.layout import ParamLayout
+    from pgmorl_amd.morl import EPFileCache, GenerationWriter, write_final
+    from pgmorl_amd.pareto import EP
+    from pgmorl_amd.sample import DeviceSnapshot, RunningMeanStd, Sample
+    lay = ParamLayout(11, 3, 2)
+    rng = np.random.RandomState(7)
+
+    def sample(k):
+        z = torch.zeros(lay.total)
+        snap = DeviceSnapshot(lay, torch.from_numpy(rng.randn(lay.total).astype(np.float32)), z, z, 10 * k)
+        ob = RunningMeanStd(shape=(11,))
+        ob.mean = rng.randn(11)
+        obj = RunningMeanStd(shape=())
+        obj.mean, obj.var = rng.randn(2), rng.rand(2) + 0.5
+        return Sample.from_snapshot(snap, {'ob_rms': ob, 'ret_rms': RunningMeanStd(shape=()), 'obj_rms': obj},
+                                    objs=np.abs(rng.randn(2)) * 10 + k)
+
+    gens = [[sample(k) for k in range(6)] for _ in range(3)]
+    args = argparse.Namespace(obj_num=2, obj_rms=True)
+    outs = {}
+    for mode in ('cache', 'plain'):
+        save = tmp_path / mode
+        args.save_dir = str(save)
+        ep = EP()
+        writer = GenerationWriter()
+        cache = EPFileCache(str(save / 'final'), writer) if mode == 'cache' else None
+        for g in gens:
+            ep.update(g)
+            if cache is not None:
+                cache.update(ep)
+        writer.join()
+        if cache is not None:  # every current member written ahead, departed members' files already deleted
+            assert sorted(os.listdir(cache.dir)) == sorted(f'{smp._ep_uid}.{x}' for smp in ep.sample_batch
+                                                           for x in ('pt', 'pkl'))
+        write_final(args, ep, cache)
+        outs[mode] = (save / 'final', len(ep.sample_batch))
+    (dc, n), (dp, n2) = outs['cache'], outs['plain']
+    assert n == n2 and n >= 2
+    assert sorted(os.listdir(dc)) == sorted(os.listdir(dp))  # no cache directory or stale member files left
+    for i in range(n):
+        a = torch.load(str(dc / f'EP_policy_{i}.pt'), weights_only=True)
+        b = torch.load(str(dp / f'EP_policy_{i}.pt'), weights_only=True)
+        assert list(a) == list(b) and all(torch.equal(a[k], b[k]) for k in a)
+        with open(dc / f'EP_env_params_{i}.pkl', 'rb') as f1, open(dp / f'EP_env_params_{i}.pkl', 'rb') as f2:
+            assert f1.read() == f2.read()
+    for f in ('objs.txt', 'env_params.txt'):
+        assert (dc / f).read_text() == (dp / f).read_text()

@@ -1,12 +1,10 @@
 #!/bin/bash
-# GPU box: the device side of the full-algorithm HV comparison (scripts/hv_full.py) against a committed oracle JSON.
-# Usage: bash scripts/hv_device.sh TAG ORACLE_JSON [ORACLE_JSON ...]   -> gpurun_out/<TAG>_<env>.json
+# GPU box: the device side of every committed oracle HV run (scripts/hv_full.py).  Usage: bash scripts/hv_device.sh TAG
 set -o pipefail
-TAG=${1:-hv}; shift
-OUT=$(pwd)/gpurun_out
-mkdir -p $OUT
-for REF in "$@"; do
-  E=$(basename $REF .json | sed 's/.*oracle_//')
-  timeout -k 10 600 python -u scripts/hv_full.py device --ref $REF --out $OUT/${TAG}_$E.json > $OUT/${TAG}_$E.log 2>&1 || { echo HV $E FAILED; tail -20 $OUT/${TAG}_$E.log; exit 1; }
-  tail -1 $OUT/${TAG}_$E.log
+TAG=${1:-r04}
+for env in hopper hopper3; do
+  ref=profiles/${TAG}_hvfull_oracle_${env}.json
+  [ -f $ref ] || continue
+  timeout -k 10 600 python -u scripts/hv_full.py device --ref $ref --out gpurun_out/${TAG}_hvfull_${env}.json > gpurun_out/hv_${TAG}_${env}.log 2>&1 || { echo HV $env FAILED; tail -5 gpurun_out/hv_${TAG}_${env}.log; exit 1; }
+  tail -c 400 gpurun_out/hv_${TAG}_${env}.log; echo
 done

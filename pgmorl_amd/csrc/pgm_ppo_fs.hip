@@ -100,14 +100,15 @@ struct FsSmem {
     static constexpr int NDT = (SB * RSL + 255) / 256;         // 1-KiB LDS-DMA pieces per staged pass
     static constexpr int SBI = 64 * ((SB + 63) / 64);          // index slots (one 64-lane DMA per wave)
     static constexpr bool ZA = R >= 8;                         // dZ2 tile aliases the H2 tile (LDS budget)
-    static constexpr int NDO = R >= 4 ? 1 : 4;                 // dO tiles: shared (row-split heads) or per wave
+    static constexpr int NHP = R >= 4 ? 1 : 4;                 // partial head outputs (R < 4: one tile per wave)
     TowerImg<O, A, K> Pm;                                      // parameters (working copy of every part)
     alignas(16) float RB[2][NDT * 256];                        // packed rows of this / the next minibatch
     int32_t IB[2][SBI];                                        // sample indices of the next two minibatches
     float H1s[SB][S16];                                        // H1 of all tiles, all 64 features
     float H2s[SB][S16];                                        // H2 (R >= 8: then dZ2)
     float Zs[ZA ? 1 : SB][S16];                                // dZ2
-    float dOs[NDO][SB][DQS];                                   // dL/d(head output), transposed for dH2
+    float dOs[SB][DQS];                                        // dL/d(head output), transposed for dH2
+    float HP[NHP][SB][DQS];                                    // R < 4: the waves' partial head outputs
     float aiv[A];                                              // actor 1 / std^2
     float red[192];  // [0, 64) head-bias partials / poll results, [64, 128) logstd partials / norms, 128+ loss sums
 };
@@ -130,7 +131,7 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
     constexpr int BPW = fs_bpw(O), NB = fs_nb(O), NOWN = fs_nown(O, NS);
     constexpr int OWV = (NOWN + 3) / 4;  // owned blocks per wave (block j of the part: wave j mod 4)
     constexpr int ISB = NB * 1024, PSB = NOWN * 1024;
-    constexpr bool HSPLIT = R >= 4;      // heads: row tiles split over the waves (else every wave does all)
+    constexpr bool HSPLIT = R >= 4;      // heads: row tiles split over the waves (else units + samples split)
     constexpr int NHT = HSPLIT ? R / 4 : R;
     constexpr int NC = R == 1 ? 2 : 1;   // accumulator chains per tile of the 16-deep contractions
     constexpr int oW2 = O * H, oWh = oW2 + H * SCR, oB1 = oWh + Q * H, oB2 = oB1 + H, oBh = oB2 + H, oLs = oBh + Q;
@@ -226,14 +227,12 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
     // layer 1, W2 before layer 2, the head block before B2 (heads read every wave's); the own part's blocks are
     // written by their owners before the parameter hand-off
     u32x4 pv[BPW];
-    auto put_block = [&](int k) {
+    auto put_block = [&](int k) {  // (the own part's blocks rewrite the values their owners already wrote)
         const int b = BPW * w + k;
-        if (b % NS != hs) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int ii = frag_img<O, A, K>(b, l, r, m);
-                if (ii >= 0) Pf[ii] = __uint_as_float(pv[k][r]);
-            }
+        for (int r = 0; r < 4; ++r) {
+            const int ii = frag_img<O, A, K>(b, l, r, m);
+            if (ii >= 0) Pf[ii] = __uint_as_float(pv[k][r]);
         }
     };
     for (int gp = 0; gp < npass; ++gp) {
@@ -281,7 +280,9 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
 #pragma unroll
             for (int k = K1B; k < K1B + 5; ++k) put_block(k);
         }
+        PGM_STAMP(11);
         lds_sync_m();  // B1: H1 of every feature block (and every wave's head block)
+        PGM_STAMP(12);
         // ---- layer 2: Z2[s][fb + c] = H1[s][:] . W2t[:][fb + c]
         f32x4 H2[R];
 #pragma unroll
@@ -308,92 +309,111 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
         }
         PGM_STAMP(1);
         lds_sync_m();  // B2: H2 of every feature block
+        PGM_STAMP(13);
         // ---- heads on the MFMA: out[s][q] = H2[s][:] . Wh[q][:] (q = lane column < Q), then the per-(sample,
-        // output) loss gradients dO in C layout (ppo.py:80-96)
+        // output) loss gradients dO (ppo.py:80-96) into the shared dO tile.  R >= 4: wave w takes row tiles w, w + 4, ...
+        // whole; R < 4: wave w contracts its own 16 units for every tile (partial outputs added through LDS) and
+        // finishes samples 4g + w of every tile (C register w).  Either way a quarter of the loss work per wave.
         const bool qv = c < Q;
-        float bh_[H / 4];
-#pragma unroll
-        for (int ks = 0; ks < H / 4; ++ks) bh_[ks] = qv ? Wt.Wh[qv ? c : 0][4 * ks + g] : 0.f;
         const float bhb = qv ? Wt.bh[c] : 0.f;
         float gbh = 0.f, gls = 0.f, lsum = 0.f;
-        f32x4 dOr[HSPLIT ? 1 : R];
-#pragma unroll
-        for (int hi = 0; hi < NHT; ++hi) {
-            const int ti = HSPLIT ? w + 4 * hi : hi;
-            const float* rr = rt(ti);
-            f32x4 ho[NC];
-#pragma unroll
-            for (int q = 0; q < NC; ++q) ho[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int ks = 0; ks < H / 4; ++ks)
-                ho[ks % NC] = mfma16(S.H2s[16 * ti + c][4 * ks + g], bh_[ks], ho[ks % NC]);
-            if constexpr (NC == 2) ho[0] += ho[1];
-            f32x4 dO;
+        // dL/d(head output) of sample s, output c (this lane), from the head output `out` (bias included)
+        auto loss1 = [&](const float* rr, int s, float out) -> float {
             if (m == 0) {  // value loss over the K objectives
+                const bool ok = c < K;
+                const float Vold = rr[s * RSL + O + A + 2 + (c < K ? c : 0)];
+                const float Rt = rr[s * RSL + O + A + 2 + K + (c < K ? c : 0)];
+                float gv, ls;
+                if (a.hp.use_clipped_value_loss) {
+                    const float dv = out - Vold;
+                    const float vc = Vold + fminf(fmaxf(dv, -clip), clip);
+                    const float l1 = (out - Rt) * (out - Rt), l2 = (vc - Rt) * (vc - Rt);
+                    const float inr = (dv >= -clip && dv <= clip) ? 1.f : 0.f;
+                    gv = wmax2(l1, l2) * 2.f * (out - Rt) + wmax2(l2, l1) * 2.f * (vc - Rt) * inr;
+                    ls = fmaxf(l1, l2);
+                } else {
+                    gv = 2.f * (out - Rt);
+                    ls = (Rt - out) * (Rt - out);
+                }
+                lsum += ok ? ls : 0.f;
+                return ok ? vscale * gv : 0.f;
+            }
+            // clipped surrogate; a sample's log-prob is a 16-lane row sum over its outputs
+            const bool av_ = c < A;
+            const float aiv = S.aiv[av_ ? c : 0], ls_c = av_ ? Wt.logstd[av_ ? c : 0] : 0.f;
+            const float diff = av_ ? rr[s * RSL + O + (av_ ? c : 0)] - out : 0.f;
+            const float lpe = av_ ? -0.5f * diff * diff * aiv - ls_c - LOG_SQRT_2PI : 0.f;
+            const float lp = row_sum16(lpe);
+            const float ratio = expf(lp - rr[s * RSL + O + A]);
+            const float ad = rr[s * RSL + O + A + 1];
+            const float s1 = ratio * ad;
+            const float s2 = fminf(fmaxf(ratio, 1.f - clip), 1.f + clip) * ad;
+            const float inr = (ratio >= 1.f - clip && ratio <= 1.f + clip) ? 1.f : 0.f;
+            const float gr = ad * (wmin2(s1, s2) + wmin2(s2, s1) * inr);
+            const float dlp = ascale * gr * ratio;
+            lsum += c == 0 ? -fminf(s1, s2) : 0.f;
+            gls += av_ ? dlp * (diff * diff * aiv - 1.f) : 0.f;
+            return av_ ? dlp * diff * aiv : 0.f;
+        };
+        float* dt = &S.dOs[0][0];
+        if constexpr (HSPLIT) {
+            float bh_[H / 4];
+#pragma unroll
+            for (int ks = 0; ks < H / 4; ++ks) bh_[ks] = qv ? Wt.Wh[qv ? c : 0][4 * ks + g] : 0.f;
+#pragma unroll
+            for (int hi = 0; hi < NHT; ++hi) {
+                const int ti = w + 4 * hi;
+                f32x4 ho[NC];
+#pragma unroll
+                for (int q = 0; q < NC; ++q) ho[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int ks = 0; ks < H / 4; ++ks)
+                    ho[ks % NC] = mfma16(S.H2s[16 * ti + c][4 * ks + g], bh_[ks], ho[ks % NC]);
+                if constexpr (NC == 2) ho[0] += ho[1];
+                PGM_STAMP(14);
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const int s = 4 * g + r;
-                    const bool ok = c < K;
-                    const float V = ho[0][r] + bhb;
-                    const float Vold = rr[s * RSL + O + A + 2 + (c < K ? c : 0)];
-                    const float Rt = rr[s * RSL + O + A + 2 + K + (c < K ? c : 0)];
-                    float gv, ls;
-                    if (a.hp.use_clipped_value_loss) {
-                        const float dv = V - Vold;
-                        const float vc = Vold + fminf(fmaxf(dv, -clip), clip);
-                        const float l1 = (V - Rt) * (V - Rt), l2 = (vc - Rt) * (vc - Rt);
-                        const float inr = (dv >= -clip && dv <= clip) ? 1.f : 0.f;
-                        gv = wmax2(l1, l2) * 2.f * (V - Rt) + wmax2(l2, l1) * 2.f * (vc - Rt) * inr;
-                        ls = fmaxf(l1, l2);
-                    } else {
-                        gv = 2.f * (V - Rt);
-                        ls = (Rt - V) * (Rt - V);
-                    }
-                    dO[r] = ok ? vscale * gv : 0.f;
-                    lsum += ok ? ls : 0.f;
-                }
-            } else {  // clipped surrogate; a sample's log-prob is a 16-lane row sum over its outputs
-                const bool av_ = c < A;
-                const float aiv = S.aiv[av_ ? c : 0], ls_c = av_ ? Wt.logstd[av_ ? c : 0] : 0.f;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int s = 4 * g + r;
-                    const float diff = av_ ? rr[s * RSL + O + (av_ ? c : 0)] - (ho[0][r] + bhb) : 0.f;
-                    const float lpe = av_ ? -0.5f * diff * diff * aiv - ls_c - LOG_SQRT_2PI : 0.f;
-                    const float lp = row_sum16(lpe);
-                    const float ratio = expf(lp - rr[s * RSL + O + A]);
-                    const float ad = rr[s * RSL + O + A + 1];
-                    const float s1 = ratio * ad;
-                    const float s2 = fminf(fmaxf(ratio, 1.f - clip), 1.f + clip) * ad;
-                    const float inr = (ratio >= 1.f - clip && ratio <= 1.f + clip) ? 1.f : 0.f;
-                    const float gr = ad * (wmin2(s1, s2) + wmin2(s2, s1) * inr);
-                    const float dlp = ascale * gr * ratio;
-                    lsum += c == 0 ? -fminf(s1, s2) : 0.f;
-                    dO[r] = av_ ? dlp * diff * aiv : 0.f;
-                    gls += av_ ? dlp * (diff * diff * aiv - 1.f) : 0.f;
+                    const float d = loss1(rt(ti), 4 * g + r, ho[0][r] + bhb);
+                    gbh += d;
+                    if (c < DQ) dt[(16 * ti + 4 * g + r) * DQS + c] = d;
                 }
             }
-            float* dt = &S.dOs[HSPLIT ? 0 : w][0][0];
+        } else {
+            float bw4[4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                gbh += dO[r];
-                if (c < DQ) dt[(16 * ti + 4 * g + r) * DQS + c] = dO[r];
+            for (int k4 = 0; k4 < 4; ++k4) bw4[k4] = qv ? Wt.Wh[qv ? c : 0][fb + 4 * k4 + g] : 0.f;
+#pragma unroll
+            for (int ti = 0; ti < R; ++ti) {
+                f32x4 ho = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int k4 = 0; k4 < 4; ++k4) ho = mfma16(S.H2s[16 * ti + c][fb + 4 * k4 + g], bw4[k4], ho);
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if (c < DQ) S.HP[w][16 * ti + 4 * g + r][c] = ho[r];
             }
-            if constexpr (!HSPLIT) dOr[hi] = dO;
+            PGM_STAMP(14);
+            lds_sync_m();  // B2h: every wave's partial head outputs
+#pragma unroll
+            for (int ti = 0; ti < R; ++ti) {
+                const int s = 4 * g + w, row = 16 * ti + s;
+                const int cq = c < DQ ? c : 0;
+                const float out = c < DQ ? ((S.HP[0][row][cq] + S.HP[1][row][cq]) + S.HP[2][row][cq]) + S.HP[3][row][cq] : 0.f;
+                const float d = loss1(rt(ti), s, out + bhb);
+                gbh += d;
+                if (c < DQ) dt[row * DQS + c] = d;
+            }
         }
+        PGM_STAMP(15);
         gbh = group4_sum(gbh);
         gls = group4_sum(gls);
         lsum = wave_sum64(lsum);
-        if constexpr (HSPLIT) {  // partial head sums of this wave's row tiles: summed in wave order after B3
-            if (g == 0) {
-                S.red[16 * w + c] = gbh;
-                S.red[64 + 16 * w + c] = gls;
-            }
+        if (g == 0) {  // this wave's partial head sums (its row tiles / its samples): summed in wave order later
+            S.red[16 * w + c] = gbh;
+            S.red[64 + 16 * w + c] = gls;
         }
-        if (t == 64 * w) S.red[128 + w] = lsum;  // wave partials (row-split heads) / identical copies (else)
+        if (t == 64 * w) S.red[128 + w] = lsum;
         PGM_STAMP(2);
-        if constexpr (HSPLIT || Sm::ZA) lds_sync_m();  // B2b: dO tiles of every wave / H2 reads done before dZ2
-        else wave_lds_fence();
+        lds_sync_m();  // B2b: the dO tile of every wave's rows / samples (and, R = 8, H2 reads done before dZ2)
         // ---- head-weight gradient gWh^T[u][q] += H2^T dO, dH2 = dO . Wh -> dZ2 (this wave's units)
         f32x4 gWh = f32x4{0.f, 0.f, 0.f, 0.f}, gW2[4], gW1[K1B];
         float gB1 = 0.f, gB2 = 0.f;
@@ -401,14 +421,14 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
         for (int ib = 0; ib < 4; ++ib) gW2[ib] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int kb = 0; kb < K1B; ++kb) gW1[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
-        const float* dtl = &S.dOs[HSPLIT ? 0 : w][0][0];
+        const float* dtl = &S.dOs[0][0];
         float (*Zt)[S16] = Sm::ZA ? S.H2s : S.Zs;
         f32x4 dZ2[R];
 #pragma unroll
         for (int ti = 0; ti < R; ++ti) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const float bo = HSPLIT ? (qv ? dtl[(16 * ti + 4 * g + r) * DQS + (qv ? c : 0)] : 0.f) : dOr[HSPLIT ? 0 : ti][r];
+                const float bo = qv ? dtl[(16 * ti + 4 * g + r) * DQS + (qv ? c : 0)] : 0.f;
                 gWh = mfma16(H2[ti][r], bo, gWh);
             }
             f32x4 zz = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -432,6 +452,14 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
                 for (int ib = 0; ib < 4; ++ib)
                     gW2[ib] = mfma16(S.H1s[16 * ti + 4 * g + r][16 * ib + c], dZ2[ti][r], gW2[ib]);
         }
+        // this wave's dW2 / head-weight blocks are final: out now (write-through under the dH1 / dW1 pass)
+        auto pub = [&](int k, const f32x4& v) {
+            const u32x4 u = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
+            __builtin_amdgcn_raw_buffer_store_b128(u, xr, islot(hs, par) + ((w * BPW + k) * 64 + l) * 16, 0, SC1);
+        };
+#pragma unroll
+        for (int ib = 0; ib < 4; ++ib) pub(K1B + ib, gW2[ib]);
+        pub(K1B + 4, gWh);
         PGM_STAMP(3);
         lds_sync_m();  // B3: dZ2 of every feature block
         // ---- dH1 = dZ2 W2 for this wave's input block, dZ1, dW1^T[k][fb + c] += X^T dZ1
@@ -467,42 +495,27 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
         PGM_STAMP(4);
 
         // ================================================================ exchange
-        // ---- 1. publish this wave's gradient blocks (its feature block of every tensor)
+        // ---- 1. publish this wave's gradient blocks (its feature block of every tensor; the dW2 / head blocks
+        // went out before B3, so their write-through overlapped the dH1 / dW1 pass)
         dbg_delay(a.dbg, gp, 0);
         {
             float vb2 = 0.f, vls = 0.f;
-            if (w == 0) {
-                if constexpr (HSPLIT) {  // the waves' head partial sums (written before B3), in wave order
-                    vb2 = ((S.red[c] + S.red[16 + c]) + S.red[32 + c]) + S.red[48 + c];
-                    vls = ((S.red[64 + c] + S.red[80 + c]) + S.red[96 + c]) + S.red[112 + c];
-                } else {
-                    vb2 = gbh;
-                    vls = gls;
-                }
+            if (w == 0) {  // the waves' head partial sums (written before B2b), in wave order
+                vb2 = ((S.red[c] + S.red[16 + c]) + S.red[32 + c]) + S.red[48 + c];
+                vls = ((S.red[64 + c] + S.red[80 + c]) + S.red[96 + c]) + S.red[112 + c];
                 // -entropy_coef * d(mean entropy)/d logstd enters once per tower (ppo.py:98): part 0
                 if (hs == 0) vls -= a.hp.entropy_coef;
             }
             const f32x4 vec = g == 0 ? f32x4{gB1, gB2, c < NQ ? vb2 : 0.f, m == 1 && c < A ? vls : 0.f}
                                      : f32x4{0.f, 0.f, 0.f, 0.f};
-            const int base = islot(hs, par) + (w * BPW * 64 + l) * 16;
-            auto st = [&](int k, const f32x4& v) {
-                const u32x4 u = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
-                                 __float_as_uint(v[3])};
-                __builtin_amdgcn_raw_buffer_store_b128(u, xr, base + k * 1024, 0, SC1);
-            };
 #pragma unroll
-            for (int kb = 0; kb < K1B; ++kb) st(kb, gW1[kb]);
-#pragma unroll
-            for (int ib = 0; ib < 4; ++ib) st(K1B + ib, gW2[ib]);
-            st(K1B + 4, gWh);
-            st(K1B + 5, vec);
+            for (int kb = 0; kb < K1B; ++kb) pub(kb, gW1[kb]);
+            pub(K1B + 5, vec);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
         lds_sync_m();
         PGM_STAMP(5);
-        float lsum_wg = 0.f;
-        if constexpr (HSPLIT) lsum_wg = ((S.red[128] + S.red[129]) + S.red[130]) + S.red[131];
-        else lsum_wg = S.red[128];
+        const float lsum_wg = ((S.red[128] + S.red[129]) + S.red[130]) + S.red[131];
         if (t == 0)
             __hip_atomic_store(gran(0, m, hs, par), ((unsigned long long)tag << 32) | __float_as_uint(lsum_wg),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -633,8 +646,8 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
         if (gp + 1 < npass) {
 #pragma unroll
             for (int k = 0; k < BPW; ++k) {
-                const int b = BPW * w + k, h = b % NS, jj = b / NS;
-                if (h != hs) pv[k] = __builtin_amdgcn_raw_buffer_load_b128(xr, pslot(h, par) + (jj * 64 + l) * 16, 0, SC1);
+                const int b = BPW * w + k, h = b % NS, jj = b / NS;  // (own part's blocks too: straight-line loads)
+                pv[k] = __builtin_amdgcn_raw_buffer_load_b128(xr, pslot(h, par) + (jj * 64 + l) * 16, 0, SC1);
             }
         }
         PGM_STAMP(10);
@@ -727,7 +740,12 @@ int ppo_update_fs(const pgm_dims* d, const MArgs& a, int ns, hipStream_t stream)
     const int R = mb / (16 * ns);
     return dispatch_dims(d->O, d->A, d->K, "pgm_ppo_update (fs)", [&](auto o, auto aa, auto k) -> int {
         constexpr int O = decltype(o)::value, A = decltype(aa)::value, K = decltype(k)::value;
-        if constexpr (O > 32) {
+#ifdef PGM_STAMPS
+        constexpr bool skip = O != 17;  // diagnostic builds: the Walker / HalfCheetah dims only (compile time)
+#else
+        constexpr bool skip = false;
+#endif
+        if constexpr (O > 32 || skip) {
             return PGM_E_UNSUPPORTED;
         } else {
             switch (ns) {

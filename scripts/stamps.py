@@ -42,9 +42,10 @@ wnames = {0: 'noise + layer-1 slices', 1: 'barrier A', 2: 'L1 sum, L2, head, dra
 unames = {0: 'layer 1 (L2 stream)', 1: 'layer 2 + tanh', 2: 'heads + loss', 3: 'gWh, dH2, gW2, dH1',
           4: 'pass barrier 1', 5: 'dW1 contraction', 6: 'pass barrier 2', 7: 'small-image reduction',
           8: 'publish + flag wait', 9: 'gather partner', 10: 'sumsq + norm hand-off', 11: 'Adam (LDS + W1 HBM)'}
-fnames = {0: 'L1 (+ loop top)', 1: 'B1 + L2', 2: 'B2 + heads + loss', 3: 'B2b + gWh, dH2, gW2', 4: 'B3 + dH1, gW1',
-          5: 'publish + drain + barrier', 6: 'image flag poll (+ row DMA)', 7: 'reduce-scatter loads + sumsq',
-          8: 'norm granules', 9: 'Adam + publish + param poll', 10: 'gather + end barrier'}
+fnames = {0: 'put W1/vec + L1', 11: 'put W2/Wh', 12: 'B1 wait', 1: 'L2 + H2 write', 13: 'B2 wait',
+          14: 'Wh reads + head MFMAs', 15: 'loss VALU', 2: 'group sums', 3: 'B2b + gWh, dH2, gW2',
+          4: 'B3 + dH1, gW1', 5: 'publish + drain + barrier', 6: 'image flag poll (+ row DMA)',
+          7: 'reduce-scatter loads + sumsq', 8: 'norm granules', 9: 'Adam + publish + param poll', 10: 'gather issue'}
 for name, steps in (('rollout', T), ('update', 320), ('mfma', 320), ('lanes', T), ('wide', T), ('wupd', 320), ('fs', 320)):
     if name == 'fs':
         names = fnames

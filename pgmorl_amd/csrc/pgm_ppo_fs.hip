@@ -91,6 +91,8 @@ __device__ __forceinline__ int frag_img(int b, int l, int r, int m) {
     return wb == 0 && m == 1 && c < A ? oLs + c : -1;
 }
 
+constexpr int SF = 72;  // fs activation-tile row stride (floats)
+
 template <int O, int A, int K, int R>
 struct FsSmem {
     static constexpr int Q = qmax<A, K>();
@@ -104,9 +106,14 @@ struct FsSmem {
     TowerImg<O, A, K> Pm;                                      // parameters (working copy of every part)
     alignas(16) float RB[2][NDT * 256];                        // packed rows of this / the next minibatch
     int32_t IB[2][SBI];                                        // sample indices of the next two minibatches
-    float H1s[SB][S16];                                        // H1 of all tiles, all 64 features
-    float H2s[SB][S16];                                        // H2 (R >= 8: then dZ2)
-    float Zs[ZA ? 1 : SB][S16];                                // dZ2
+    // activation tiles [sample][feature], row stride SF = 72 floats (= 8 mod 64): the feature-contracting products read
+    // 4 consecutive features per lane with ds_read_b128 (16-B aligned, conflict-free for the 16-row tiles)
+    static constexpr bool HT = R <= 4;                         // H1 also [feature][sample] (the dW2 A operand)
+    static constexpr int STT = HT ? 72 : 4;                    // its row stride (16 R <= 64 samples, = 8 mod 64)
+    alignas(16) float H1s[SB][SF];                             // H1 of all tiles, all 64 features
+    alignas(16) float H2s[SB][SF];                             // H2 (R >= 8: then dZ2)
+    alignas(16) float Zs[ZA ? 1 : SB][SF];                     // dZ2
+    alignas(16) float H1T[HT ? H : 1][STT];                    // H1 transposed (R <= 4)
     float dOs[SB][DQS];                                        // dL/d(head output), transposed for dH2
     float HP[NHP][SB][DQS];                                    // R < 4: the waves' partial head outputs
     float aiv[A];                                              // actor 1 / std^2
@@ -273,6 +280,9 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
                 tanh_bias_pk<4>(zz, bias, H1[ti]);
 #pragma unroll
                 for (int r = 0; r < 4; ++r) S.H1s[16 * ti + 4 * g + r][fb + c] = H1[ti][r];
+                if constexpr (Sm::HT)
+                    *reinterpret_cast<float4*>(&S.H1T[fb + c][16 * ti + 4 * g]) =
+                        make_float4(H1[ti][0], H1[ti][1], H1[ti][2], H1[ti][3]);
             }
         }
         PGM_STAMP(0);
@@ -289,12 +299,20 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
         for (int ti = 0; ti < R; ++ti)
 #pragma unroll
             for (int q = 0; q < NC; ++q) z[ti][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+        // k-step (j, i) contracts input k = 16 j + 4 g + i in lane group g: four consecutive inputs per lane and j, so
+        // the A operands of four k-steps are one ds_read_b128 (the B rows follow the same order)
 #pragma unroll
-        for (int ks = 0; ks < H / 4; ++ks) {
-            const int k = 4 * ks + g;
-            const float bw = Wt.W2t[k][fb + c];
+        for (int j = 0; j < 4; ++j) {
+            float bw[4];
 #pragma unroll
-            for (int ti = 0; ti < R; ++ti) z[ti][ks % NC] = mfma16(S.H1s[16 * ti + c][k], bw, z[ti][ks % NC]);
+            for (int i = 0; i < 4; ++i) bw[i] = Wt.W2t[16 * j + 4 * g + i][fb + c];
+#pragma unroll
+            for (int ti = 0; ti < R; ++ti) {
+                const float4 a4 = *reinterpret_cast<const float4*>(&S.H1s[16 * ti + c][16 * j + 4 * g]);
+                const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) z[ti][(4 * j + i) % NC] = mfma16(av[i], bw[i], z[ti][(4 * j + i) % NC]);
+            }
         }
         {
             const float bias = Wt.b2[fb + c];
@@ -357,9 +375,10 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
         };
         float* dt = &S.dOs[0][0];
         if constexpr (HSPLIT) {
-            float bh_[H / 4];
+            float4 bh4[4];  // head rows in the permuted k order (16 j + 4 g + i), one ds_read_b128 per j
 #pragma unroll
-            for (int ks = 0; ks < H / 4; ++ks) bh_[ks] = qv ? Wt.Wh[qv ? c : 0][4 * ks + g] : 0.f;
+            for (int j = 0; j < 4; ++j)
+                bh4[j] = qv ? *reinterpret_cast<const float4*>(&Wt.Wh[qv ? c : 0][16 * j + 4 * g]) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
             for (int hi = 0; hi < NHT; ++hi) {
                 const int ti = w + 4 * hi;
@@ -367,8 +386,12 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
 #pragma unroll
                 for (int q = 0; q < NC; ++q) ho[q] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                for (int ks = 0; ks < H / 4; ++ks)
-                    ho[ks % NC] = mfma16(S.H2s[16 * ti + c][4 * ks + g], bh_[ks], ho[ks % NC]);
+                for (int j = 0; j < 4; ++j) {
+                    const float4 a4 = *reinterpret_cast<const float4*>(&S.H2s[16 * ti + c][16 * j + 4 * g]);
+                    const float av[4] = {a4.x, a4.y, a4.z, a4.w}, bv[4] = {bh4[j].x, bh4[j].y, bh4[j].z, bh4[j].w};
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) ho[(4 * j + i) % NC] = mfma16(av[i], bv[i], ho[(4 * j + i) % NC]);
+                }
                 if constexpr (NC == 2) ho[0] += ho[1];
                 PGM_STAMP(14);
 #pragma unroll
@@ -379,14 +402,16 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
                 }
             }
         } else {
-            float bw4[4];
-#pragma unroll
-            for (int k4 = 0; k4 < 4; ++k4) bw4[k4] = qv ? Wt.Wh[qv ? c : 0][fb + 4 * k4 + g] : 0.f;
+            // this wave's units k = fb + 4 g + i (one ds_read_b128 of the head row and of the H2 row)
+            const float4 b4 = qv ? *reinterpret_cast<const float4*>(&Wt.Wh[qv ? c : 0][fb + 4 * g]) : make_float4(0.f, 0.f, 0.f, 0.f);
+            const float bv[4] = {b4.x, b4.y, b4.z, b4.w};
 #pragma unroll
             for (int ti = 0; ti < R; ++ti) {
                 f32x4 ho = f32x4{0.f, 0.f, 0.f, 0.f};
+                const float4 a4 = *reinterpret_cast<const float4*>(&S.H2s[16 * ti + c][fb + 4 * g]);
+                const float av[4] = {a4.x, a4.y, a4.z, a4.w};
 #pragma unroll
-                for (int k4 = 0; k4 < 4; ++k4) ho = mfma16(S.H2s[16 * ti + c][fb + 4 * k4 + g], bw4[k4], ho);
+                for (int i = 0; i < 4; ++i) ho = mfma16(av[i], bv[i], ho);
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
                     if (c < DQ) S.HP[w][16 * ti + 4 * g + r][c] = ho[r];
@@ -422,7 +447,7 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
 #pragma unroll
         for (int kb = 0; kb < K1B; ++kb) gW1[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
         const float* dtl = &S.dOs[0][0];
-        float (*Zt)[S16] = Sm::ZA ? S.H2s : S.Zs;
+        float (*Zt)[SF] = Sm::ZA ? S.H2s : S.Zs;
         f32x4 dZ2[R];
 #pragma unroll
         for (int ti = 0; ti < R; ++ti) {
@@ -446,11 +471,21 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
                 Zt[16 * ti + 4 * g + r][fb + c] = dZ2[ti][r];
             }
             // dW2^T[in][fb + c] += H1^T dZ2 (A = H1 of every feature block in C layout from its tile)
+            if constexpr (Sm::HT) {  // A = H1[sample 16 ti + 4 g + r][16 ib + c]: one ds_read_b128 of the transposed tile
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
+                for (int ib = 0; ib < 4; ++ib) {
+                    const float4 a4 = *reinterpret_cast<const float4*>(&S.H1T[16 * ib + c][16 * ti + 4 * g]);
+                    const float av[4] = {a4.x, a4.y, a4.z, a4.w};
 #pragma unroll
-                for (int ib = 0; ib < 4; ++ib)
-                    gW2[ib] = mfma16(S.H1s[16 * ti + 4 * g + r][16 * ib + c], dZ2[ti][r], gW2[ib]);
+                    for (int r = 0; r < 4; ++r) gW2[ib] = mfma16(av[r], dZ2[ti][r], gW2[ib]);
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int ib = 0; ib < 4; ++ib)
+                        gW2[ib] = mfma16(S.H1s[16 * ti + 4 * g + r][16 * ib + c], dZ2[ti][r], gW2[ib]);
+            }
         }
         // this wave's dW2 / head-weight blocks are final: out now (write-through under the dH1 / dW1 pass)
         auto pub = [&](int k, const f32x4& v) {
@@ -468,11 +503,17 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
 #pragma unroll
             for (int q = 0; q < NC; ++q) z[ti][q] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int ks = 0; ks < H / 4; ++ks) {
-            const int o = 4 * ks + g;
-            const float bw = Wt.W2t[fb + c][o];
+        for (int j = 0; j < 4; ++j) {  // output o = 16 j + 4 g + i of k-step (j, i), as in layer 2
+            float bw[4];
 #pragma unroll
-            for (int ti = 0; ti < R; ++ti) z[ti][ks % NC] = mfma16(Zt[16 * ti + c][o], bw, z[ti][ks % NC]);
+            for (int i = 0; i < 4; ++i) bw[i] = Wt.W2t[fb + c][16 * j + 4 * g + i];
+#pragma unroll
+            for (int ti = 0; ti < R; ++ti) {
+                const float4 a4 = *reinterpret_cast<const float4*>(&Zt[16 * ti + c][16 * j + 4 * g]);
+                const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) z[ti][(4 * j + i) % NC] = mfma16(av[i], bw[i], z[ti][(4 * j + i) % NC]);
+            }
         }
 #pragma unroll
         for (int ti = 0; ti < R; ++ti) {

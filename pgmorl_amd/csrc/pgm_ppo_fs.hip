@@ -47,9 +47,10 @@ namespace pgm {
 constexpr int fs_bpw(int O) { return (O + 15) / 16 + 6; }
 constexpr int fs_nb(int O) { return 4 * fs_bpw(O); }
 constexpr int fs_nown(int O, int NS) { return (fs_nb(O) + NS - 1) / NS; }  // blocks per owner (max)
-// payload: image slots [P][2][NS][2 parities][NB KiB], then parameter slots [P][2][NS][2][NOWN KiB]
+// payload: image slots [P][2][NS][2 parities][NB KiB], then parameter slots [P][2][NS][2][NOWN x 2 KiB] (room for
+// the tagged form: every value an 8-B {value, tag} granule)
 inline size_t fs_payload_bytes(int P, int O, int NS) {
-    return (size_t)P * 2 * NS * 2 * (size_t)(fs_nb(O) + fs_nown(O, NS)) * 1024;
+    return (size_t)P * 2 * NS * 2 * (size_t)(fs_nb(O) + 2 * fs_nown(O, NS)) * 1024;
 }
 // NS sized by the workspace: the largest power of two with 16 NS ceil(P/8) <= 256 (a 256-CU MI355X), at most 16
 inline int fs_ns_cap(int P) {
@@ -124,7 +125,9 @@ constexpr size_t fs_smem_bytes() {  // > 80 KiB: one workgroup per CU (the co-re
     return sizeof(FsSmem<O, A, K, R>) > 81 * 1024 ? sizeof(FsSmem<O, A, K, R>) : 81 * 1024;
 }
 
-template <int O, int A, int K, int NS, int R>
+// PTAG: the parameter hop without a flag -- owners store every new value as an 8-B {value, tag} granule (16-B stores of
+// two granules, no drain / barrier / flag), readers re-load a block until all its tags are this step's
+template <int O, int A, int K, int NS, int R, bool PTAG>
 __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
     static_assert(O <= 32 && R >= 1 && R <= 8 && (R & (R - 1)) == 0, "fs tiles");
     using Sm = FsSmem<O, A, K, R>;
@@ -137,7 +140,7 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
     constexpr int CR = RS / 4;
     constexpr int BPW = fs_bpw(O), NB = fs_nb(O), NOWN = fs_nown(O, NS);
     constexpr int OWV = (NOWN + 3) / 4;  // owned blocks per wave (block j of the part: wave j mod 4)
-    constexpr int ISB = NB * 1024, PSB = NOWN * 1024;
+    constexpr int ISB = NB * 1024, PSB = NOWN * 2048;
     constexpr bool HSPLIT = R >= 4;      // heads: row tiles split over the waves (else units + samples split)
     constexpr int NHT = HSPLIT ? R / 4 : R;
     constexpr int NC = R == 1 ? 2 : 1;   // accumulator chains per tile of the 16-deep contractions
@@ -233,13 +236,57 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
     // and written into the image during the next one, each just before its first reader: W1 + vector block before
     // layer 1, W2 before layer 2, the head block before B2 (heads read every wave's); the own part's blocks are
     // written by their owners before the parameter hand-off
-    u32x4 pv[BPW];
+    u32x4 pv[BPW], ph[PTAG ? BPW : 1];  // PTAG: pv = {p0, tag, p1, tag}, ph = {p2, tag, p3, tag}
+    auto pval = [&](int k, int r) -> float {
+        if constexpr (PTAG) {
+            const u32x4& v = r < 2 ? pv[k] : ph[k];
+            return __uint_as_float(v[2 * (r & 1)]);
+        } else {
+            return __uint_as_float(pv[k][r]);
+        }
+    };
     auto put_block = [&](int k) {  // (the own part's blocks rewrite the values their owners already wrote)
         const int b = BPW * w + k;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int ii = frag_img<O, A, K>(b, l, r, m);
-            if (ii >= 0) Pf[ii] = __uint_as_float(pv[k][r]);
+            if (ii >= 0) Pf[ii] = pval(k, r);
+        }
+    };
+    auto pload = [&](int k, int par_) {
+        const int b = BPW * w + k, h = b % NS, jj = b / NS;  // (own part's blocks too: straight-line loads)
+        if constexpr (PTAG) {
+            pv[k] = __builtin_amdgcn_raw_buffer_load_b128(xr, pslot(h, par_) + (jj * 128 + 2 * l) * 16, 0, SC1);
+            ph[k] = __builtin_amdgcn_raw_buffer_load_b128(xr, pslot(h, par_) + (jj * 128 + 2 * l + 1) * 16, 0, SC1);
+        } else {
+            pv[k] = __builtin_amdgcn_raw_buffer_load_b128(xr, pslot(h, par_) + (jj * 64 + l) * 16, 0, SC1);
+        }
+    };
+    // PTAG: until every block of this wave carries step tag `tg`, re-load the blocks that do not (bounded)
+    auto pverify = [&](unsigned tg, int par_) {
+        if constexpr (PTAG) {
+            unsigned pending = (1u << BPW) - 1;
+            for (unsigned spins = 0; pending; ++spins) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                unsigned bad = 0;
+#pragma unroll
+                for (int k = 0; k < BPW; ++k) {
+                    if (pending & (1u << k)) {
+                        const bool ok = pv[k][1] == tg && pv[k][3] == tg && ph[k][1] == tg && ph[k][3] == tg;
+                        if (__builtin_amdgcn_ballot_w64(!ok)) bad |= 1u << k;
+                    }
+                }
+                pending = bad;
+                if (!pending) break;
+                if (spins > (1u << 22) || __hip_atomic_load(fail_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                    __hip_atomic_store(fail_word, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+                for (int k = 0; k < BPW; ++k)
+                    if (pending & (1u << k)) pload(k, par_);
+            }
         }
     };
     for (int gp = 0; gp < npass; ++gp) {
@@ -249,6 +296,7 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
         auto rt = [&](int ti) { return rb + ti * 16 * RSL; };
         // ================================================================ tiles
         if (gp > 0) {
+            pverify((unsigned)gp, (gp - 1) & 1);  // the previous step's parameters (tag = its step + 1)
 #pragma unroll
             for (int k = 0; k < K1B; ++k) put_block(k);
             put_block(K1B + 5);
@@ -665,31 +713,45 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
                     ov[i][r] = vv;
                     op[i][r] = pp;
                 }
-                const u32x4 u = {__float_as_uint(op[i][0]), __float_as_uint(op[i][1]), __float_as_uint(op[i][2]),
-                                 __float_as_uint(op[i][3])};
-                __builtin_amdgcn_raw_buffer_store_b128(u, xr, pslot(hs, par) + ((w + 4 * i) * 64 + l) * 16, 0, SC1);
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int ii = frag_img<O, A, K>(b, l, r, m);
                     if (ii >= 0) Pf[ii] = op[i][r];
                 }
             }
+            // the part's owned block w + 4 i (slot position always valid: blocks past NB publish unused values, so every
+            // wave issues the same number of stores)
+            const int jj = w + 4 * i;
+            if constexpr (PTAG) {
+                const u32x4 u0 = {__float_as_uint(op[i][0]), tag, __float_as_uint(op[i][1]), tag};
+                const u32x4 u1 = {__float_as_uint(op[i][2]), tag, __float_as_uint(op[i][3]), tag};
+                __builtin_amdgcn_raw_buffer_store_b128(u0, xr, pslot(hs, par) + (jj * 128 + 2 * l) * 16, 0, SC1);
+                __builtin_amdgcn_raw_buffer_store_b128(u1, xr, pslot(hs, par) + (jj * 128 + 2 * l + 1) * 16, 0, SC1);
+            } else {
+                const u32x4 u = {__float_as_uint(op[i][0]), __float_as_uint(op[i][1]), __float_as_uint(op[i][2]),
+                                 __float_as_uint(op[i][3])};
+                __builtin_amdgcn_raw_buffer_store_b128(u, xr, pslot(hs, par) + (jj * 64 + l) * 16, 0, SC1);
+            }
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // + the row DMA issued during the image poll
-        lds_sync_m();
-        if (t == 0)
-            __hip_atomic_store(gran(2, m, hs, par), (unsigned long long)tag << 32, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        if (w == 0 && l < NS && l != hs) spin(gran(2, m, l, par));
-        lds_sync_m();  // every part's blocks published; the next minibatch's rows landed
+        if constexpr (PTAG) {
+            // no drain: only the row DMA issued during the image poll must have landed (it is older than the 2 OWV
+            // stores just issued), for every wave, before the next step reads the rows
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * OWV) : "memory");
+            lds_sync_m();
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // + the row DMA issued during the image poll
+            lds_sync_m();
+            if (t == 0)
+                __hip_atomic_store(gran(2, m, hs, par), (unsigned long long)tag << 32, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            if (w == 0 && l < NS && l != hs) spin(gran(2, m, l, par));
+            lds_sync_m();  // every part's blocks published; the next minibatch's rows landed
+        }
         PGM_STAMP(9);
         // ---- the other parts' new blocks of this wave's feature block: loads in flight into the next step
         if (gp + 1 < npass) {
 #pragma unroll
-            for (int k = 0; k < BPW; ++k) {
-                const int b = BPW * w + k, h = b % NS, jj = b / NS;  // (own part's blocks too: straight-line loads)
-                pv[k] = __builtin_amdgcn_raw_buffer_load_b128(xr, pslot(h, par) + (jj * 64 + l) * 16, 0, SC1);
-            }
+            for (int k = 0; k < BPW; ++k) pload(k, par);
         }
         PGM_STAMP(10);
     }
@@ -729,7 +791,8 @@ static int launch_fs_k(const pgm_dims* d, const MArgs& a, hipStream_t stream) {
         set_error("pgm_ppo_update (fs): LDS %zu bytes exceeds 160 KiB", smem);
         return PGM_E_UNSUPPORTED;
     }
-    auto kern = ppo_update_fs_kernel<O, A, K, NS, R>;
+    const char* pt = getenv("PGM_FS_PTAG");
+    auto kern = pt && pt[0] == '1' ? ppo_update_fs_kernel<O, A, K, NS, R, true> : ppo_update_fs_kernel<O, A, K, NS, R, false>;
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update (fs)");
     const int grid = fs_grid(d->P, NS);
@@ -748,7 +811,10 @@ static int launch_fs_k(const pgm_dims* d, const MArgs& a, hipStream_t stream) {
 int fs_choose_ns(const pgm_dims* d, int mb) {
     if (d->O > 32) return 0;
     const int cus = device_cu_count();
+    const char* cap = getenv("PGM_FS_NS");  // A/B: at most this many parts per tower
+    const int nmax = cap && atoi(cap) >= 2 ? atoi(cap) : 16;
     for (int ns = fs_ns_cap(d->P); ns >= 2; ns >>= 1) {
+        if (ns > nmax) continue;
         if (fs_grid(d->P, ns) > cus || mb % (16 * ns) != 0) continue;
         const int R = mb / (16 * ns);
         if (R >= 1 && R <= 8 && (R & (R - 1)) == 0) return ns;

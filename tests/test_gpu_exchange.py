@@ -27,8 +27,9 @@ DELAY = 4_000_000  # shader cycles (~2 ms): far beyond one Adam step, far below 
 
 
 def _run_update(env, P, T, N, E, M, split, delay, monkeypatch):
-    if split == 'fs':
+    if split in ('fs', 'fst'):  # fst: the tagged parameter hop
         monkeypatch.setenv('PGM_UPDATE_KERNEL', 'fs')
+        monkeypatch.setenv('PGM_FS_PTAG', '1' if split == 'fst' else '0')
     else:
         monkeypatch.setenv('PGM_UPDATE_SPLIT', split)
     if delay is not None:
@@ -88,24 +89,25 @@ def test_block_of_inverts_the_kernel_maps():
 CASES = [('2', 0, 0, 0, 0), ('2', 0, 1, 1, 0), ('2', 0, 0, 1, 1), ('2', 0, 1, 0, 1), ('2', 0, 0, 0, 2), ('2', 0, 1, 1, 2),
          ('4', 0, 0, 0, 0), ('4', 0, 1, 3, 0), ('4', 0, 1, 2, 1), ('4', 0, 0, 0, 2), ('4', 0, 1, 0, 2), ('4', 0, 0, 3, 2),
          ('fs', 0, 0, 0, 0), ('fs', 1, 1, 15, 0), ('fs', 0, 1, 7, 1), ('fs', 1, 0, 3, 2), ('fs', 0, 1, 0, 2),
-         ('fs', 1, 1, 9, 3), ('fs', 0, 0, 15, 3)]
+         ('fs', 1, 1, 9, 3), ('fs', 0, 0, 15, 3),
+         ('fst', 0, 1, 4, 3), ('fst', 1, 0, 15, 3), ('fst', 0, 0, 0, 0), ('fst', 1, 1, 8, 2)]
 
 
 @pytest.mark.parametrize('split,task,tower,part,where', CASES)
 def test_delayed_handoff_keeps_parity(gpu, split, task, tower, part, where, monkeypatch):
     # Walker, 2 tasks, mb = 256 (the single-tile specialisations of MODE 2 / t16; fs: 16 parts of one 16-row tile),
     # 4 Adam steps; the stall hits step 1 (both parities are exercised before and after it)
-    block = block_of(split, task, tower, part, 16 if split == 'fs' else 4)
+    block = block_of(split, task, tower, part, 16 if split in ('fs', 'fst') else 4)
     _run_update('MO-Walker2d-v2', 2, 256, 4, 1, 4, split, (1, block, where, DELAY), monkeypatch)
 
 
-@pytest.mark.parametrize('split', ['2', '4', 'fs'])
+@pytest.mark.parametrize('split', ['2', '4', 'fs', 'fst'])
 def test_delay_on_last_step_and_ragged_grid(gpu, split, monkeypatch):
     # Hopper-v3 (3 objectives), 5 tasks (a partial group of 8 tasks in the block map), multi-pass minibatches for
     # MODE 2 / t16 (mb = 128 with N = 2: not the single-tile path; fs: 8 parts of one tile); stall the last task's
     # actor part 0 on the last step
     P = 5
-    block = block_of(split, P - 1, 1, 0, 8 if split == 'fs' else 4)
+    block = block_of(split, P - 1, 1, 0, 8 if split in ('fs', 'fst') else 4)
     _run_update('MO-Hopper-v3', P, 128, 2, 1, 2, split, (1, block, 2, DELAY), monkeypatch)
 
 

@@ -57,8 +57,11 @@ def _check_update(env, P, N, E, M, mb, seed, entropy_coef=0.0):
                                         ('MO-Hopper-v3', 27, 4, 256),       # NS 4, R 4, 3 objectives (config 3)
                                         ('MO-Hopper-v2', 5, 1, 64),         # NS 4, R 1 (config 0)
                                         ('MO-Ant-v2', 3, 2, 128)])          # NS 8, R 1, O = 27 (two dW1 blocks)
-def test_fs_update_all_tasks(gpu, monkeypatch, env, P, N, mb):
+@pytest.mark.parametrize('ptag', ['0', '1'])
+def test_fs_update_all_tasks(gpu, monkeypatch, env, P, N, mb, ptag):
+    # ptag 1: the parameter hop as tagged {value, step} granules, readers re-loading until the tags match
     monkeypatch.setenv('PGM_UPDATE_KERNEL', 'fs')
+    monkeypatch.setenv('PGM_FS_PTAG', ptag)
     _check_update(env, P, N, E=2, M=2, mb=mb, seed=41)  # 4 Adam steps: both slot parities twice
 
 

@@ -173,6 +173,12 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
     auto pslot = [&](int h, int par) { return a.P * 2 * NS * 2 * ISB + ((((p * 2 + m) * NS + h) * 2 + par)) * PSB; };
     auto gran = [&](int kind, int mm, int h, int par) { return a.ws + fs_gran(a.P, NS, kind, p, mm, h, par); };
     unsigned long long* const fail_word = a.ws + 2 * a.P;
+    // the timed-out wait, for the host's error message: bit 0, bit 1 + site (0 image flags, 1 norm granules, 2 parameter
+    // flags, 3 tagged parameter blocks), the awaited tag in bits 8..23, the workgroup (task, tower, part) from bit 24
+    auto fail_code = [&](int site, unsigned tg) -> unsigned long long {
+        return 1ull | (2ull << site) | ((unsigned long long)(tg & 0xffff) << 8) |
+               ((unsigned long long)((p * 2 + m) * NS + hs) << 24);
+    };
 
     // ---- staging (as the 16-row kernel): the minibatch's permutation indices by 4-B LDS-DMA one minibatch
     // earlier than its rows; rows by 16-B LDS-DMA (pieces past SB * RSL re-read the last row into padding)
@@ -278,8 +284,9 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
                 }
                 pending = bad;
                 if (!pending) break;
-                if (spins > (1u << 22) || __hip_atomic_load(fail_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                    __hip_atomic_store(fail_word, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (__hip_atomic_load(fail_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+                if (spins > (1u << 22)) {
+                    __hip_atomic_store(fail_word, fail_code(3, tg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     break;
                 }
                 __builtin_amdgcn_s_sleep(1);
@@ -609,13 +616,13 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
             __hip_atomic_store(gran(0, m, hs, par), ((unsigned long long)tag << 32) | __float_as_uint(lsum_wg),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // spin on a tagged granule (bounded; a timeout marks the launch failed and every later poll skips)
-        auto spin = [&](const unsigned long long* gr) -> unsigned long long {
+        auto spin = [&](const unsigned long long* gr, int site) -> unsigned long long {
             if (__hip_atomic_load(fail_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return 0ull;
             for (unsigned spins = 0;; ++spins) {
                 const unsigned long long x = __hip_atomic_load(gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if ((unsigned)(x >> 32) == tag) return x;
                 if (spins > (1u << 26)) {
-                    __hip_atomic_store(fail_word, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(fail_word, fail_code(site, tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     return 0ull;
                 }
                 __builtin_amdgcn_s_sleep(1);
@@ -624,7 +631,7 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
         if (w == 0) {
             if (l < NS) {  // lane h polls part h's image flag (the NS - 1 polls run concurrently)
                 dbg_delay(a.dbg, gp, 1);
-                S.red[l] = l == hs ? lsum_wg : __uint_as_float((unsigned)spin(gran(0, m, l, par)));
+                S.red[l] = l == hs ? lsum_wg : __uint_as_float((unsigned)spin(gran(0, m, l, par), 0));
             }
         } else {  // the next minibatch's rows (and the one after's indices) while wave 0 polls
             if (gp + 1 < npass) issue_rows((gp + 1) & 1, (gp + 1) & 1, w - 1, 3);
@@ -674,7 +681,7 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
         if (w == 0 && l < 2 * NS) {
             dbg_delay(a.dbg, gp, 2);
             const int mm = l / NS, hh = l - mm * NS;
-            S.red[64 + l] = mm == m && hh == hs ? sq_wg : __uint_as_float((unsigned)spin(gran(1, mm, hh, par)));
+            S.red[64 + l] = mm == m && hh == hs ? sq_wg : __uint_as_float((unsigned)spin(gran(1, mm, hh, par), 1));
         }
         lds_sync_m();
         float total = 0.f;
@@ -744,7 +751,7 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
             if (t == 0)
                 __hip_atomic_store(gran(2, m, hs, par), (unsigned long long)tag << 32, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
-            if (w == 0 && l < NS && l != hs) spin(gran(2, m, l, par));
+            if (w == 0 && l < NS && l != hs) spin(gran(2, m, l, par), 2);
             lds_sync_m();  // every part's blocks published; the next minibatch's rows landed
         }
         PGM_STAMP(9);

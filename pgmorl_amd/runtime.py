@@ -122,6 +122,7 @@ class TaskBatch:
         # sticky OR of every update's exchange-timeout word (workspace word 2P, include/pgm_abi.h): a launch
         # whose spin-wait gave up produced invalid parameters; check_update() turns that into PGMError
         self.update_failed = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        self.last_fail_word = 0
         self.set_active(P)
         self.reset_stats()
 
@@ -289,17 +290,18 @@ class TaskBatch:
         Adam state are invalid); resets the sticky flag.  Synchronises with the stream (after the overlapped
         evaluation, whose stream folds the last update's flag)."""
         self.wait_eval()
-        failed = int(self.update_failed.item()) != 0
-        if failed:
+        word = int(self.update_failed.item())
+        self.last_fail_word = word  # (the OR of the timed-out launches' words: kernels may encode the wait site)
+        if word != 0:
             self.update_failed.zero_()
-        return failed
+        return word != 0
 
     def check_update(self):
         """Raise PGMError if any PPO update since the last check timed out (take_update_failed).  Call it once
         per generation or after a timed region, not per update.  Multi-GPU callers share the flag across ranks
         first (MOPGPopulation.run) so that every rank raises together."""
         if self.take_update_failed():
-            raise PGMError(UPDATE_TIMEOUT_MSG)
+            raise PGMError(f'{UPDATE_TIMEOUT_MSG} (word 0x{self.last_fail_word & (2**64 - 1):x})')
 
     def evaluate(self, ob_mean=None, ob_var=None, out=None):
         mean = self.ob_mean if ob_mean is None else ob_mean

@@ -12,11 +12,9 @@ run() {  # name, env assignment ('' = default), bench args...
   env $e timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-whole-run --no-strong "$@" > $OUT/ab_${TAG}_$n.json 2> $OUT/ab_${TAG}_$n.err || { echo BENCH $n FAILED; tail -5 $OUT/ab_${TAG}_$n.err; return 1; }
   python -c "import json;d=json.load(open('$OUT/ab_${TAG}_$n.json'));r=d['roofline'];print('$n', round(d['value']/1e6,3),'M/s', round(d['ms_per_step'],3),'ms/step', r['kernel'], round(r['avg_launch_ms'],3),'ms frac', round(r['frac'],3))"
 }
-for P in 5 10 20; do
-  run p${P}_def '' --scaling strong --tasks $P && run p${P}_ptag PGM_FS_PTAG=1 --scaling strong --tasks $P || exit 1
-done
+# the tagged parameter hop first: a timed-out exchange is a handled error (the word names the wait), not a GPU fault
+run p5_ptag PGM_FS_PTAG=1 --scaling strong --tasks 5 || echo "p5_ptag failed (handled), continuing"
+for P in 5 10 20; do run p${P}_def '' --scaling strong --tasks $P || exit 1; done
 run p5_ns8 "PGM_UPDATE_KERNEL=fs PGM_FS_NS=8" --scaling strong --tasks 5 && \
-run p5_ns8_ptag "PGM_UPDATE_KERNEL=fs PGM_FS_NS=8 PGM_FS_PTAG=1" --scaling strong --tasks 5 && \
 run p40_def '' --scaling strong --tasks 40 && run p40_fs PGM_UPDATE_KERNEL=fs --scaling strong --tasks 40 && \
-run p40_fs_ptag "PGM_UPDATE_KERNEL=fs PGM_FS_PTAG=1" --scaling strong --tasks 40 && \
-run hopper2_p5_def '' --env-name MO-Hopper-v2 --tasks 5 --num-processes 1 && run hopper2_p5_ptag PGM_FS_PTAG=1 --env-name MO-Hopper-v2 --tasks 5 --num-processes 1 || exit 1
+run hopper2_p5_def '' --env-name MO-Hopper-v2 --tasks 5 --num-processes 1 || exit 1

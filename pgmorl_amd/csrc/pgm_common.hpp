@@ -164,25 +164,32 @@ __device__ __forceinline__ float pl16_fold(float a, float b) {  // rows (0,1,2,3
     const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
+// (update_dpp with bound_ctrl set, every lane a valid source: the DPP combiner folds each into one v_add_f32_dpp)
 __device__ __forceinline__ float row_sum16(float v) {
-    v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x128, 0xf, 0xf, false));  // row_ror:8
-    v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x124, 0xf, 0xf, false));  // row_ror:4
-    v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x122, 0xf, 0xf, false));  // row_ror:2
-    v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x121, 0xf, 0xf, false));  // row_ror:1
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xf, 0xf, true));  // row_ror:8
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xf, 0xf, true));  // row_ror:4
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x122, 0xf, 0xf, true));  // row_ror:2
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x121, 0xf, 0xf, true));  // row_ror:1
     return v;
 }
+// rows (optional, 128 floats of LDS): the two reduced rows stored by every lane, so that another wave reads value i at
+// rows[(i / 4) * 64 + {0, 32, 16, 48}[i % 4]] without the readlanes
 template <int M>
-__device__ __forceinline__ void wave_sum64_multi(const float (&v)[M], float (&out)[M]) {
+__device__ __forceinline__ void wave_sum64_multi(const float (&v)[M], float (&out)[M], float* rows = nullptr) {
     static_assert(M >= 1 && M <= 8, "1..8 values");
     auto at = [&](int i) { return i < M ? v[i] : 0.f; };
+    const int ln = __lane_id();
     // level 1: pairs (0,1) (2,3) (4,5) (6,7); level 2: (s01, s23) -> rows [v0, v2, v1, v3], (s45, s67) likewise
-    const float r0 = row_sum16(pl16_fold(pl32_fold(at(0), at(1)), pl32_fold(at(2), at(3))));
+    // (a pair wholly past M is the constant 0, not a fold of zeros: the compiler does not fold the permlane of 0)
+    const float r0 = row_sum16(pl16_fold(pl32_fold(at(0), at(1)), M > 2 ? pl32_fold(at(2), at(3)) : 0.f));
     const int lane_of[4] = {0, 32, 16, 48};  // value i of a group sits in row {0, 2, 1, 3}[i]
 #pragma unroll
     for (int i = 0; i < (M < 4 ? M : 4); ++i)
         out[i] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r0), lane_of[i]));
+    if (rows) rows[ln] = r0;
     if constexpr (M > 4) {
-        const float r1 = row_sum16(pl16_fold(pl32_fold(at(4), at(5)), pl32_fold(at(6), at(7))));
+        const float r1 = row_sum16(pl16_fold(pl32_fold(at(4), at(5)), M > 6 ? pl32_fold(at(6), at(7)) : 0.f));
+        if (rows) rows[64 + ln] = r1;
 #pragma unroll
         for (int i = 4; i < M; ++i) out[i] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r1), lane_of[i - 4]));
     }

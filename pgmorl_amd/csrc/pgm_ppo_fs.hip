@@ -47,10 +47,13 @@ namespace pgm {
 constexpr int fs_bpw(int O) { return (O + 15) / 16 + 6; }
 constexpr int fs_nb(int O) { return 4 * fs_bpw(O); }
 constexpr int fs_nown(int O, int NS) { return (fs_nb(O) + NS - 1) / NS; }  // blocks per owner (max)
-// payload: image slots [P][2][NS][2 parities][NB KiB], then parameter slots [P][2][NS][2][NOWN x 2 KiB] (room for
-// the tagged form: every value an 8-B {value, tag} granule)
+// parameter-slot positions a part writes: every wave publishes the same number of blocks (ceil(NOWN / 4)), past NOWN
+// unused values, so a slot holds 4 ceil(NOWN / 4) block positions
+constexpr int fs_pslots(int O, int NS) { return 4 * ((fs_nown(O, NS) + 3) / 4); }
+// payload: image slots [P][2][NS][2 parities][NB KiB], then parameter slots [P][2][NS][2][fs_pslots x 2 KiB] (room
+// for the tagged form: every value an 8-B {value, tag} granule)
 inline size_t fs_payload_bytes(int P, int O, int NS) {
-    return (size_t)P * 2 * NS * 2 * (size_t)(fs_nb(O) + 2 * fs_nown(O, NS)) * 1024;
+    return (size_t)P * 2 * NS * 2 * (size_t)(fs_nb(O) + 2 * fs_pslots(O, NS)) * 1024;
 }
 // NS sized by the workspace: the largest power of two with 16 NS ceil(P/8) <= 256 (a 256-CU MI355X), at most 16
 inline int fs_ns_cap(int P) {
@@ -140,7 +143,7 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
     constexpr int CR = RS / 4;
     constexpr int BPW = fs_bpw(O), NB = fs_nb(O), NOWN = fs_nown(O, NS);
     constexpr int OWV = (NOWN + 3) / 4;  // owned blocks per wave (block j of the part: wave j mod 4)
-    constexpr int ISB = NB * 1024, PSB = NOWN * 2048;
+    constexpr int ISB = NB * 1024, PSB = fs_pslots(O, NS) * 2048;  // (the tagged form fills a slot: 4 OWV x 2 KiB)
     constexpr bool HSPLIT = R >= 4;      // heads: row tiles split over the waves (else units + samples split)
     constexpr int NHT = HSPLIT ? R / 4 : R;
     constexpr int NC = R == 1 ? 2 : 1;   // accumulator chains per tile of the 16-deep contractions

@@ -170,7 +170,7 @@ __device__ __forceinline__ void wave_sum64_d_multi(const double (&v)[M], double 
         out[0] = wave_sum64_d(v[0]);
     } else {
         auto at = [&](int i) { return i < M ? v[i] : 0.0; };
-        const double r = row_sum16_d(pl16_fold_d(pl32_fold_d(at(0), at(1)), pl32_fold_d(at(2), at(3))));
+        const double r = row_sum16_d(pl16_fold_d(pl32_fold_d(at(0), at(1)), M > 2 ? pl32_fold_d(at(2), at(3)) : 0.0));
         const int lane_of[4] = {0, 32, 16, 48};  // value i sits in row {0, 2, 1, 3}[i]
 #pragma unroll
         for (int i = 0; i < M; ++i) out[i] = readlane_d(r, lane_of[i]);

@@ -118,18 +118,63 @@ __device__ __forceinline__ void fmac_one(float (&acc)[NA], float v, const float 
 #define PGM_FU14 PGM_FU13 PGM_FL13
 #define PGM_FU15 PGM_FU14 PGM_FL14
 #define PGM_FU16 PGM_FU15 PGM_FL15
+// (volatile in the stamps build only: a plain asm block may move across the s_memtime stamps)
+#ifdef PGM_STAMPS
+#define PGM_ASM_Q volatile
+#else
+#define PGM_ASM_Q
+#endif
 #define PGM_FMAC_ASM(body)                                                                                       \
-    asm("s_nop 1\n\t" body                                                                                    \
+    asm PGM_ASM_Q("s_nop 1\n\t" body                                                                          \
         : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3])                                                \
         : "v"(v), "v"(wv[0]), "v"(wv[1]), "v"(wv[2]), "v"(wv[3]), "v"(wv[4]), "v"(wv[5]), "v"(wv[6]), "v"(wv[7]), \
           "v"(wv[8]), "v"(wv[9]), "v"(wv[10]), "v"(wv[11]), "v"(wv[12]), "v"(wv[13]), "v"(wv[14]), "v"(wv[15]))
-template <int NK, int NA>
+// FIRST: the layer's first row -- accumulators 1..3 start with a v_mul_f32_dpp instead of a zeroing v_mov + v_fmac
+#define PGM_FM1 "v_mul_f32_dpp %1, %4, %6 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+#define PGM_FM2 "v_mul_f32_dpp %2, %4, %7 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+#define PGM_FM3 "v_mul_f32_dpp %3, %4, %8 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+#define PGM_FMAC_ASM_FIRST(body)                                                                                 \
+    asm PGM_ASM_Q("s_nop 1\n\t" body                                                                          \
+        : "+v"(acc[0]), "=&v"(acc[1]), "=&v"(acc[2]), "=&v"(acc[3])                                             \
+        : "v"(v), "v"(wv[0]), "v"(wv[1]), "v"(wv[2]), "v"(wv[3]), "v"(wv[4]), "v"(wv[5]), "v"(wv[6]), "v"(wv[7]), \
+          "v"(wv[8]), "v"(wv[9]), "v"(wv[10]), "v"(wv[11]), "v"(wv[12]), "v"(wv[13]), "v"(wv[14]), "v"(wv[15]))
+#define PGM_FF4 PGM_FL0 PGM_FM1 PGM_FM2 PGM_FM3
+#define PGM_FF5 PGM_FF4 PGM_FL4
+#define PGM_FF6 PGM_FF5 PGM_FL5
+#define PGM_FF7 PGM_FF6 PGM_FL6
+#define PGM_FF8 PGM_FF7 PGM_FL7
+#define PGM_FF9 PGM_FF8 PGM_FL8
+#define PGM_FF10 PGM_FF9 PGM_FL9
+#define PGM_FF11 PGM_FF10 PGM_FL10
+#define PGM_FF12 PGM_FF11 PGM_FL11
+#define PGM_FF13 PGM_FF12 PGM_FL12
+#define PGM_FF14 PGM_FF13 PGM_FL13
+#define PGM_FF15 PGM_FF14 PGM_FL14
+#define PGM_FF16 PGM_FF15 PGM_FL15
+template <int NK, int NA, bool FIRST = false>
 __device__ __forceinline__ void fmac_row_bcast(float (&acc)[NA], float v, const float* w) {
     static_assert(NK >= 1 && NK <= 16, "1..16 lanes");
     float wv[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) wv[i] = i < NK ? w[i] : 0.f;
-    if constexpr (NA == 4) {
+    if constexpr (FIRST && NA == 4 && NK >= 4 && PGM_EXP != 61) {  // (61, A/B: zeroed accumulators, 2.02 vs 1.90 ms)
+        if constexpr (NK == 4) PGM_FMAC_ASM_FIRST(PGM_FF4);
+        else if constexpr (NK == 5) PGM_FMAC_ASM_FIRST(PGM_FF5);
+        else if constexpr (NK == 6) PGM_FMAC_ASM_FIRST(PGM_FF6);
+        else if constexpr (NK == 7) PGM_FMAC_ASM_FIRST(PGM_FF7);
+        else if constexpr (NK == 8) PGM_FMAC_ASM_FIRST(PGM_FF8);
+        else if constexpr (NK == 9) PGM_FMAC_ASM_FIRST(PGM_FF9);
+        else if constexpr (NK == 10) PGM_FMAC_ASM_FIRST(PGM_FF10);
+        else if constexpr (NK == 11) PGM_FMAC_ASM_FIRST(PGM_FF11);
+        else if constexpr (NK == 12) PGM_FMAC_ASM_FIRST(PGM_FF12);
+        else if constexpr (NK == 13) PGM_FMAC_ASM_FIRST(PGM_FF13);
+        else if constexpr (NK == 14) PGM_FMAC_ASM_FIRST(PGM_FF14);
+        else if constexpr (NK == 15) PGM_FMAC_ASM_FIRST(PGM_FF15);
+        else PGM_FMAC_ASM_FIRST(PGM_FF16);
+    } else if constexpr (FIRST) {
+        acc[1] = acc[2] = acc[3] = 0.f;  // (NK < 4: zeroed, then accumulated)
+        fmac_row_bcast<NK, NA, false>(acc, v, w);
+    } else if constexpr (NA == 4) {
         if constexpr (NK == 1) PGM_FMAC_ASM(PGM_FU1);
         else if constexpr (NK == 2) PGM_FMAC_ASM(PGM_FU2);
         else if constexpr (NK == 3) PGM_FMAC_ASM(PGM_FU3);
@@ -230,14 +275,16 @@ struct ActorLane {
     // the same action mean from registers: lane k < O holds input feature k (other lanes: anything).  Every input
     // reaches every lane by a row copy + row_newbcast DPP operand of the FMA (no LDS round trip, no v_readlane);
     // four accumulator chains per layer.
-    __device__ void forward_reg(float xv, int l, float (&mu)[A], float* h1row = nullptr) const {
+    // murow (optional): the head sums' two reduced rows for another wave (wave_sum64_multi rows)
+    __device__ void forward_reg(float xv, int l, float (&mu)[A], float* h1row = nullptr, float* murow = nullptr) const {
         constexpr int R1 = (O + 15) / 16;
         float X[R1];
         row_copies<R1>(xv, X);
-        float z[4] = {b1, 0.f, 0.f, 0.f};
+        float z[4];
+        z[0] = b1;
         static_for<R1>([&](auto jc) {
             constexpr int j = decltype(jc)::value;
-            fmac_row_bcast<(O - 16 * j < 16 ? O - 16 * j : 16), 4>(z, X[j], &w1[16 * j]);
+            fmac_row_bcast<(O - 16 * j < 16 ? O - 16 * j : 16), 4, j == 0>(z, X[j], &w1[16 * j]);
         });
         const float hl = tanh_fast((z[0] + z[1]) + (z[2] + z[3]));
         float h2;
@@ -271,10 +318,13 @@ struct ActorLane {
             constexpr int NA2 = PGM_EXP == 41 ? 8 : 4;  // layer-2 accumulator chains (A/B)
             float y[NA2];
             y[0] = b2;
+            if constexpr (NA2 != 4) {
 #pragma unroll
-            for (int i = 1; i < NA2; ++i) y[i] = 0.f;
+                for (int i = 1; i < NA2; ++i) y[i] = 0.f;
+            }
+            fmac_row_bcast<16, NA2, NA2 == 4>(y, Hc[0], &w2[0]);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) fmac_row_bcast<16, NA2>(y, Hc[j], &w2[16 * j]);
+            for (int j = 1; j < 4; ++j) fmac_row_bcast<16, NA2>(y, Hc[j], &w2[16 * j]);
 #pragma unroll
             for (int i = 4; i < NA2; ++i) y[i - 4] += y[i];
             h2 = tanh_fast((y[0] + y[1]) + (y[2] + y[3]));
@@ -282,7 +332,7 @@ struct ActorLane {
         float pr[A];
 #pragma unroll
         for (int j = 0; j < A; ++j) pr[j] = h2 * wm[j];
-        wave_sum64_multi<A>(pr, mu);
+        wave_sum64_multi<A>(pr, mu, murow);
 #pragma unroll
         for (int j = 0; j < A; ++j) mu[j] += bm[j];
     }
@@ -354,6 +404,12 @@ struct EnvLane {
 
 // ------------------------------------------------------------------------------------------ rollout
 constexpr int NCH = 32;  // rollout steps per staged noise chunk
+// The step's action side off the chain (default): the chain waves draw the action and step the dynamics only; the
+// objective waves redo the draw from the head sums' rows (same fp32 operations, so the same action), and own the
+// log-prob, |clip(a)|^2, the action / log-prob / mask stores.  A single wave issues at most one VALU instruction per
+// ~4 cycles, and the chain wave is the one whose instruction count sets the step time (two waves per SIMD).
+// PGM_EXP 48 (A/B): everything on the chain waves.
+#define PGM_ROLL_OBJ_SIDE (PGM_EXP != 48)
 
 template <int O, int A, int NN>
 struct LaneSmem {
@@ -364,6 +420,8 @@ struct LaneSmem {
     double e2[2][NN];                    // |clip(a)|^2 of env n, by step parity
     int dn[2][NN];                       // done of env n, by step parity
     double t2[32];                       // 2^(j/32): tanh_d3's exp table
+    double rinv[2][64];                  // the chain's merged 1 / sqrt(var + eps) per statistic lane, by step parity
+    float mur[2][NN][128];               // env n's action-mean rows (wave_sum64_multi rows), by step parity
     alignas(16) float eps[2][NN][NCH * A];  // action noise of env n for NCH steps, double-buffered
 };
 
@@ -387,11 +445,14 @@ __device__ __forceinline__ double clipd_s(double x, double lo, double hi) {
 //  * CHAIN waves (w < NW) run the observation chain: policy -> Gaussian draw -> fp64 dynamics -> time
 //    limit / auto-reset -> ob_rms merge -> next normalised input, and store obs / actions / log-probs / masks;
 //  * OBJECTIVE waves (w >= NW, env slots of wave w - NW) run everything the chain does not need: the raw
-//    objectives (fp64 wave sums of V . s'), the discounted objective / ret accumulators, the obj_rms / ret_rms
-//    merges and the rewards, reading s', |a|^2 and done from parity-buffered LDS rows after each step's
-//    barrier.  They run one step behind (step t's objective side after barrier t, its accumulators merged
-//    after barrier t + 1), so they only fill the chain waves' stall slots on the shared SIMDs.
-// Both roles execute the same barriers (one per step plus one drain).
+//    objectives (fp64 wave sums of V . s'), the discounted objective / ret accumulators and the rewards,
+//    reading s', |a|^2 and done from parity-buffered LDS rows after each step's barrier.  They run one step
+//    behind (step t's objective side after barrier t), so they only fill the chain waves' stall slots on the
+//    shared SIMDs.  The obj_rms / ret_rms merges of their accumulators (after barrier t + 1) run in the CHAIN
+//    waves' ob_rms merge, which executes all 64 statistic lanes of the row anyway: the two roles share each
+//    SIMD's issue slots, so the objective waves' own copy of that fp64 merge was pure extra issue.  The merged
+//    reciprocal std goes to LDS, and step t's reward leaves after barrier t + 2.
+// Both roles execute the same barriers (one per step plus two drain barriers).
 template <int O, int A, int K, int NN>
 __global__ __launch_bounds__(512) void rollout_lane_kernel(RolloutArgs a) {
     static_assert(lanes_fit<O, K>(), "lane roles need O + K + 1 <= 64");
@@ -432,13 +493,20 @@ __global__ __launch_bounds__(512) void rollout_lane_kernel(RolloutArgs a) {
     }
     const bool upd = role == 0 ? nc.use_ob != 0 : role == 1 ? nc.use_obj != 0 : role == 2;
     double inv = 1.0;
-    // 1 / (count + N) for the next merge: hardware reciprocal + two Newton steps, formed before the barrier
+    // 1 / (count + N) for the next merge: hardware reciprocal + two Newton steps, formed before the barrier.
+    // (Measured and dropped: the merge's old-statistics factors var cnt / tot, cnt N / tot^2, N / tot formed here too,
+    // so that var' = fma(delta^2, ., fma(sq, 1 / tot, .)) after the barrier: 1.90 -> 1.99 ms per Walker P = 40 rollout.)
     double itot = 0.0;
     auto prep_merge = [&]() {
         const double tot = cnt + (double)NN;
         double r = __builtin_amdgcn_rcp(tot);
         r = fma(r, fma(-tot, r, 1.0), r);
         itot = fma(r, fma(-tot, r, 1.0), r);
+    };
+    // 1 / sqrt(x) to ~4e-15 relative (one Newton step): the normalised observations and the rewards leave as fp32
+    auto rsqrt_1 = [](double x) {
+        const double r = __builtin_amdgcn_rsq(x);
+        return fma(r * fma(-x * r, r, 1.0), 0.5, r);
     };
     // statistics merge of this lane's role (counts from before the merge; numpy's mean / var divide by N,
     // exact for N a power of two); prep_merge() ran since the last merge
@@ -462,7 +530,8 @@ __global__ __launch_bounds__(512) void rollout_lane_kernel(RolloutArgs a) {
             mean = mean + delta * (double)NN * itot;
             var = (var * cnt + (sq * rn) * (double)NN + delta * delta * cnt * (double)NN * itot) * itot;
             cnt += (double)NN;
-            inv = rsqrt_d(var + nc.eps);
+            // PGM_EXP 62 (A/B): two Newton steps (2.02 vs 1.90 ms per Walker P = 40 rollout)
+            inv = PGM_EXP == 62 ? rsqrt_d(var + nc.eps) : rsqrt_1(var + nc.eps);
         }
     };
     if (threadIdx.x < 32) S.t2[threadIdx.x] = exp2((double)threadIdx.x / 32.0);
@@ -510,7 +579,6 @@ __global__ __launch_bounds__(512) void rollout_lane_kernel(RolloutArgs a) {
             s0_o[e] = a.st.s0[(size_t)n * O + lo];
             elapsed[e] = a.st.elapsed[p * NN + n];
         }
-        const bool upd0 = role == 0 && nc.use_ob;
 
         // ---- slot 0: after_update() carry (storage.py:71-75) and the first policy input
         float xr[NE];  // PGM_ROLL_DPP: normalised input feature l of env slot e (lanes < O), else S.x
@@ -590,6 +658,9 @@ __global__ __launch_bounds__(512) void rollout_lane_kernel(RolloutArgs a) {
                 if (step + 1 + NCH < T) load_eps((step + 1) / NCH + 1);
                 wave_lds_fence_r();
             }
+            // 1 / (count + N) of this step's merge: the counts are known since the last merge, and formed here its
+            // fp64 reciprocal and Newton steps interleave with the forward instead of stalling before the barrier
+            if constexpr (PGM_EXP != 63) prep_merge();
             float ejc[A];  // PREF: this step's noise of env slot 0 (from ejn); the next step's goes into ejn
             if constexpr (PREF) {
                 const int n = min(w, NN - 1), s1 = step + 1 < T ? step + 1 : step;
@@ -608,31 +679,42 @@ __global__ __launch_bounds__(512) void rollout_lane_kernel(RolloutArgs a) {
 #pragma unroll
                 for (int j = 0; j < A; ++j) ej[j] = PREF ? ejc[j] : S.eps[(step / NCH) & 1][n][cs * A + j];
                 float mu[A];
-                if constexpr (PGM_ROLL_DPP) pol.forward_reg(xr[e], l, mu, S.h1[w]);
+                if constexpr (PGM_EXP == 51) {  // timing ablation only (wrong results): no policy forward
+#pragma unroll
+                    for (int j = 0; j < A; ++j) mu[j] = xr[e] * 1e-3f;
+                } else if constexpr (PGM_ROLL_DPP) pol.forward_reg(xr[e], l, mu, S.h1[w], PGM_ROLL_OBJ_SIDE ? &S.mur[buf][n][0] : nullptr);
                 else pol.forward(S.x[n], S.h1[w], l, mu);
                 PGM_STAMP(1);
-                // Gaussian draw (torch.normal(mean, std) = eps * std + mean), log-prob and clipped action, all
-                // wave-uniform; lanes 0..A-1 store the action row, lane 0 its log-prob
+                // Gaussian draw (torch.normal(mean, std) = eps * std + mean) and clipped action, wave-uniform
+                // (PGM_EXP 48: also the log-prob and |clip(a)|^2 here; lanes 0..A-1 store the action row, lane 0 its
+                // log-prob)
                 float lpt[A], avs[A];
                 double ac[A], sq[A], pu[A];
 #pragma unroll
                 for (int j = 0; j < A; ++j) {
                     const float av = fmaf(ej[j], pol.sd[j], mu[j]);
-                    const float dz = (av - mu[j]) * pol.rsd[j];
-                    lpt[j] = -0.5f * dz * dz - pol.ls[j] - LOG_SQRT_2PI;
-                    avs[j] = av;
                     ac[j] = clipd_s((double)av, alo[j], ahi[j]);
-                    sq[j] = ac[j] * ac[j];
                     pu[j] = U[j] * ac[j];
+                    if constexpr (!PGM_ROLL_OBJ_SIDE) {
+                        const float dz = (av - mu[j]) * pol.rsd[j];
+                        lpt[j] = -0.5f * dz * dz - pol.ls[j] - LOG_SQRT_2PI;
+                        avs[j] = av;
+                        sq[j] = ac[j] * ac[j];
+                    }
                 }
-                // |clip(a)|^2 for the objective side, formed here (beside the tanh chain, not behind it)
-                double e2v = tree_sum(sq);
-                asm volatile("" : "+v"(e2v));
+                double e2v = 0.0;
+                if constexpr (!PGM_ROLL_OBJ_SIDE) {  // |clip(a)|^2 for the objective side
+                    e2v = tree_sum(sq);
+                    asm volatile("" : "+v"(e2v));
+                }
                 // dynamics (fp64, lane = feature): s' = tanh(d s + U clip(a) + c)
-                const double sn = tanh_d3(dd * s_o[e] + tree_sum(pu) + cc, S.t2);
-                const float lp = tree_sum(lpt);
-                store_lane(r_act, l < A ? (uint32_t)(((size_t)step * NN + n) * A + l) * 4 : OOB_OFF, sel_lane(avs, l));
-                store_lane(r_logp, l == 0 ? (uint32_t)((size_t)step * NN + n) * 4 : OOB_OFF, lp);
+                const double sn = PGM_EXP == 53 ? dd * s_o[e] + tree_sum(pu) + cc  // (53: timing ablation, no tanh)
+                                                : tanh_d3(dd * s_o[e] + tree_sum(pu) + cc, S.t2);
+                if constexpr (!PGM_ROLL_OBJ_SIDE) {
+                    const float lp = tree_sum(lpt);
+                    store_lane(r_act, l < A ? (uint32_t)(((size_t)step * NN + n) * A + l) * 4 : OOB_OFF, sel_lane(avs, l));
+                    store_lane(r_logp, l == 0 ? (uint32_t)((size_t)step * NN + n) * 4 : OOB_OFF, lp);
+                }
                 PGM_STAMP(6);
                 // time limit, auto-reset; the objective side's inputs (s', |a|^2, done) to the parity rows
                 const int el = elapsed[e] + 1;
@@ -643,18 +725,23 @@ __global__ __launch_bounds__(512) void rollout_lane_kernel(RolloutArgs a) {
                 if (role == 0) S.sr[buf][n][l] = s_o[e];  // lanes O.. of the row belong to the objective waves
                 S.sn[buf][n][l] = sn;
                 if (l == 0) {
-                    S.e2[buf][n] = e2v;
-                    S.dn[buf][n] = dn;
+                    if constexpr (!PGM_ROLL_OBJ_SIDE) S.e2[buf][n] = e2v;
+                    S.dn[buf][n] = dn | bf << 1;
                 }
-                const uint32_t moff = (uint32_t)((size_t)(step + 1) * NN + n) * 4;
-                store_lane(r_msk, l == 0 ? moff : OOB_OFF, dn ? 0.f : 1.f);
-                store_lane(r_bad, l == 0 ? moff : OOB_OFF, bf ? 0.f : 1.f);
+                if constexpr (!PGM_ROLL_OBJ_SIDE) {
+                    const uint32_t moff = (uint32_t)((size_t)(step + 1) * NN + n) * 4;
+                    store_lane(r_msk, l == 0 ? moff : OOB_OFF, dn ? 0.f : 1.f);
+                    store_lane(r_bad, l == 0 ? moff : OOB_OFF, bf ? 0.f : 1.f);
+                }
                 if (e == 0) PGM_STAMP(2);
             }
-            prep_merge();
+            if constexpr (PGM_EXP == 63) prep_merge();  // (63, A/B: formed just before the barrier)
             lds_sync();
             PGM_STAMP(3);
-            merge(buf, upd0);
+            // every statistic of the row: ob_rms (lanes < O, this step's states) and, for the objective waves, obj_rms /
+            // ret_rms (their accumulators of the previous step; nothing in step 0's row).  The chain waves execute all
+            // 64 lanes of the merge anyway; the objective waves read the reciprocal std from S.rinv a barrier later.
+            if constexpr (PGM_EXP != 52) merge(buf, role == 0 || step > 0);  // (52: timing ablation, no merge)
             PGM_STAMP(4);
             // ---- normalised fp32 obs: the next input and the rollout buffer
 #pragma unroll
@@ -669,9 +756,15 @@ __global__ __launch_bounds__(512) void rollout_lane_kernel(RolloutArgs a) {
                 store_lane(r_obs, role == 0 ? (uint32_t)(((size_t)(step + 1) * NN + n) * O + l) * 4 : OOB_OFF, f);
             }
             if constexpr (!PGM_ROLL_DPP) wave_lds_fence_r();
+            if (w == 0) S.rinv[buf][l] = inv;  // read after the next barrier (off this wave's chain)
             PGM_STAMP(5);
         }
-        lds_sync();  // the objective waves' drain merge
+        // drain: the last step's objective / ret accumulators (row T & 1), then one more barrier for their reward
+        prep_merge();  // (the counts after step T - 1's merge)
+        lds_sync();
+        merge(T & 1, role == 1 || role == 2);
+        if (w == 0) S.rinv[T & 1][l] = inv;
+        lds_sync();
         // ---- env state and observation statistics back to HBM
 #pragma unroll
         for (int e = 0; e < NE; ++e) {
@@ -680,15 +773,46 @@ __global__ __launch_bounds__(512) void rollout_lane_kernel(RolloutArgs a) {
             if (fl) a.st.s[((size_t)p * NN + n) * O + l] = s_o[e];
             if (l == 0) a.st.elapsed[p * NN + n] = elapsed[e];
         }
-        if (w == 0 && role == 0) {
-            a.ns.ob_mean[(size_t)p * O + l] = mean;
-            a.ns.ob_var[(size_t)p * O + l] = var;
-            if (l == 0) a.ns.ob_count[p] = cnt;
+        if (w == 0) {
+            if (role == 0) {
+                a.ns.ob_mean[(size_t)p * O + l] = mean;
+                a.ns.ob_var[(size_t)p * O + l] = var;
+                if (l == 0) a.ns.ob_count[p] = cnt;
+            } else if (role == 1) {
+                a.ns.obj_mean[p * K + ko] = mean;
+                a.ns.obj_var[p * K + ko] = var;
+                if (ko == 0) a.ns.obj_count[p] = cnt;
+            } else if (role == 2) {
+                a.ns.ret_mean[p] = mean;
+                a.ns.ret_var[p] = var;
+                a.ns.ret_count[p] = cnt;
+            }
         }
     } else {
         // =========================================================== objective waves
         float* rew = a.rb.rewards + (size_t)p * T * NN * K;
         const auto r_rew = out_rsrc(rew, (size_t)T * NN * K * 4);
+        const auto r_act = out_rsrc(a.rb.actions + (size_t)p * T * NN * A, (size_t)T * NN * A * 4);
+        const auto r_logp = out_rsrc(a.rb.logp + (size_t)p * T * NN, (size_t)T * NN * 4);
+        const auto r_msk = out_rsrc(masks, (size_t)(T + 1) * NN * 4);
+        const auto r_bad = out_rsrc(bad, (size_t)(T + 1) * NN * 4);
+        // the action side (PGM_ROLL_OBJ_SIDE): the policy's per-action constants as the chain's ActorLane holds them
+        float bm[A], ls[A], sd[A], rsd[A];
+        double alo[A], ahi[A];
+        {
+            const float* prm = a.params + (size_t)p * L.total;
+#pragma unroll
+            for (int j = 0; j < A; ++j) {
+                bm[j] = prm[L.off[PGM_P_MEAN_B] + j];
+                ls[j] = prm[L.off[PGM_P_LOGSTD] + j];
+                sd[j] = expf(ls[j]);
+                rsd[j] = 1.0f / sd[j];
+                alo[j] = a.spec.act_lo[j];
+                ahi[j] = a.spec.act_hi[j];
+                asm volatile("" : "+v"(bm[j]), "+v"(ls[j]), "+v"(sd[j]), "+v"(rsd[j]));
+                asm volatile("" : "+v"(alo[j]), "+v"(ahi[j]));
+            }
+        }
         double V[K], ebase[K], ecoef[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -698,7 +822,7 @@ __global__ __launch_bounds__(512) void rollout_lane_kernel(RolloutArgs a) {
             asm volatile("" : "+v"(ebase[k]));
             asm volatile("" : "+v"(ecoef[k]));
         }
-        double objacc[NE][K], ret[NE], objraw[NE][K];
+        double objacc[NE][K], ret[NE], objraw[NE][K], objprev[NE][K];
         int dprev[NE];
 #pragma unroll
         for (int e = 0; e < NE; ++e) {
@@ -707,31 +831,39 @@ __global__ __launch_bounds__(512) void rollout_lane_kernel(RolloutArgs a) {
             for (int k = 0; k < K; ++k) {
                 objacc[e][k] = a.st.obj_acc[((size_t)p * NN + n) * K + k];
                 objraw[e][k] = 0.0;
+                objprev[e][k] = 0.0;
             }
             ret[e] = a.st.ret[p * NN + n];
             dprev[e] = 0;
         }
         int obj_valid = a.st.obj_acc_valid[p];
-        const double clip_lo = -nc.cliprew, clip_hi = nc.cliprew;
+        // wave-uniform constants of the step loop in VGPRs: as SGPRs they are spilled (the NormCfg tuple) and reloaded by
+        // v_readlane every step
+        double clip_lo = -nc.cliprew, clip_hi = nc.cliprew, gam = nc.gamma;
+        asm volatile("" : "+v"(clip_lo), "+v"(clip_hi), "+v"(gam));
         const bool scale_out = nc.use_obj != 0;
-        // reward of step ts (role-1 lanes, after the merge of its accumulators): clip(obj / sqrt(var + eps))
-        auto emit_reward = [&](int e, int n, int ts) {
-            double r = sel_lane_d(objraw[e], ko);
-            if (scale_out) r = clipd_s(r * inv, clip_lo, clip_hi);
+        // reward of step ts (role-1 lanes) from its raw objectives and the reciprocal std after the merge of its
+        // accumulators: clip(obj / sqrt(var + eps))
+        auto emit_reward = [&](int n, int ts, const double (&raw)[K], double rinv) {
+            double r = sel_lane_d(raw, ko);
+            if (scale_out) r = clipd_s(r * rinv, clip_lo, clip_hi);
             store_lane(r_rew, role == 1 ? (uint32_t)((((size_t)ts * NN + n) * K + ko) * 4) : OOB_OFF, (float)r);
         };
-        // the statistics row lanes of roles 1 / 2 for the merge after barrier t + 1 (step t's accumulators);
-        // the first row (step 0's barrier) carries nothing for them (merge inactive at step 0)
+        // the statistics row lanes of roles 1 / 2 for the chain's merge after barrier t + 1 (step t's
+        // accumulators); the first row (step 0's barrier) carries nothing for them.  That merge's reciprocal std
+        // reaches S.rinv before barrier t + 2, so step t's reward leaves two steps behind.
         for (int step = 0; step < T; ++step) {
             const int buf = step & 1;
-            prep_merge();
             lds_sync();
-            merge(buf, (role == 1 || role == 2) && step > 0);
+            if constexpr (PGM_EXP == 50) continue;  // timing ablation only (wrong results): objective waves idle
+            const double rinv = S.rinv[buf ^ 1][l];  // the chain's merge after barrier step - 1
 #pragma unroll
             for (int e = 0; e < NE; ++e) {
                 const int n = w + 4 * e;
                 if (n >= NN) break;
-                if (step > 0) emit_reward(e, n, step - 1);
+                if (step > 1) emit_reward(n, step - 2, objprev[e], rinv);
+#pragma unroll
+                for (int k = 0; k < K; ++k) objprev[e][k] = objraw[e][k];
                 // objective side of step t: reset by done_{t-1}, raw objectives (wave sums), discounted
                 // accumulators (vec_normalize.py:32-45), the row of step t + 1
                 if (dprev[e]) {
@@ -740,8 +872,36 @@ __global__ __launch_bounds__(512) void rollout_lane_kernel(RolloutArgs a) {
                     ret[e] = 0.0;
                 }
                 const double sn = S.sn[buf][n][l];
-                const double e2 = S.e2[buf][n];
-                dprev[e] = S.dn[buf][n];
+                const int dnb = S.dn[buf][n];
+                double e2;
+                if constexpr (PGM_ROLL_OBJ_SIDE) {
+                    // the chain's Gaussian draw again (same fp32 operations on the same mean and noise), the log-prob,
+                    // |clip(a)|^2 and the action / log-prob / mask stores of step `step`
+                    constexpr int lane_of[4] = {0, 32, 16, 48};
+                    float lpt[A], avs[A];
+                    double sq[A];
+#pragma unroll
+                    for (int j = 0; j < A; ++j) {
+                        const float muj = S.mur[buf][n][(j >> 2) * 64 + lane_of[j & 3]] + bm[j];
+                        const float ej = S.eps[(step / NCH) & 1][n][(step % NCH) * A + j];
+                        const float av = fmaf(ej, sd[j], muj);
+                        const float dz = (av - muj) * rsd[j];
+                        lpt[j] = -0.5f * dz * dz - ls[j] - LOG_SQRT_2PI;
+                        avs[j] = av;
+                        const double ac = clipd_s((double)av, alo[j], ahi[j]);
+                        sq[j] = ac * ac;
+                    }
+                    e2 = tree_sum(sq);
+                    const float lp = tree_sum(lpt);
+                    store_lane(r_act, l < A ? (uint32_t)(((size_t)step * NN + n) * A + l) * 4 : OOB_OFF, sel_lane(avs, l));
+                    store_lane(r_logp, l == 0 ? (uint32_t)((size_t)step * NN + n) * 4 : OOB_OFF, lp);
+                    const uint32_t moff = (uint32_t)((size_t)(step + 1) * NN + n) * 4;
+                    store_lane(r_msk, l == 0 ? moff : OOB_OFF, (dnb & 1) ? 0.f : 1.f);
+                    store_lane(r_bad, l == 0 ? moff : OOB_OFF, (dnb & 2) ? 0.f : 1.f);
+                } else {
+                    e2 = S.e2[buf][n];
+                }
+                dprev[e] = dnb & 1;
                 double ob[K];
 #pragma unroll
                 for (int k = 0; k < K; ++k) ob[k] = V[k] * sn;
@@ -750,23 +910,31 @@ __global__ __launch_bounds__(512) void rollout_lane_kernel(RolloutArgs a) {
                 for (int k = 0; k < K; ++k) {
                     ob[k] += ebase[k] - ecoef[k] * e2;
                     objraw[e][k] = ob[k];
-                    objacc[e][k] = obj_valid ? objacc[e][k] * nc.gamma + ob[k] : ob[k];
+                    objacc[e][k] = obj_valid ? objacc[e][k] * gam + ob[k] : ob[k];
                 }
-                ret[e] = ret[e] * nc.gamma + 0.0;  // SynthMO's scalar reward is 0 (vec_normalize.py:32)
+                ret[e] = ret[e] * gam + 0.0;  // SynthMO's scalar reward is 0 (vec_normalize.py:32)
                 const double rv = role == 1 ? sel_lane_d(objacc[e], ko) : role == 2 ? ret[e] : 0.0;
                 if (role == 1 || role == 2) S.sr[buf ^ 1][n][l] = rv;
             }
             obj_valid = 1;
         }
-        // ---- drain: merge the last step's objective / ret accumulators, its reward, the done reset
-        prep_merge();
+        // ---- drain: the reward of step T - 2 (barrier T, the chain then merges step T - 1's accumulators), the done
+        // reset, the reward of step T - 1 (barrier T + 1)
         lds_sync();
-        merge(T & 1, role == 1 || role == 2);
+        const double rinv_a = S.rinv[(T - 1) & 1][l];
 #pragma unroll
         for (int e = 0; e < NE; ++e) {
             const int n = w + 4 * e;
             if (n >= NN) break;
-            emit_reward(e, n, T - 1);
+            if (T > 1) emit_reward(n, T - 2, objprev[e], rinv_a);
+        }
+        lds_sync();
+        const double rinv_b = S.rinv[T & 1][l];
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+            const int n = w + 4 * e;
+            if (n >= NN) break;
+            emit_reward(n, T - 1, objraw[e], rinv_b);
             if (dprev[e]) {
 #pragma unroll
                 for (int k = 0; k < K; ++k) objacc[e][k] = 0.0;
@@ -775,18 +943,7 @@ __global__ __launch_bounds__(512) void rollout_lane_kernel(RolloutArgs a) {
             if (l < K) a.st.obj_acc[((size_t)p * NN + n) * K + l] = sel_lane_d(objacc[e], l);
             if (l == 0) a.st.ret[p * NN + n] = ret[e];
         }
-        if (w == 0) {
-            if (role == 1) {
-                a.ns.obj_mean[p * K + ko] = mean;
-                a.ns.obj_var[p * K + ko] = var;
-                if (ko == 0) a.ns.obj_count[p] = cnt;
-            } else if (role == 2) {
-                a.ns.ret_mean[p] = mean;
-                a.ns.ret_var[p] = var;
-                a.ns.ret_count[p] = cnt;
-                a.st.obj_acc_valid[p] = obj_valid;
-            }
-        }
+        if (w == 0 && l == 0) a.st.obj_acc_valid[p] = obj_valid;
     }
     PGM_STAMP_FLUSH;
 }

@@ -118,7 +118,7 @@ def test_update_workspace_covers_every_split(env, P, N, T):
     tower): tagged granules (the row-split updates' norm granules, 2 towers x 4 parts x 2 step parities x P + 1, then
     from granule 16 P + 8 the feature-split update's [3 kinds][P][2 towers][<= 16 parts][2 parities]; 256-B padded),
     exchange slots [P][2 towers][4 parts][2 parities], and the packed sample table + the feature-split payload
-    (obs_dim <= 32: [P][2][NS][2] image slots of NB KiB and parameter slots of 2 ceil(NB / NS) KiB, NS the largest
+    (obs_dim <= 32: [P][2][NS][2] image slots of NB KiB and parameter slots of 8 ceil(ceil(NB / NS) / 4) KiB, NS the largest
     power of two <= 16 with 16 NS ceil(P / 8) <= 256, NB = 4 (ceil(O / 16) + 6)) or the parts' private parameter
     rows (wide)."""
     from pgmorl_amd import envspec
@@ -137,7 +137,7 @@ def test_update_workspace_covers_every_split(env, P, N, T):
         while ns > 1 and 16 * ns * -(-P // 8) > 256:
             ns //= 2
         nb = 4 * (-(-O // 16) + 6)
-        fs = P * 2 * ns * 2 * (nb + 2 * -(-nb // ns)) * 1024 if ns >= 2 else 0
+        fs = P * 2 * ns * 2 * (nb + 2 * 4 * -(-(-(-nb // ns)) // 4)) * 1024 if ns >= 2 else 0
         want = flags + P * 2 * 4 * 2 * xslot * 8 + P * T * N * rs * 4 + fs
     else:
         img = H * (H + 1) + Q * H + 2 * H + Q + A

@@ -510,7 +510,7 @@ def main():
     # the fixed population split over the ranks (pop 40 -> 40 / 20 / 10 / 5 per GPU), measured in the
     # same run: the strong-scaling curve the north star targets (>= 6x at 1 -> 8), beside the weak headline
     strong = None
-    if not args.no_strong and args.scaling == 'weak':
+    if not args.no_strong and args.scaling == 'weak' and world > 1:
         sblocks = [task_block(args.strong_tasks, r, world) for r in range(world)]
         sl = main_leg if sblocks == blocks else leg(args, spec, dev, rank, world, sblocks, 'strong')
         strong = {'global_tasks': args.strong_tasks, 'tasks_per_rank': [b - a for a, b in sblocks],

@@ -41,7 +41,8 @@ def main():
         w = sum(write.get(name, [0])) / max(1, len(write.get(name, [])))
         kernels[name] = {'launches': len(fetch.get(name, [])), 'fetch_bytes_raw': f, 'fetch_bytes': 2 * f,
                          'write_bytes': w, 'hbm_bytes_per_launch': 2 * f + w}
-    upd = [k for k in kernels if 'ppo_update_' in k]
+    # the update kernel of the workload: the one launched most (a second variant can only come from another leg)
+    upd = sorted((k for k in kernels if 'ppo_update_' in k), key=lambda k: (-kernels[k]['launches'], k))
     env, P, N = opt('--env-name', 'MO-Walker2d-v2'), opt('--tasks', '40'), opt('--num-processes', '4')
     T, E, M = opt('--num-steps', '2048'), opt('--ppo-epoch', '10'), opt('--num-mini-batch', '32')
     out = {'workload': f'{env}/P{P}/N{N}/T{T}/E{E}/M{M}',

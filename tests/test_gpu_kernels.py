@@ -279,7 +279,10 @@ def _teacher_forced_check(tb, p, pol, spec, s0, noise):
 @pytest.mark.parametrize('env,N,T', [('MO-Hopper-v2', 4, 48), ('MO-Walker2d-v2', 2, 520), ('MO-Hopper-v3', 6, 40),
                                      ('MO-Hopper-v3', 8, 40), ('MO-Walker2d-v2', 1, 33), ('MO-Ant-v2', 4, 24),
                                      ('MO-Humanoid-v2', 8, 40), ('MO-Humanoid-v2', 8, 1003), ('MO-Humanoid-v2', 4, 33),
-                                     ('MO-Humanoid-v2', 2, 20), ('MO-Humanoid-v2', 1, 70)])
+                                     ('MO-Humanoid-v2', 2, 20), ('MO-Humanoid-v2', 1, 70),
+                                     # T = 1, 2, 3: the objective waves' rewards leave two steps behind the chain,
+                                     # so these runs end inside the drain
+                                     ('MO-Walker2d-v2', 4, 1), ('MO-Walker2d-v2', 4, 2), ('MO-Hopper-v3', 8, 3)])
 def test_rollout(gpu, env, N, T, kernel, monkeypatch):
     # lanes: one wave per env + batched critic values (default for N in 1/2/4/8; obs_dim > 48 takes the wide
     # kernel: k-sliced layer 1 over 4 waves, feature-per-lane dynamics); block: workgroup per step.
@@ -312,6 +315,36 @@ def test_rollout(gpu, env, N, T, kernel, monkeypatch):
         np.testing.assert_array_equal(tb.masks[p].cpu().numpy(), ro.masks[..., 0].numpy())
         np.testing.assert_array_equal(tb.bad_masks[p].cpu().numpy(), ro.bad_masks[..., 0].numpy())
         _close(tb.obj_var[p].cpu(), envs.obj_rms.var, 0, 1e-6, 'obj_rms.var')
+
+
+@pytest.mark.parametrize('env,N,T', [('MO-Walker2d-v2', 4, 2), ('MO-Hopper-v3', 4, 1), ('MO-Walker2d-v2', 2, 37)])
+def test_rollout_carry_short(gpu, env, N, T):
+    """Consecutive rollouts with the after_update carry (storage.py:71-75) at short T: the objective / ret
+    accumulators, their running statistics and the done resets cross every launch boundary, and the rewards of a
+    launch's last two steps leave in the kernel's drain (two steps behind the chain)."""
+    P, R = 2, 4
+    spec, tb, pols = _batch_with_policies(env, P, N, T, seed=9, scale=0.05)
+    s0 = envspec.reset_table(spec['obs_dim'], 0, N)
+    noise = torch.randn(R, T, N, spec['act_dim'], generator=torch.Generator().manual_seed(10), dtype=torch.float64)
+    tb.env_reset()
+    dev = []
+    for r in range(R):
+        tb.rollout(r, noise=noise[r].float(), carry=r > 0)
+        dev.append({k: getattr(tb, k).cpu().clone() for k in ('obs', 'rewards', 'masks', 'bad_masks')})
+    for p in range(P):
+        envs = VecNormalizedSynth(spec, s0, 0.995)
+        ro = oppo.RolloutStorage(T, N, spec['obs_dim'], spec['act_dim'], spec['obj_num'])
+        ro.obs[0].copy_(torch.from_numpy(envs.reset()).double())
+        for r in range(R):
+            if r > 0:
+                ro.after_update()
+            _oracle_rollout(pols[p], envs, ro, noise[r].float().double())
+            _close(dev[r]['obs'][p], ro.obs, 5e-5, 1e-4, f'obs (rollout {r})')
+            _close(dev[r]['rewards'][p], ro.rewards, 5e-5, 1e-4, f'rewards (rollout {r})')
+            np.testing.assert_array_equal(dev[r]['masks'][p].numpy(), ro.masks[..., 0].numpy())
+            np.testing.assert_array_equal(dev[r]['bad_masks'][p].numpy(), ro.bad_masks[..., 0].numpy())
+        _close(tb.obj_var[p].cpu(), envs.obj_rms.var, 0, 1e-6, 'obj_rms.var')
+        _close(tb.ob_var[p].cpu(), envs.ob_rms.var, 1e-9, 1e-6, 'ob_rms.var')
 
 
 def test_rollout_perf_rng_equals_explicit_noise(gpu):

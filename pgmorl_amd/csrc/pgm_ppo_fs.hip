@@ -55,11 +55,12 @@ constexpr int fs_pslots(int O, int NS) { return 4 * ((fs_nown(O, NS) + 3) / 4); 
 inline size_t fs_payload_bytes(int P, int O, int NS) {
     return (size_t)P * 2 * NS * 2 * (size_t)(fs_nb(O) + 2 * fs_pslots(O, NS)) * 1024;
 }
-// NS sized by the workspace: the largest power of two with 16 NS ceil(P/8) <= 256 (a 256-CU MI355X), at most 16
+// NS sized by the workspace: the largest power of two with 16 NS ceil(P/8) <= 512 (a 256-CU MI355X with two
+// workgroups per CU where R <= 2 lets them share one, fs_choose_ns), at most 16
 inline int fs_ns_cap(int P) {
     const int groups = (P + 7) / 8;
     int ns = 16;
-    while (ns > 1 && 16 * ns * groups > 256) ns >>= 1;
+    while (ns > 1 && 16 * ns * groups > 512) ns >>= 1;
     return ns;
 }
 inline int fs_grid(int P, int NS) { return 16 * NS * ((P + 7) / 8); }
@@ -105,7 +106,8 @@ struct FsSmem {
     static constexpr int SB = 16 * R;                          // rows of this part per minibatch
     static constexpr int NDT = (SB * RSL + 255) / 256;         // 1-KiB LDS-DMA pieces per staged pass
     static constexpr int SBI = 64 * ((SB + 63) / 64);          // index slots (one 64-lane DMA per wave)
-    static constexpr bool ZA = R >= 8;                         // dZ2 tile aliases the H2 tile (LDS budget)
+    // dZ2 tile aliases the H2 tile (LDS budget: R = 8 for 160 KiB; R = 2 to stay under 80 KiB, two workgroups per CU)
+    static constexpr bool ZA = R >= 8 || R == 2;
     static constexpr int NHP = R >= 4 ? 1 : 4;                 // partial head outputs (R < 4: one tile per wave)
     TowerImg<O, A, K> Pm;                                      // parameters (working copy of every part)
     alignas(16) float RB[2][NDT * 256];                        // packed rows of this / the next minibatch
@@ -123,9 +125,11 @@ struct FsSmem {
     float aiv[A];                                              // actor 1 / std^2
     float red[192];  // [0, 64) head-bias partials / poll results, [64, 128) logstd partials / norms, 128+ loss sums
 };
+// one workgroup per CU: padded past 80 KiB (the placement the launcher's grid assumes); dual (two per CU, 16 NS ceil(P/8)
+// > CUs): the struct itself, which must then fit 80 KiB
 template <int O, int A, int K, int R>
-constexpr size_t fs_smem_bytes() {  // > 80 KiB: one workgroup per CU (the co-residency argument of the launcher)
-    return sizeof(FsSmem<O, A, K, R>) > 81 * 1024 ? sizeof(FsSmem<O, A, K, R>) : 81 * 1024;
+constexpr size_t fs_smem_bytes(bool dual) {
+    return dual || sizeof(FsSmem<O, A, K, R>) > 81 * 1024 ? sizeof(FsSmem<O, A, K, R>) : 81 * 1024;
 }
 
 // PTAG: the parameter hop without a flag -- owners store every new value as an 8-B {value, tag} granule (16-B stores of
@@ -794,17 +798,24 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
     }
 }
 
+// op 0: launch (dual: two workgroups per CU); op 1: 1 if two workgroups of this kernel fit one CU (LDS and registers), else 0
 template <int O, int A, int K, int NS, int R>
-static int launch_fs_k(const pgm_dims* d, const MArgs& a, hipStream_t stream) {
-    const size_t smem = fs_smem_bytes<O, A, K, R>();
+static int launch_fs_k(const pgm_dims* d, const MArgs& a, bool dual, int op, hipStream_t stream) {
+    const size_t smem = fs_smem_bytes<O, A, K, R>(dual || op == 1);
     if (smem > 160 * 1024) {
         set_error("pgm_ppo_update (fs): LDS %zu bytes exceeds 160 KiB", smem);
-        return PGM_E_UNSUPPORTED;
+        return op == 1 ? 0 : PGM_E_UNSUPPORTED;
     }
     const char* pt = getenv("PGM_FS_PTAG");
     auto kern = pt && pt[0] == '1' ? ppo_update_fs_kernel<O, A, K, NS, R, true> : ppo_update_fs_kernel<O, A, K, NS, R, false>;
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update (fs)");
+    if (e != hipSuccess) return op == 1 ? 0 : hip_fail(e, "pgm_ppo_update (fs)");
+    if (op == 1) {
+        int per_cu = 0;
+        if (smem > 80 * 1024 || hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, 256, smem) != hipSuccess)
+            return 0;
+        return per_cu >= 2 ? 1 : 0;
+    }
     const int grid = fs_grid(d->P, NS);
     if (int rc = check_coresident((const void*)kern, 256, smem, grid, "pgm_ppo_update (fs)")) return rc;
     const size_t zb = ppo_flag_bytes(d->P);  // norm / flag granules (the payload needs no reset: tags order it)
@@ -816,28 +827,46 @@ static int launch_fs_k(const pgm_dims* d, const MArgs& a, hipStream_t stream) {
     return launch_status("pgm_ppo_update (fs)");
 }
 
+int ppo_update_fs_op(const pgm_dims* d, const MArgs& a, int ns, bool dual, int op, hipStream_t stream);
+
 // NS parts per tower for this launch: the workspace cap, the device's CUs, mb divisible into 16-row tiles of at most
-// 8 per part; 0 = the feature-split update does not apply
-int fs_choose_ns(const pgm_dims* d, int mb) {
+// 8 per part; 0 = the feature-split update does not apply.  *dual = 1: the grid (16 NS ceil(P/8) workgroups) exceeds
+// the CU count and runs two workgroups per CU, taken for R = 2 where both fit one CU (<= 80 KiB LDS, <= 256
+// registers): a step's three hand-offs then overlap the other workgroup's tiles (HalfCheetah P = 20: NS 4, R 4
+// 4.45 ms -> NS 8, R 2 4.01 ms; profiles/r04r_fs_dual_ab.json).  PGM_FS_DUAL=0 (A/B): one per CU only.
+int fs_choose_ns(const pgm_dims* d, int mb, int* dual) {
+    *dual = 0;
     if (d->O > 32) return 0;
     const int cus = device_cu_count();
     const char* cap = getenv("PGM_FS_NS");  // A/B: at most this many parts per tower
     const int nmax = cap && atoi(cap) >= 2 ? atoi(cap) : 16;
+    const char* dsel = getenv("PGM_FS_DUAL");
+    const bool dual_ok = !(dsel && dsel[0] == '0');
     for (int ns = fs_ns_cap(d->P); ns >= 2; ns >>= 1) {
         if (ns > nmax) continue;
-        if (fs_grid(d->P, ns) > cus || mb % (16 * ns) != 0) continue;
+        if (mb % (16 * ns) != 0) continue;
         const int R = mb / (16 * ns);
-        if (R >= 1 && R <= 8 && (R & (R - 1)) == 0) return ns;
+        if (R < 1 || R > 8 || (R & (R - 1)) != 0) continue;
+        const int grid = fs_grid(d->P, ns);
+        if (grid <= cus) return ns;
+        if (dual_ok && R == 2 && grid <= 2 * cus) {  // (R 4 -> 2 pays; R 2 -> 1 does not: Walker P = 10 3.18 -> 3.70 ms)
+            MArgs q{};
+            q.hp.num_mini_batch = d->T * d->N / mb;
+            if (ppo_update_fs_op(d, q, ns, true, 1, nullptr) == 1) {
+                *dual = 1;
+                return ns;
+            }
+        }
     }
     return 0;
 }
 
 template <int O, int A, int K, int NS>
-static int launch_fs_ns(const pgm_dims* d, const MArgs& a, int R, hipStream_t stream) {
+static int launch_fs_ns(const pgm_dims* d, const MArgs& a, int R, bool dual, int op, hipStream_t stream) {
     // minibatches of 64 / 128 / 256 / 512 rows (N = 1 / 2 / 4 / 8 at T = 2048, M = 32): 16 NS R = mb
     auto one = [&](auto rc) -> int {
         constexpr int RR = decltype(rc)::value, MB = 16 * NS * RR;
-        if constexpr (MB == 64 || MB == 128 || MB == 256 || MB == 512) return launch_fs_k<O, A, K, NS, RR>(d, a, stream);
+        if constexpr (MB == 64 || MB == 128 || MB == 256 || MB == 512) return launch_fs_k<O, A, K, NS, RR>(d, a, dual, op, stream);
         set_error("pgm_ppo_update (fs): minibatch of %d rows unsupported", MB);
         return PGM_E_UNSUPPORTED;
     };
@@ -852,7 +881,10 @@ static int launch_fs_ns(const pgm_dims* d, const MArgs& a, int R, hipStream_t st
 }
 
 // called by pgm_ppo_mfma.hip's launcher after the sample table is packed
-int ppo_update_fs(const pgm_dims* d, const MArgs& a, int ns, hipStream_t stream) {
+int ppo_update_fs(const pgm_dims* d, const MArgs& a, int ns, bool dual, hipStream_t stream) {
+    return ppo_update_fs_op(d, a, ns, dual, 0, stream);
+}
+int ppo_update_fs_op(const pgm_dims* d, const MArgs& a, int ns, bool dual, int op, hipStream_t stream) {
     const int mb = d->T * d->N / a.hp.num_mini_batch;
     const int R = mb / (16 * ns);
     return dispatch_dims(d->O, d->A, d->K, "pgm_ppo_update (fs)", [&](auto o, auto aa, auto k) -> int {
@@ -863,13 +895,13 @@ int ppo_update_fs(const pgm_dims* d, const MArgs& a, int ns, hipStream_t stream)
         constexpr bool skip = false;
 #endif
         if constexpr (O > 32 || skip) {
-            return PGM_E_UNSUPPORTED;
+            return op == 1 ? 0 : PGM_E_UNSUPPORTED;
         } else {
             switch (ns) {
-                case 2: return launch_fs_ns<O, A, K, 2>(d, a, R, stream);
-                case 4: return launch_fs_ns<O, A, K, 4>(d, a, R, stream);
-                case 8: return launch_fs_ns<O, A, K, 8>(d, a, R, stream);
-                case 16: return launch_fs_ns<O, A, K, 16>(d, a, R, stream);
+                case 2: return launch_fs_ns<O, A, K, 2>(d, a, R, dual, op, stream);
+                case 4: return launch_fs_ns<O, A, K, 4>(d, a, R, dual, op, stream);
+                case 8: return launch_fs_ns<O, A, K, 8>(d, a, R, dual, op, stream);
+                case 16: return launch_fs_ns<O, A, K, 16>(d, a, R, dual, op, stream);
             }
             set_error("pgm_ppo_update (fs): NS=%d unsupported", ns);
             return PGM_E_UNSUPPORTED;

@@ -2065,8 +2065,8 @@ int launch_mode(const pgm_dims* d, const MArgs& a, hipStream_t stream) {
     return launch_mode_k<O, A, K, MODE, false>(d, a, stream);
 }
 
-int fs_choose_ns(const pgm_dims* d, int mb);
-int ppo_update_fs(const pgm_dims* d, const MArgs& a, int ns, hipStream_t stream);
+int fs_choose_ns(const pgm_dims* d, int mb, int* dual);
+int ppo_update_fs(const pgm_dims* d, const MArgs& a, int ns, bool dual, hipStream_t stream);
 
 // Which obs_dim <= 32 update runs (one rule for the launcher and pgm_ppo_update_variant):
 //   * feature-split with the reduce-scattered Adam (pgm_ppo_fs.hip) while it gets >= FS_AUTO_NS parts per tower
@@ -2079,29 +2079,31 @@ int ppo_update_fs(const pgm_dims* d, const MArgs& a, int ns, hipStream_t stream)
 // row-split kernels.
 constexpr int FS_AUTO_NS = 4;
 struct UpdateChoice {
-    int kind;  // 0 = MODE (mode), 1 = t16 (ns, w), 2 = feature-split (ns)
-    int ns, w, mode;
+    int kind;  // 0 = MODE (mode), 1 = t16 (ns, w), 2 = feature-split (ns, dual: two workgroups per CU)
+    int ns, w, mode, dual;
 };
 static UpdateChoice choose_update(const pgm_dims* d, int mb) {
     const char* ksel = getenv("PGM_UPDATE_KERNEL");
     const char* sel = getenv("PGM_UPDATE_SPLIT");
     const bool force_fs = ksel && ksel[0] == 'f' && ksel[1] == 's';
     const bool auto_k = !sel && (!ksel || !ksel[0] || (ksel[0] == 'a' && ksel[1] == 'u'));
-    const int fs_ns = fs_choose_ns(d, mb);
-    if (fs_ns > 0 && (force_fs || (auto_k && fs_ns >= FS_AUTO_NS))) return {2, fs_ns, 4, 0};
+    int fs_dual = 0;
+    const int fs_ns = fs_choose_ns(d, mb, &fs_dual);
+    if (fs_ns > 0 && (force_fs || (auto_k && fs_ns >= FS_AUTO_NS))) return {2, fs_ns, 4, 0, fs_dual};
     const int cap = sel && sel[0] >= '0' && sel[0] <= '4' ? sel[0] - '0' : 4;
     const int cus = device_cu_count();
-    if (cap >= 4 && t16_grid(d->P, 4) <= cus) return {1, 4, 4, 0};
-    if (cap == 3 && t16_grid(d->P, 2) <= cus) return {1, 2, 8, 0};
-    if (cap >= 2 && mode2_grid(d->P) <= cus) return {0, 2, 4, 2};
-    if (cap >= 1 && 2 * d->P <= cus) return {0, 1, 4, 1};
-    return {0, 1, 4, 0};
+    if (cap >= 4 && t16_grid(d->P, 4) <= cus) return {1, 4, 4, 0, 0};
+    if (cap == 3 && t16_grid(d->P, 2) <= cus) return {1, 2, 8, 0, 0};
+    if (cap >= 2 && mode2_grid(d->P) <= cus) return {0, 2, 4, 2, 0};
+    if (cap >= 1 && 2 * d->P <= cus) return {0, 1, 4, 1, 0};
+    return {0, 1, 4, 0, 0};
 }
 
 int describe_update_mfma(const pgm_dims* d, const pgm_ppo_hparams* hp, char* buf, int n) {
     const int mb = d->T * d->N / hp->num_mini_batch;
     const UpdateChoice c = choose_update(d, mb);
-    if (c.kind == 2) return snprintf(buf, n, "ppo_update_fs_kernel (NS=%d, R=%d)", c.ns, mb / (16 * c.ns));
+    if (c.kind == 2)
+        return snprintf(buf, n, "ppo_update_fs_kernel (NS=%d, R=%d%s)", c.ns, mb / (16 * c.ns), c.dual ? ", 2 per CU" : "");
     if (c.kind == 1) return snprintf(buf, n, "ppo_update_t16_kernel (NS=%d, W=%d)", c.ns, c.w);
     return snprintf(buf, n, "ppo_update_mfma_kernel (MODE %d)", c.mode);
 }
@@ -2121,7 +2123,7 @@ int launch_ppo_update_mfma(const pgm_dims* d, const MArgs& a, const pgm_rollout_
     // per lane), so the grid must fit the CU count (choose_update)
     static_assert(sizeof(MSmem<O, A, K, true>) > 80 * 1024, "split residency argument needs > 80 KiB LDS");
     const UpdateChoice c = choose_update(d, d->T * d->N / a.hp.num_mini_batch);
-    if (c.kind == 2) return ppo_update_fs(d, a, c.ns, stream);
+    if (c.kind == 2) return ppo_update_fs(d, a, c.ns, c.dual != 0, stream);
     if (c.kind == 1) return c.ns == 4 ? launch_t16<O, A, K, 4, 4>(d, a, stream) : launch_t16<O, A, K, 2, 8>(d, a, stream);
     if (c.mode == 2) return launch_mode<O, A, K, 2>(d, a, stream);
     if (c.mode == 1) return launch_mode<O, A, K, 1>(d, a, stream);

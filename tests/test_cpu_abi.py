@@ -119,7 +119,7 @@ def test_update_workspace_covers_every_split(env, P, N, T):
     from granule 16 P + 8 the feature-split update's [3 kinds][P][2 towers][<= 16 parts][2 parities]; 256-B padded),
     exchange slots [P][2 towers][4 parts][2 parities], and the packed sample table + the feature-split payload
     (obs_dim <= 32: [P][2][NS][2] image slots of NB KiB and parameter slots of 8 ceil(ceil(NB / NS) / 4) KiB, NS the largest
-    power of two <= 16 with 16 NS ceil(P / 8) <= 256, NB = 4 (ceil(O / 16) + 6)) or the parts' private parameter
+    power of two <= 16 with 16 NS ceil(P / 8) <= 512, NB = 4 (ceil(O / 16) + 6)) or the parts' private parameter
     rows (wide)."""
     from pgmorl_amd import envspec
     spec = envspec.make_spec(env)
@@ -134,7 +134,7 @@ def test_update_workspace_covers_every_split(env, P, N, T):
         n = O + A + 2 + 2 * K
         rs = 16 if n <= 16 else 32 if n <= 32 else 64 if n <= 64 else 128
         ns = 16
-        while ns > 1 and 16 * ns * -(-P // 8) > 256:
+        while ns > 1 and 16 * ns * -(-P // 8) > 512:  # two workgroups per CU where they fit (fs_choose_ns)
             ns //= 2
         nb = 4 * (-(-O // 16) + 6)
         fs = P * 2 * ns * 2 * (nb + 2 * 4 * -(-(-(-nb // ns)) // 4)) * 1024 if ns >= 2 else 0

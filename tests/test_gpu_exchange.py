@@ -111,6 +111,15 @@ def test_delay_on_last_step_and_ragged_grid(gpu, split, monkeypatch):
     _run_update('MO-Hopper-v3', P, 128, 2, 1, 2, split, (1, block, 2, DELAY), monkeypatch)
 
 
+@pytest.mark.parametrize('task,tower,part,where', [(19, 1, 7, 1), (0, 0, 0, 3), (13, 1, 4, 2), (8, 0, 3, 0)])
+def test_delay_two_workgroups_per_cu(gpu, task, tower, part, where, monkeypatch):
+    # Walker P = 20 with 8 parts per tower of two 16-row tiles: 384 workgroups, two per CU where they share one
+    # (fs_choose_ns dual); a stalled workgroup may share its CU with another task's part while its partners spin
+    monkeypatch.setenv('PGM_FS_DUAL', '1')
+    block = block_of('fs', task, tower, part, 8)
+    _run_update('MO-Walker2d-v2', 20, 256, 4, 1, 4, 'fs', (1, block, where, DELAY), monkeypatch)
+
+
 def test_coresidency_check_refuses_an_oversized_grid(gpu, monkeypatch):
     """The launcher refuses (PGM_E_UNSUPPORTED -> PGMError) a grid whose workgroups cannot all be resident:
     PGM_TEST_RESIDENT_CUS pretends the device has fewer CUs than the grid's workgroups (one per CU)."""

@@ -49,20 +49,34 @@ def _check_update(env, P, N, E, M, mb, seed, entropy_coef=0.0):
         _close(stats[p], st, 1e-5, 1e-4, f'{env} task {p}: loss stats')
 
 
-# (env, P, N, minibatch rows) -> the launcher's NS: 16 tasks-per-XCD-group rule (16 NS ceil(P / 8) <= 256 CUs)
-@pytest.mark.parametrize('env,P,N,mb', [('MO-Walker2d-v2', 5, 4, 256),      # NS 16, R 1 (pop 40 over 8 GPUs)
-                                        ('MO-Walker2d-v2', 10, 4, 256),     # NS 8, R 2 (pop 40 over 4 GPUs)
-                                        ('MO-HalfCheetah-v2', 20, 4, 256),  # NS 4, R 4 (config 2's per-GPU load)
-                                        ('MO-Walker2d-v2', 40, 4, 256),     # NS 2, R 8 (config 1)
-                                        ('MO-Hopper-v3', 27, 4, 256),       # NS 4, R 4, 3 objectives (config 3)
-                                        ('MO-Hopper-v2', 5, 1, 64),         # NS 4, R 1 (config 0)
-                                        ('MO-Ant-v2', 3, 2, 128)])          # NS 8, R 1, O = 27 (two dW1 blocks)
+# (env, P, N, minibatch rows, two workgroups per CU allowed) -> the launcher's NS: 16 tasks-per-XCD-group rule
+# (16 NS ceil(P / 8) <= 256 CUs, or <= 512 with two workgroups per CU where R = 2 fits one CU twice)
+@pytest.mark.parametrize('env,P,N,mb,dual', [('MO-Walker2d-v2', 5, 4, 256, '1'),     # NS 16, R 1 (pop 40 over 8 GPUs)
+                                             ('MO-Walker2d-v2', 10, 4, 256, '1'),    # NS 8, R 2 (pop 40 / 4: R 1 not doubled)
+                                             ('MO-HalfCheetah-v2', 20, 4, 256, '1'),  # NS 8, R 2, 2 per CU (config 2)
+                                             ('MO-HalfCheetah-v2', 20, 4, 256, '0'),  # NS 4, R 4
+                                             ('MO-Walker2d-v2', 40, 4, 256, '1'),    # NS 2, R 8 (config 1)
+                                             ('MO-Hopper-v3', 27, 4, 256, '1'),      # NS 8, R 2, 2 per CU, 3 objectives
+                                             ('MO-Hopper-v2', 5, 1, 64, '1'),        # NS 4, R 1 (config 0)
+                                             ('MO-Ant-v2', 3, 2, 128, '1')])         # NS 8, R 1, O = 27 (two dW1 blocks)
 @pytest.mark.parametrize('ptag', ['0', '1'])
-def test_fs_update_all_tasks(gpu, monkeypatch, env, P, N, mb, ptag):
+def test_fs_update_all_tasks(gpu, monkeypatch, env, P, N, mb, dual, ptag):
     # ptag 1: the parameter hop as tagged {value, step} granules, readers re-loading until the tags match
     monkeypatch.setenv('PGM_UPDATE_KERNEL', 'fs')
     monkeypatch.setenv('PGM_FS_PTAG', ptag)
+    monkeypatch.setenv('PGM_FS_DUAL', dual)
     _check_update(env, P, N, E=2, M=2, mb=mb, seed=41)  # 4 Adam steps: both slot parities twice
+
+
+def test_fs_two_workgroups_per_cu_variant(gpu):
+    """The launcher's own description of the dual placement (pgm_ppo_update_variant)."""
+    from pgmorl_amd.runtime import TaskBatch
+    tb = TaskBatch('MO-HalfCheetah-v2', 20, num_processes=4, num_steps=2048)
+    assert tb.update_variant() == 'ppo_update_fs_kernel (NS=8, R=2, 2 per CU)'
+    tb = TaskBatch('MO-Walker2d-v2', 5, num_processes=4, num_steps=2048)
+    assert tb.update_variant() == 'ppo_update_fs_kernel (NS=16, R=1)'
+    tb = TaskBatch('MO-Walker2d-v2', 10, num_processes=4, num_steps=2048)
+    assert tb.update_variant() == 'ppo_update_fs_kernel (NS=8, R=2)'
 
 
 @pytest.mark.parametrize('kernel', ['fs', 'default'])

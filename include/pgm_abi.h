@@ -178,9 +178,10 @@ int pgm_adv_normalize(const pgm_dims* d, const pgm_rollout_buf* rb, const double
  * when NULL), reset inside the call on `stream` unless pgm_ppo_update_reset did it since the last call.
  * The critic and actor towers of a task run on separate CUs that exchange the squared gradient norm per
  * minibatch step.  obs_dim <= 32 and small per-GPU populations (>= 4 parts per tower fit: 16 NS ceil(P/8) <= CUs,
- * minibatch rows a multiple of 16 NS): each tower on NS = 16 / 8 / 4 CUs that split the minibatch rows, the four
- * waves of a CU split the hidden features, and the gradient is reduce-scattered over the parts before Adam (the
- * feature-split update).  Otherwise each tower is split over four CUs (a quarter of the minibatch rows each, gradient
+ * or <= 2 x CUs with two workgroups per CU when each part takes two 16-row tiles; minibatch rows a multiple of 16 NS):
+ * each tower on NS = 16 / 8 / 4 workgroups that split the minibatch rows, the four waves of a workgroup split the
+ * hidden features, and the gradient is reduce-scattered over the parts before Adam (the feature-split update;
+ * PGM_FS_DUAL=0 keeps one workgroup per CU).  Otherwise each tower is split over four CUs (a quarter of the minibatch rows each, gradient
  * images added through the workspace) while 64 * ceil(P/8) <= CU count, else over two CUs while
  * 32 * ceil(P/8) <= CU count (obs_dim > 32: 32 * ceil(P/4) / 16 * ceil(P/4)).  obs_dim <= 32: tower
  * images LDS-resident (falls back to 2 CUs per task, then 1, as P grows); obs_dim > 32 (Humanoid): layer
@@ -195,7 +196,7 @@ int pgm_ppo_update(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params, 
 size_t pgm_ppo_update_workspace_bytes(const pgm_dims* d);
 /* The update kernel pgm_ppo_update would launch for these dims and hyper-parameters on the current device (same
  * selection rule, including the PGM_UPDATE_KERNEL / PGM_UPDATE_SPLIT overrides), as text into buf[n]
- * (e.g. "ppo_update_fs_kernel (NS=16, R=1)"): what benchmarks and profiles report.  No reference
+ * (e.g. "ppo_update_fs_kernel (NS=16, R=1)", "... (NS=8, R=2, 2 per CU)"): what benchmarks and profiles report.  No reference
  * counterpart (diagnostic). */
 int pgm_ppo_update_variant(const pgm_dims* d, const pgm_ppo_hparams* hp, char* buf, int n);
 /* Zero, on `stream`, the part of the workspace the next pgm_ppo_update for dims d would reset inside the call,

@@ -174,8 +174,10 @@ __device__ __forceinline__ float row_sum16(float v) {
 }
 // rows (optional, 128 floats of LDS): the two reduced rows stored by every lane, so that another wave reads value i at
 // rows[(i / 4) * 64 + {0, 32, 16, 48}[i % 4]] without the readlanes
+// grow (optional, 8 floats of global memory): value i stored by one lane as an sc1 store at grow[(i / 4) * 4 + {0, 2, 1, 3}[i % 4]]
 template <int M>
-__device__ __forceinline__ void wave_sum64_multi(const float (&v)[M], float (&out)[M], float* rows = nullptr) {
+__device__ __forceinline__ void wave_sum64_multi(const float (&v)[M], float (&out)[M], float* rows = nullptr,
+                                                 float* grow = nullptr) {
     static_assert(M >= 1 && M <= 8, "1..8 values");
     auto at = [&](int i) { return i < M ? v[i] : 0.f; };
     const int ln = __lane_id();
@@ -187,9 +189,11 @@ __device__ __forceinline__ void wave_sum64_multi(const float (&v)[M], float (&ou
     for (int i = 0; i < (M < 4 ? M : 4); ++i)
         out[i] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r0), lane_of[i]));
     if (rows) rows[ln] = r0;
+    if (grow && (ln & 15) == 0) __hip_atomic_store(grow + (ln >> 4), r0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if constexpr (M > 4) {
         const float r1 = row_sum16(pl16_fold(pl32_fold(at(4), at(5)), M > 6 ? pl32_fold(at(6), at(7)) : 0.f));
         if (rows) rows[64 + ln] = r1;
+        if (grow && (ln & 15) == 0) __hip_atomic_store(grow + 4 + (ln >> 4), r1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
         for (int i = 4; i < M; ++i) out[i] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r1), lane_of[i - 4]));
     }

@@ -203,6 +203,10 @@ struct RolloutArgs {
     const float* noise;
     uint64_t seed;
     int carry;
+    // split lane rollout only (set by its launcher): the chain -> objective stream of the task (progress words, states,
+    // action-mean rows, done flags) and this launch's epoch (the progress words are never reset)
+    void* scratch = nullptr;
+    unsigned epoch = 0;
 };
 
 struct EvalArgs {

@@ -276,7 +276,8 @@ struct ActorLane {
     // reaches every lane by a row copy + row_newbcast DPP operand of the FMA (no LDS round trip, no v_readlane);
     // four accumulator chains per layer.
     // murow (optional): the head sums' two reduced rows for another wave (wave_sum64_multi rows)
-    __device__ void forward_reg(float xv, int l, float (&mu)[A], float* h1row = nullptr, float* murow = nullptr) const {
+    __device__ void forward_reg(float xv, int l, float (&mu)[A], float* h1row = nullptr, float* murow = nullptr,
+                                float* mugrow = nullptr) const {
         constexpr int R1 = (O + 15) / 16;
         float X[R1];
         row_copies<R1>(xv, X);
@@ -332,7 +333,7 @@ struct ActorLane {
         float pr[A];
 #pragma unroll
         for (int j = 0; j < A; ++j) pr[j] = h2 * wm[j];
-        wave_sum64_multi<A>(pr, mu, murow);
+        wave_sum64_multi<A>(pr, mu, murow, mugrow);
 #pragma unroll
         for (int j = 0; j < A; ++j) mu[j] += bm[j];
     }
@@ -434,6 +435,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t out_rsrc(const void* base, siz
 __device__ __forceinline__ void store_lane(__amdgpu_buffer_rsrc_t r, uint32_t off, float v) {
     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (int)off, 0, 0);
 }
+// SPLIT scratch layout (bytes): the P progress words (256-B aligned), then states, mean rows, done flags
+__host__ __device__ inline size_t split_hdr_bytes(int P) { return ((size_t)P * 8 + 255) / 256 * 256; }
+__host__ __device__ inline size_t split_scratch_bytes(int P, int T, int N, int O) {
+    return split_hdr_bytes(P) + (size_t)P * T * N * (O * 8 + 32 + 4);
+}
+
 // clip as two bare v_max_f64 / v_min_f64 that the scheduler may move (clipd_hw is a volatile asm barrier)
 __device__ __forceinline__ double clipd_s(double x, double lo, double hi) {
     double r;
@@ -453,17 +460,33 @@ __device__ __forceinline__ double clipd_s(double x, double lo, double hi) {
 //    SIMD's issue slots, so the objective waves' own copy of that fp64 merge was pure extra issue.  The merged
 //    reciprocal std goes to LDS, and step t's reward leaves after barrier t + 2.
 // Both roles execute the same barriers (one per step plus two drain barriers).
-template <int O, int A, int K, int NN>
-__global__ __launch_bounds__(512) void rollout_lane_kernel(RolloutArgs a) {
+//
+// SPLIT: the two roles in two workgroups per task (blocks p and P + p), so the chain waves have their SIMDs to
+// themselves (objective waves idle measured 1.95 -> 1.81 ms per Walker P = 40 rollout).  The objective side only needs
+// the chain's per-step states (pre-reset, fp64), action-mean rows and done flags: the chain workgroup streams them to the
+// scratch with sc1 stores and publishes its progress every NCH / 2 steps (every storing wave's vmcnt(0), a workgroup
+// barrier, one relaxed agent store of epoch << 32 | steps); the objective workgroup polls it, loads with sc1 (the
+// validated hand-off: MI355X_MICROARCH.md, first row of the sc1 table), redoes the action side, and runs the obj_rms /
+// ret_rms merge itself right after each step (its rewards no longer wait for the chain's barriers).
+template <int O, int A, int K, int NN, bool SPLIT>
+__global__ __launch_bounds__(SPLIT ? 256 : 512) void rollout_lane_kernel(RolloutArgs a) {
     static_assert(lanes_fit<O, K>(), "lane roles need O + K + 1 <= 64");
     constexpr int NW = NN < 4 ? NN : 4;  // waves per role
     constexpr int NE = (NN + 3) / 4;     // env slots per wave
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     auto& S = *reinterpret_cast<LaneSmem<O, A, NN>*>(smem_raw);
-    const int p = blockIdx.x, l = threadIdx.x & 63;
+    const int p = SPLIT ? (int)blockIdx.x % a.P : (int)blockIdx.x, l = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const bool chain = wv < NW;
-    const int w = chain ? wv : wv - NW;  // env slot base of this wave
+    const bool chain = SPLIT ? (int)blockIdx.x < a.P : wv < NW;
+    const int w = SPLIT ? wv : chain ? wv : wv - NW;  // env slot base of this wave
+    // SPLIT scratch of task p: progress word, pre-reset states [T][NN][O], action-mean rows [T][NN][8], done flags [T][NN]
+    unsigned long long* const prog = reinterpret_cast<unsigned long long*>(a.scratch) + p;
+    double* const snb = reinterpret_cast<double*>(reinterpret_cast<char*>(a.scratch) + split_hdr_bytes(a.P)) +
+                        (size_t)p * a.T * NN * O;
+    float* const mub = reinterpret_cast<float*>(reinterpret_cast<char*>(a.scratch) + split_hdr_bytes(a.P) +
+                                                (size_t)a.P * a.T * NN * O * 8) + (size_t)p * a.T * NN * 8;
+    int* const dnbuf = reinterpret_cast<int*>(reinterpret_cast<char*>(a.scratch) + split_hdr_bytes(a.P) +
+                                              (size_t)a.P * a.T * NN * (O * 8 + 32)) + (size_t)p * a.T * NN;
     const int T = a.T;
     const NormCfg nc = norm_cfg(a.ns);
     const Layout& L = a.L;
@@ -682,7 +705,10 @@ __global__ __launch_bounds__(512) void rollout_lane_kernel(RolloutArgs a) {
                 if constexpr (PGM_EXP == 51) {  // timing ablation only (wrong results): no policy forward
 #pragma unroll
                     for (int j = 0; j < A; ++j) mu[j] = xr[e] * 1e-3f;
-                } else if constexpr (PGM_ROLL_DPP) pol.forward_reg(xr[e], l, mu, S.h1[w], PGM_ROLL_OBJ_SIDE ? &S.mur[buf][n][0] : nullptr);
+                } else if constexpr (PGM_ROLL_DPP) {
+                    if constexpr (SPLIT) pol.forward_reg(xr[e], l, mu, S.h1[w], nullptr, mub + ((size_t)step * NN + n) * 8);
+                    else pol.forward_reg(xr[e], l, mu, S.h1[w], PGM_ROLL_OBJ_SIDE ? &S.mur[buf][n][0] : nullptr);
+                }
                 else pol.forward(S.x[n], S.h1[w], l, mu);
                 PGM_STAMP(1);
                 // Gaussian draw (torch.normal(mean, std) = eps * std + mean) and clipped action, wave-uniform
@@ -723,10 +749,15 @@ __global__ __launch_bounds__(512) void rollout_lane_kernel(RolloutArgs a) {
                 elapsed[e] = dn ? 0 : el;
                 s_o[e] = dn ? s0_o[e] : sn;
                 if (role == 0) S.sr[buf][n][l] = s_o[e];  // lanes O.. of the row belong to the objective waves
-                S.sn[buf][n][l] = sn;
-                if (l == 0) {
-                    if constexpr (!PGM_ROLL_OBJ_SIDE) S.e2[buf][n] = e2v;
-                    S.dn[buf][n] = dn | bf << 1;
+                if constexpr (SPLIT) {  // to the objective workgroup (sc1 stores, published below)
+                    if (fl) __hip_atomic_store(snb + ((size_t)step * NN + n) * O + l, sn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (l == 0) __hip_atomic_store(dnbuf + (size_t)step * NN + n, dn | bf << 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                } else {
+                    S.sn[buf][n][l] = sn;
+                    if (l == 0) {
+                        if constexpr (!PGM_ROLL_OBJ_SIDE) S.e2[buf][n] = e2v;
+                        S.dn[buf][n] = dn | bf << 1;
+                    }
                 }
                 if constexpr (!PGM_ROLL_OBJ_SIDE) {
                     const uint32_t moff = (uint32_t)((size_t)(step + 1) * NN + n) * 4;
@@ -736,12 +767,19 @@ __global__ __launch_bounds__(512) void rollout_lane_kernel(RolloutArgs a) {
                 if (e == 0) PGM_STAMP(2);
             }
             if constexpr (PGM_EXP == 63) prep_merge();  // (63, A/B: formed just before the barrier)
+            // SPLIT: publish steps [0, step] to the objective workgroup every NCH / 2 steps (not at the chunk ends, where the
+            // next noise chunk's loads were just issued: vmcnt(0) would wait for them) and after the last step
+            const bool publish = SPLIT && (step % NCH == NCH / 2 - 1 || step == T - 1);
+            if (publish) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             lds_sync();
+            if (publish && w == 0 && l == 0)
+                __hip_atomic_store(prog, ((unsigned long long)a.epoch << 32) | (unsigned)(step + 1), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
             PGM_STAMP(3);
             // every statistic of the row: ob_rms (lanes < O, this step's states) and, for the objective waves, obj_rms /
             // ret_rms (their accumulators of the previous step; nothing in step 0's row).  The chain waves execute all
             // 64 lanes of the merge anyway; the objective waves read the reciprocal std from S.rinv a barrier later.
-            if constexpr (PGM_EXP != 52) merge(buf, role == 0 || step > 0);  // (52: timing ablation, no merge)
+            if constexpr (PGM_EXP != 52) merge(buf, SPLIT ? role == 0 : role == 0 || step > 0);  // (52: ablation, no merge)
             PGM_STAMP(4);
             // ---- normalised fp32 obs: the next input and the rollout buffer
 #pragma unroll
@@ -756,15 +794,17 @@ __global__ __launch_bounds__(512) void rollout_lane_kernel(RolloutArgs a) {
                 store_lane(r_obs, role == 0 ? (uint32_t)(((size_t)(step + 1) * NN + n) * O + l) * 4 : OOB_OFF, f);
             }
             if constexpr (!PGM_ROLL_DPP) wave_lds_fence_r();
-            if (w == 0) S.rinv[buf][l] = inv;  // read after the next barrier (off this wave's chain)
+            if (!SPLIT && w == 0) S.rinv[buf][l] = inv;  // read after the next barrier (off this wave's chain)
             PGM_STAMP(5);
         }
         // drain: the last step's objective / ret accumulators (row T & 1), then one more barrier for their reward
-        prep_merge();  // (the counts after step T - 1's merge)
-        lds_sync();
-        merge(T & 1, role == 1 || role == 2);
-        if (w == 0) S.rinv[T & 1][l] = inv;
-        lds_sync();
+        if constexpr (!SPLIT) {
+            prep_merge();  // (the counts after step T - 1's merge)
+            lds_sync();
+            merge(T & 1, role == 1 || role == 2);
+            if (w == 0) S.rinv[T & 1][l] = inv;
+            lds_sync();
+        }
         // ---- env state and observation statistics back to HBM
 #pragma unroll
         for (int e = 0; e < NE; ++e) {
@@ -778,7 +818,190 @@ __global__ __launch_bounds__(512) void rollout_lane_kernel(RolloutArgs a) {
                 a.ns.ob_mean[(size_t)p * O + l] = mean;
                 a.ns.ob_var[(size_t)p * O + l] = var;
                 if (l == 0) a.ns.ob_count[p] = cnt;
-            } else if (role == 1) {
+            } else if (role == 1 && !SPLIT) {
+                a.ns.obj_mean[p * K + ko] = mean;
+                a.ns.obj_var[p * K + ko] = var;
+                if (ko == 0) a.ns.obj_count[p] = cnt;
+            } else if (role == 2 && !SPLIT) {
+                a.ns.ret_mean[p] = mean;
+                a.ns.ret_var[p] = var;
+                a.ns.ret_count[p] = cnt;
+            }
+        }
+    } else if constexpr (SPLIT) {
+        // =========================================================== objective workgroup (SPLIT)
+        float* rew = a.rb.rewards + (size_t)p * T * NN * K;
+        const auto r_rew = out_rsrc(rew, (size_t)T * NN * K * 4);
+        const auto r_act = out_rsrc(a.rb.actions + (size_t)p * T * NN * A, (size_t)T * NN * A * 4);
+        const auto r_logp = out_rsrc(a.rb.logp + (size_t)p * T * NN, (size_t)T * NN * 4);
+        const auto r_msk = out_rsrc(masks, (size_t)(T + 1) * NN * 4);
+        const auto r_bad = out_rsrc(bad, (size_t)(T + 1) * NN * 4);
+        double V[K], ebase[K], ecoef[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            V[k] = fl ? a.spec.V[k * O + lo] : 0.0;
+            ebase[k] = a.spec.ebase[k];
+            ecoef[k] = a.spec.ecoef[k];
+            asm volatile("" : "+v"(ebase[k]), "+v"(ecoef[k]));
+        }
+        float bm[A], ls[A], sd[A], rsd[A];
+        double alo[A], ahi[A];
+        {
+            const float* prm = a.params + (size_t)p * L.total;
+#pragma unroll
+            for (int j = 0; j < A; ++j) {
+                bm[j] = prm[L.off[PGM_P_MEAN_B] + j];
+                ls[j] = prm[L.off[PGM_P_LOGSTD] + j];
+                sd[j] = expf(ls[j]);
+                rsd[j] = 1.0f / sd[j];
+                alo[j] = a.spec.act_lo[j];
+                ahi[j] = a.spec.act_hi[j];
+                asm volatile("" : "+v"(bm[j]), "+v"(ls[j]), "+v"(sd[j]), "+v"(rsd[j]));
+                asm volatile("" : "+v"(alo[j]), "+v"(ahi[j]));
+            }
+        }
+        double objacc[NE][K], ret[NE], objraw[NE][K];
+        int dprev[NE];
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+            const int n = min(w + 4 * e, NN - 1);
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                objacc[e][k] = a.st.obj_acc[((size_t)p * NN + n) * K + k];
+                objraw[e][k] = 0.0;
+            }
+            ret[e] = a.st.ret[p * NN + n];
+            dprev[e] = 0;
+        }
+        int obj_valid = a.st.obj_acc_valid[p];
+        double clip_lo = -nc.cliprew, clip_hi = nc.cliprew, gam = nc.gamma;
+        asm volatile("" : "+v"(clip_lo), "+v"(clip_hi), "+v"(gam));
+        const bool scale_out = nc.use_obj != 0;
+        const unsigned long long base = (unsigned long long)a.epoch << 32;
+        unsigned long long avail = 0;  // steps [0, avail) of this launch published by the chain workgroup
+        // steps in chunks of CHK: once the chain has published a chunk, every load of it is issued at once into registers
+        // (one load latency per chunk, not per step; the chain publishes every NCH / 2 steps)
+        constexpr int CHK = NE == 1 ? 8 : 4;
+        constexpr int pos[4] = {0, 2, 1, 3};
+        for (int c0 = 0; c0 < T; c0 += CHK) {
+            const int cend = min(c0 + CHK, T);
+            if (avail < (unsigned long long)cend) {  // wave-uniform: this wave polls, then loads what the poll covers
+                for (unsigned spins = 0;; ++spins) {
+                    const unsigned long long x = __hip_atomic_load(prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (x >= base + (unsigned long long)cend) {
+                        avail = x - base;
+                        break;
+                    }
+                    if (spins > (1u << 24)) {  // bounded (the grid is checked co-resident): garbage, never a hang
+                        avail = (unsigned long long)T;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+            }
+            double psn[CHK][NE];
+            int pdn[CHK][NE];
+            float pmr[CHK][NE][A], pej[CHK][NE][A];
+#pragma unroll
+            for (int i = 0; i < CHK; ++i) {
+                const int st = min(c0 + i, T - 1);
+#pragma unroll
+                for (int e = 0; e < NE; ++e) {
+                    const int n = min(w + 4 * e, NN - 1);
+                    const size_t sn_i = (size_t)st * NN + n;
+                    psn[i][e] = __hip_atomic_load(snb + sn_i * O + lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    pdn[i][e] = __hip_atomic_load(dnbuf + sn_i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+                    for (int j = 0; j < A; ++j) {
+                        pmr[i][e][j] = __hip_atomic_load(mub + sn_i * 8 + (j >> 2) * 4 + pos[j & 3], __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT);
+                        const size_t ei = sn_i * A + j;
+                        pej[i][e][j] = a.noise ? a.noise[ei] : counter_normal(a.seed, ei);
+                    }
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < CHK; ++i) {
+                const int step = c0 + i;
+                if (step >= T) break;
+                const int buf = step & 1;
+                prep_merge();
+#pragma unroll
+                for (int e = 0; e < NE; ++e) {
+                    const int n = w + 4 * e;
+                    if (n >= NN) break;
+                    const size_t sn_i = (size_t)step * NN + n;
+                    const double sn = fl ? psn[i][e] : 0.0;
+                    const int dnb = pdn[i][e];
+                    // the chain's Gaussian draw again (same fp32 operations on the same mean and noise), the log-prob,
+                    // |clip(a)|^2 and the action / log-prob / mask stores of step `step`
+                    float lpt[A], avs[A];
+                    double sq[A];
+#pragma unroll
+                    for (int j = 0; j < A; ++j) {
+                        const float muj = pmr[i][e][j] + bm[j];
+                        const float av = fmaf(pej[i][e][j], sd[j], muj);
+                        const float dz = (av - muj) * rsd[j];
+                        lpt[j] = -0.5f * dz * dz - ls[j] - LOG_SQRT_2PI;
+                        avs[j] = av;
+                        const double ac = clipd_s((double)av, alo[j], ahi[j]);
+                        sq[j] = ac * ac;
+                    }
+                    const double e2 = tree_sum(sq);
+                    const float lp = tree_sum(lpt);
+                    store_lane(r_act, l < A ? (uint32_t)(sn_i * A + l) * 4 : OOB_OFF, sel_lane(avs, l));
+                    store_lane(r_logp, l == 0 ? (uint32_t)sn_i * 4 : OOB_OFF, lp);
+                    const uint32_t moff = (uint32_t)((size_t)(step + 1) * NN + n) * 4;
+                    store_lane(r_msk, l == 0 ? moff : OOB_OFF, (dnb & 1) ? 0.f : 1.f);
+                    store_lane(r_bad, l == 0 ? moff : OOB_OFF, (dnb & 2) ? 0.f : 1.f);
+                    // objective side: reset by done_{t-1}, raw objectives (wave sums), discounted accumulators
+                    if (dprev[e]) {
+#pragma unroll
+                        for (int k = 0; k < K; ++k) objacc[e][k] = 0.0;
+                        ret[e] = 0.0;
+                    }
+                    dprev[e] = dnb & 1;
+                    double ob[K];
+#pragma unroll
+                    for (int k = 0; k < K; ++k) ob[k] = V[k] * sn;
+                    wave_sum64_d_multi<K>(ob, ob);
+#pragma unroll
+                    for (int k = 0; k < K; ++k) {
+                        ob[k] += ebase[k] - ecoef[k] * e2;
+                        objraw[e][k] = ob[k];
+                        objacc[e][k] = obj_valid ? objacc[e][k] * gam + ob[k] : ob[k];
+                    }
+                    ret[e] = ret[e] * gam + 0.0;  // SynthMO's scalar reward is 0 (vec_normalize.py:32)
+                    const double rv = role == 1 ? sel_lane_d(objacc[e], ko) : role == 2 ? ret[e] : 0.0;
+                    if (role == 1 || role == 2) S.sr[buf][n][l] = rv;
+                }
+                obj_valid = 1;
+                lds_sync();  // every env's accumulators of this step
+                merge(buf, role == 1 || role == 2);
+#pragma unroll
+                for (int e = 0; e < NE; ++e) {
+                    const int n = w + 4 * e;
+                    if (n >= NN) break;
+                    double r = sel_lane_d(objraw[e], ko);
+                    if (scale_out) r = clipd_s(r * inv, clip_lo, clip_hi);
+                    store_lane(r_rew, role == 1 ? (uint32_t)((((size_t)step * NN + n) * K + ko) * 4) : OOB_OFF, (float)r);
+                }
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+            const int n = w + 4 * e;
+            if (n >= NN) break;
+            if (dprev[e]) {
+#pragma unroll
+                for (int k = 0; k < K; ++k) objacc[e][k] = 0.0;
+                ret[e] = 0.0;
+            }
+            if (l < K) a.st.obj_acc[((size_t)p * NN + n) * K + l] = sel_lane_d(objacc[e], l);
+            if (l == 0) a.st.ret[p * NN + n] = ret[e];
+        }
+        if (w == 0) {
+            if (role == 1) {
                 a.ns.obj_mean[p * K + ko] = mean;
                 a.ns.obj_var[p * K + ko] = var;
                 if (ko == 0) a.ns.obj_count[p] = cnt;
@@ -787,6 +1010,7 @@ __global__ __launch_bounds__(512) void rollout_lane_kernel(RolloutArgs a) {
                 a.ns.ret_var[p] = var;
                 a.ns.ret_count[p] = cnt;
             }
+            if (l == 0) a.st.obj_acc_valid[p] = obj_valid;
         }
     } else {
         // =========================================================== objective waves
@@ -1230,6 +1454,42 @@ static int launch_k(Kern k, dim3 grid, dim3 block, size_t smem, hipStream_t s, c
 
 static bool lanes_dims(int O, int K) { return O <= 48 && O + K + 1 <= 64; }
 
+// The split rollout's chain -> objective scratch, one per device, grown on demand (a library-internal buffer: the
+// rollout ABI has no workspace argument), and the launch epoch its progress words carry (never reset: a word from an
+// earlier launch is below every value this launch waits for).  Rollouts on one device run in stream order (the
+// drop-in issues them on one stream), which the shared scratch relies on.
+static void* split_scratch(size_t bytes, int P, hipStream_t s, unsigned* epoch) {
+    static void* ptr[64];
+    static size_t cap[64];
+    static unsigned ep[64];
+    static int hdr_p[64];  // the task count whose progress words were last zeroed (the layout depends on P)
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+        set_error("pgm_rollout: no current device for the split scratch");
+        return nullptr;
+    }
+    if (cap[dev] < bytes) {
+        if (ptr[dev]) (void)hipFree(ptr[dev]);  // (synchronises: growth is rare)
+        ptr[dev] = nullptr;
+        cap[dev] = 0;
+        hdr_p[dev] = 0;
+        if (hipMalloc(&ptr[dev], bytes) != hipSuccess) {
+            set_error("pgm_rollout: split scratch of %zu bytes", bytes);
+            return nullptr;
+        }
+        cap[dev] = bytes;
+    }
+    if (hdr_p[dev] != P) {  // zero the progress words once per layout; the epoch orders every later launch
+        if (hipMemsetAsync(ptr[dev], 0, split_hdr_bytes(P), s) != hipSuccess) {
+            set_error("pgm_rollout: split scratch reset");
+            return nullptr;
+        }
+        hdr_p[dev] = P;
+    }
+    *epoch = ++ep[dev];
+    return ptr[dev];
+}
+
 bool rollout_lanes_supported(const pgm_dims* d) {
     return lanes_dims(d->O, d->K) && (d->N == 1 || d->N == 2 || d->N == 4 || d->N == 8);
 }
@@ -1240,9 +1500,27 @@ bool eval_waves_supported(const pgm_dims* d, int eval_num) {
 
 template <int O, int A, int K, int NN>
 static int launch_rollout_n(const pgm_dims* d, const RolloutArgs& a, hipStream_t s) {
-    if (int rc = launch_k(rollout_lane_kernel<O, A, K, NN>, dim3(d->P), dim3(2 * 64 * (NN < 4 ? NN : 4)),
-                          sizeof(LaneSmem<O, A, NN>), s, a, "pgm_rollout"))
+    constexpr int NW = NN < 4 ? NN : 4;
+    // PGM_ROLL_SPLIT=1 (A/B): the roles in two workgroups per task.  Measured slower, Walker P = 40 2.31 vs 1.90 ms per
+    // rollout + critic values: every published chunk costs the chain a drain of its sc1 stores (~1.5 us per publish),
+    // and the objective workgroup's loads of each chunk pay a memory round trip (the sc1 stores dropped the lines from L2)
+    const char* sel = getenv("PGM_ROLL_SPLIT");
+    const bool split = sel && sel[0] == '1' && 2 * d->P <= device_cu_count();
+    if (split) {
+        RolloutArgs b = a;
+        b.scratch = split_scratch(split_scratch_bytes(d->P, d->T, NN, O), d->P, s, &b.epoch);
+        if (!b.scratch) return PGM_E_HIP;
+        auto kern = rollout_lane_kernel<O, A, K, NN, true>;
+        const size_t smem = sizeof(LaneSmem<O, A, NN>);
+        hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        if (e != hipSuccess) return hip_fail(e, "pgm_rollout");
+        // the objective workgroups spin on the chain workgroups' progress: the whole grid must be resident
+        if (int rc = check_coresident((const void*)kern, 64 * NW, smem, 2 * d->P, "pgm_rollout (split)")) return rc;
+        if (int rc = launch_k(kern, dim3(2 * d->P), dim3(64 * NW), smem, s, b, "pgm_rollout")) return rc;
+    } else if (int rc = launch_k(rollout_lane_kernel<O, A, K, NN, false>, dim3(d->P), dim3(2 * 64 * NW),
+                                 sizeof(LaneSmem<O, A, NN>), s, a, "pgm_rollout")) {
         return rc;
+    }
     return launch_critic_values(d, a, s);
 }
 

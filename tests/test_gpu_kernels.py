@@ -275,7 +275,7 @@ def _teacher_forced_check(tb, p, pol, spec, s0, noise):
     _close(tb.ob_var[p].cpu(), envs.ob_rms.var, 1e-9, 1e-6, 'ob_rms.var')
 
 
-@pytest.mark.parametrize('kernel', ['lanes', 'block'])
+@pytest.mark.parametrize('kernel', ['lanes', 'block', 'split'])
 @pytest.mark.parametrize('env,N,T', [('MO-Hopper-v2', 4, 48), ('MO-Walker2d-v2', 2, 520), ('MO-Hopper-v3', 6, 40),
                                      ('MO-Hopper-v3', 8, 40), ('MO-Walker2d-v2', 1, 33), ('MO-Ant-v2', 4, 24),
                                      ('MO-Humanoid-v2', 8, 40), ('MO-Humanoid-v2', 8, 1003), ('MO-Humanoid-v2', 4, 33),
@@ -287,7 +287,10 @@ def test_rollout(gpu, env, N, T, kernel, monkeypatch):
     # lanes: one wave per env + batched critic values (default for N in 1/2/4/8; obs_dim > 48 takes the wide
     # kernel: k-sliced layer 1 over 4 waves, feature-per-lane dynamics); block: workgroup per step.
     # Humanoid T = 1003 crosses the 1000-step time limit (auto-reset, bad_transition) and 31 noise chunks
-    monkeypatch.setenv('PGM_ROLLOUT_KERNEL', kernel)
+    # split (A/B): the lane kernel's chain and objective roles in two workgroups per task (PGM_ROLL_SPLIT=1)
+    if kernel == 'split':
+        monkeypatch.setenv('PGM_ROLL_SPLIT', '1')
+    monkeypatch.setenv('PGM_ROLLOUT_KERNEL', 'lanes' if kernel == 'split' else kernel)
     P = 2
     spec, tb, pols = _batch_with_policies(env, P, N, T, seed=3, scale=0.05)
     s0 = envspec.reset_table(spec['obs_dim'], 0, N)

@@ -850,9 +850,26 @@ int fs_choose_ns(const pgm_dims* d, int mb, int* dual) {
         const int grid = fs_grid(d->P, ns);
         if (grid <= cus) return ns;
         if (dual_ok && R == 2 && grid <= 2 * cus) {  // (R 4 -> 2 pays; R 2 -> 1 does not: Walker P = 10 3.18 -> 3.70 ms)
-            MArgs q{};
-            q.hp.num_mini_batch = d->T * d->N / mb;
-            if (ppo_update_fs_op(d, q, ns, true, 1, nullptr) == 1) {
+            // the occupancy answer per (device, dims, NS), cached: this runs before every update launch
+            static int memo[16][8];  // [slot] = {device, O, A, K, ns, answer + 1, mb, tagged-hop variant}
+            int dev = 0;
+            (void)hipGetDevice(&dev);
+            const char* pt = getenv("PGM_FS_PTAG");  // (its kernel holds more registers)
+            const int ptag = pt && pt[0] == '1';
+            int ans = -1;
+            for (auto& m : memo)
+                if (m[5] && m[0] == dev && m[1] == d->O && m[2] == d->A && m[3] == d->K && m[4] == ns && m[6] == mb &&
+                    m[7] == ptag)
+                    ans = m[5] - 1;
+            if (ans < 0) {
+                MArgs q{};
+                q.hp.num_mini_batch = d->T * d->N / mb;
+                ans = ppo_update_fs_op(d, q, ns, true, 1, nullptr) == 1 ? 1 : 0;
+                static int next = 0;
+                int* m = memo[next++ & 15];
+                m[0] = dev, m[1] = d->O, m[2] = d->A, m[3] = d->K, m[4] = ns, m[5] = ans + 1, m[6] = mb, m[7] = ptag;
+            }
+            if (ans == 1) {
                 *dual = 1;
                 return ns;
             }

@@ -865,7 +865,7 @@ int fs_choose_ns(const pgm_dims* d, int mb, int* dual) {
                 MArgs q{};
                 q.hp.num_mini_batch = d->T * d->N / mb;
                 ans = ppo_update_fs_op(d, q, ns, true, 1, nullptr) == 1 ? 1 : 0;
-                static int next = 0;
+                static unsigned next = 0;
                 int* m = memo[next++ & 15];
                 m[0] = dev, m[1] = d->O, m[2] = d->A, m[3] = d->K, m[4] = ns, m[5] = ans + 1, m[6] = mb, m[7] = ptag;
             }

@@ -51,7 +51,8 @@ def parse():
     ap.add_argument('--num-steps', type=int, default=2048)
     ap.add_argument('--ppo-epoch', type=int, default=10)
     ap.add_argument('--num-mini-batch', type=int, default=32)
-    ap.add_argument('--cpu-iters', type=int, default=5, help='oracle iterations per process for cpu_baseline')
+    ap.add_argument('--cpu-iters', type=int, default=16,
+                    help='oracle iterations per process for cpu_baseline (16: ~20 s of wall time on the box)')
     ap.add_argument('--cpu-procs', type=int, default=15,
                     help='concurrent oracle processes: the 16-core host share of one GPU on the box minus the '
                          'bench process itself (the box allows 16 processes with the GPU open)')
@@ -152,8 +153,11 @@ def cpu_baseline(args, spec, tasks):
     steps = sum(r[3] for r in res)
     value = steps / (t1 - t0)
     per_core = value / procs
+    rates = np.array([r[3] / (r[2] - r[1]) for r in res])  # each process's own rate (the spread across cores)
     return {'value': value, 'unit': 'env steps/sec', 'cores': procs, 'kind': 'port',
             'per_core': per_core, 'extrapolated_96vcpu': per_core * 96,
+            'per_process': {'min': float(rates.min()), 'median': float(np.median(rates)), 'max': float(rates.max()),
+                            'rel_sd': float(rates.std(ddof=1) / rates.mean()) if len(rates) > 1 else 0.0},
             'extrapolation': f'per-core value x 96 vCPUs (reference hardware, README.md:92-94)',
             'host': {'affinity_cpus': ncpu, 'os_cpu_count': os.cpu_count(), 'lscpu': _lscpu()},
             'sample': f'{procs} concurrent single-thread processes x {args.cpu_iters} MOPG iterations each '
@@ -266,16 +270,40 @@ def whole_run(args, iter_value):
                       f'num_env_steps {int(args.whole_run_steps)}, N=4, T=2048, E=10, M=32, device RNG, seed 0'}
 
 
+# the sources each update-kernel family is compiled from (a PMC summary is only quoted for the exact sources it measured)
+KERNEL_SOURCES = {
+    'ppo_update_mfma_kernel': ['pgm_ppo_mfma.hip'], 'ppo_update_t16_kernel': ['pgm_ppo_mfma.hip'],
+    'ppo_update_fs_kernel': ['pgm_ppo_fs.hip'], 'ppo_update_wide_kernel': ['pgm_ppo_wide.hip'],
+}
+KERNEL_HEADERS = ['pgm_common.hpp', 'pgm_mfma.hpp', 'pgm_ppo_shared.hpp', 'pgm_dispatch.hpp']
+
+
+def kernel_source_hash(variant):
+    """sha256 (16 hex digits) of the source files the update kernel named by ``variant`` (pgm_ppo_update_variant) is
+    built from, plus the shared headers; None for an unknown family."""
+    import hashlib
+    fam = (variant or '').split(' ')[0]
+    if fam not in KERNEL_SOURCES:
+        return None
+    h = hashlib.sha256()
+    for f in KERNEL_SOURCES[fam] + KERNEL_HEADERS:
+        with open(os.path.join(ROOT, 'pgmorl_amd', 'csrc', f), 'rb') as fp:
+            h.update(f.encode() + b'\0' + fp.read())
+    return h.hexdigest()[:16]
+
+
 def pmc_traffic(args, workload, kernel):
     """roofline.traffic: HBM-side bytes per launch of the update kernel from the committed PMC summary of THIS
-    workload at HEAD (profiles/pmc_head.json: one entry per workload, the kernel family checked against the one
-    the launcher picks; A/B files are not listed there).  (None, reason) when none matches."""
+    workload (profiles/pmc_head.json: one entry per workload; A/B files are never listed there).  The entry must be
+    for the same launch -- the full pgm_ppo_update_variant string (family, NS, R, two per CU) -- and for the same
+    kernel sources (kernel_source_hash); otherwise (None, reason): a stale or other-variant PMC is never quoted."""
     if args.traffic_file:
         try:
             d = json.load(open(args.traffic_file))
         except Exception as e:
             return None, f'{args.traffic_file}: {e!r}'
-        ent = {'kernel': d.get('kernel'), 'hbm_bytes_per_launch': d.get('hbm_bytes_per_launch'),
+        ent = {'variant': d.get('variant'), 'source_hash': d.get('source_hash'),
+               'hbm_bytes_per_launch': d.get('hbm_bytes_per_launch'),
                'source': args.traffic_file} if d.get('workload') == workload else None
     else:
         try:
@@ -284,9 +312,10 @@ def pmc_traffic(args, workload, kernel):
             return None, f'profiles/pmc_head.json: {e!r}'
     if not ent:
         return None, f'no PMC summary for {workload}'
-    fam = (kernel or '').split(' ')[0]
-    if not fam or fam not in (ent.get('kernel') or ''):
-        return None, f"PMC summary {ent['source']} is for {ent.get('kernel')}, not {kernel}"
+    if not kernel or ent.get('variant') != kernel:
+        return None, f"PMC summary {ent.get('source')} is for {ent.get('variant')!r}, not {kernel!r}"
+    if ent.get('source_hash') != kernel_source_hash(kernel):
+        return None, f"PMC summary {ent.get('source')} measured other kernel sources (stale)"
     return ent['hbm_bytes_per_launch'], ent['source']
 
 

@@ -4,9 +4,10 @@
  * Every entry point is batched over P tasks (policies), takes CALLER-OWNED device buffers
  * (plain pointers; no allocation inside), is ordered on the passed hipStream_t and returns
  * an int status (PGM_OK or a negative PGM_E_*).  pgm_last_error() returns a thread-local
- * message for the last failure.  No global mutable state besides that string and the
- * pre-zeroed-workspace marks of pgm_ppo_update_reset: calls on distinct streams are independent.  One host
- * thread per device.
+ * message for the last failure.  No global mutable state besides that string, the pre-zeroed-workspace
+ * marks of pgm_ppo_update_reset (mutex-guarded) and a per-device CU count (an immutable device property):
+ * no cached launch decisions, no allocation inside the library.  Calls on distinct streams are
+ * independent.  One host thread per device.
  *
  * Reference seams replaced (albo437/PGMORL; paths relative to the reference tree):
  *   pgm_act_forward       Policy.act / get_value            a2c_ppo_acktr/model.py:57-73
@@ -186,13 +187,15 @@ int pgm_adv_normalize(const pgm_dims* d, const pgm_rollout_buf* rb, const double
  * 32 * ceil(P/8) <= CU count (obs_dim > 32: 32 * ceil(P/4) / 16 * ceil(P/4)).  obs_dim <= 32: tower
  * images LDS-resident (falls back to 2 CUs per task, then 1, as P grows); obs_dim > 32 (Humanoid): layer
  * 1 streamed from L2, needs 2P <= CU count (PGM_E_UNSUPPORTED otherwise: shard the tasks over more
- * GPUs).  PGM_UPDATE_SPLIT=0/1/2/3/4 caps the row split (3 = an A/B-only variant, selected only explicitly);
- * PGM_UPDATE_KERNEL=fs forces the feature-split update wherever it fits, =mfma the row-split kernels.
+ * GPUs).  PGM_UPDATE_SPLIT=0/1/2/4 caps the row split; PGM_UPDATE_KERNEL=fs forces the feature-split
+ * update wherever it fits, =mfma the row-split kernels.
  * After the call, the 8-byte word at index 2P of the workspace is nonzero iff an exchange timed out
  * (the workgroups were not co-resident); the results of such a call are invalid. */
 int pgm_ppo_update(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params, float* adam_m,
                    float* adam_v, int32_t* adam_step, const float* lr, const int32_t* perms,
                    const pgm_rollout_buf* rb, float* stats, void* workspace, pgm_stream_t stream);
+/* Workspace bytes for dims d; monotone in d->P, so a workspace sized for P serves every call with P' <= P tasks
+ * (the same other dims). */
 size_t pgm_ppo_update_workspace_bytes(const pgm_dims* d);
 /* The update kernel pgm_ppo_update would launch for these dims and hyper-parameters on the current device (same
  * selection rule, including the PGM_UPDATE_KERNEL / PGM_UPDATE_SPLIT overrides), as text into buf[n]

@@ -3,6 +3,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <atomic>
+
 #include "pgm_common.hpp"
 
 namespace pgm {
@@ -27,15 +29,19 @@ int launch_status(const char* what) {
     return PGM_OK;
 }
 
+// CUs of the current device, cached per device (the library's only cache: an immutable device property, written with
+// the same value by any thread that races on it)
 int device_cu_count() {
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            cus = 1;
+    static std::atomic<int> cus[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 1;
+    if (dev >= 0 && dev < 64) {
+        if (const int c = cus[dev].load(std::memory_order_relaxed)) return c;
     }
-    return cus;
+    int c = 0;
+    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c < 1) return 1;
+    if (dev >= 0 && dev < 64) cus[dev].store(c, std::memory_order_relaxed);
+    return c;
 }
 
 int check_coresident(const void* kern, int block, size_t smem, int grid, const char* what) {

@@ -50,10 +50,9 @@ constexpr int fs_nown(int O, int NS) { return (fs_nb(O) + NS - 1) / NS; }  // bl
 // parameter-slot positions a part writes: every wave publishes the same number of blocks (ceil(NOWN / 4)), past NOWN
 // unused values, so a slot holds 4 ceil(NOWN / 4) block positions
 constexpr int fs_pslots(int O, int NS) { return 4 * ((fs_nown(O, NS) + 3) / 4); }
-// payload: image slots [P][2][NS][2 parities][NB KiB], then parameter slots [P][2][NS][2][fs_pslots x 2 KiB] (room
-// for the tagged form: every value an 8-B {value, tag} granule)
+// payload: image slots [P][2][NS][2 parities][NB KiB], then parameter slots [P][2][NS][2][fs_pslots KiB]
 inline size_t fs_payload_bytes(int P, int O, int NS) {
-    return (size_t)P * 2 * NS * 2 * (size_t)(fs_nb(O) + 2 * fs_pslots(O, NS)) * 1024;
+    return (size_t)P * 2 * NS * 2 * (size_t)(fs_nb(O) + fs_pslots(O, NS)) * 1024;
 }
 // NS sized by the workspace: the largest power of two with 16 NS ceil(P/8) <= 512 (a 256-CU MI355X with two
 // workgroups per CU where R <= 2 lets them share one, fs_choose_ns), at most 16
@@ -70,10 +69,12 @@ __host__ __device__ inline int fs_gran(int P, int NS, int kind, int p, int m, in
     return 16 * P + 8 + ((((kind * P + p) * 2 + m) * NS + hs) * 2 + par);
 }
 
+// Sized for the largest NS (16), not fs_ns_cap(P): a caller may allocate the workspace for a capacity P and launch
+// with fewer active tasks (TaskBatch.set_active), whose cap can be LARGER (8 parts at P = 32, 4 at P = 33), and
+// NS (NB + pslots(NS)) grows with NS, so this bounds the payload of every launch with P' <= P tasks.
 size_t fs_workspace_extra(const pgm_dims* d) {
     if (d->O > 32) return 0;
-    const int ns = fs_ns_cap(d->P);
-    return ns >= 2 ? fs_payload_bytes(d->P, d->O, ns) : 0;
+    return fs_payload_bytes(d->P, d->O, 16);
 }
 
 // fragment slot (block b, lane l, register r) -> tower image index (TowerImg), -1 for padding
@@ -132,9 +133,9 @@ constexpr size_t fs_smem_bytes(bool dual) {
     return dual || sizeof(FsSmem<O, A, K, R>) > 81 * 1024 ? sizeof(FsSmem<O, A, K, R>) : 81 * 1024;
 }
 
-// PTAG: the parameter hop without a flag -- owners store every new value as an 8-B {value, tag} granule (16-B stores of
-// two granules, no drain / barrier / flag), readers re-load a block until all its tags are this step's
-template <int O, int A, int K, int NS, int R, bool PTAG>
+// (Measured and dropped: the parameter hop without a flag -- owners storing every new value as an 8-B {value, tag}
+// granule, readers re-loading a block until all its tags are this step's: P = 5 3.45 vs 2.93 ms, P = 20 5.06 vs 4.38 ms.)
+template <int O, int A, int K, int NS, int R>
 __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
     static_assert(O <= 32 && R >= 1 && R <= 8 && (R & (R - 1)) == 0, "fs tiles");
     using Sm = FsSmem<O, A, K, R>;
@@ -147,7 +148,7 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
     constexpr int CR = RS / 4;
     constexpr int BPW = fs_bpw(O), NB = fs_nb(O), NOWN = fs_nown(O, NS);
     constexpr int OWV = (NOWN + 3) / 4;  // owned blocks per wave (block j of the part: wave j mod 4)
-    constexpr int ISB = NB * 1024, PSB = fs_pslots(O, NS) * 2048;  // (the tagged form fills a slot: 4 OWV x 2 KiB)
+    constexpr int ISB = NB * 1024, PSB = fs_pslots(O, NS) * 1024;
     constexpr bool HSPLIT = R >= 4;      // heads: row tiles split over the waves (else units + samples split)
     constexpr int NHT = HSPLIT ? R / 4 : R;
     constexpr int NC = R == 1 ? 2 : 1;   // accumulator chains per tile of the 16-deep contractions
@@ -181,7 +182,7 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
     auto gran = [&](int kind, int mm, int h, int par) { return a.ws + fs_gran(a.P, NS, kind, p, mm, h, par); };
     unsigned long long* const fail_word = a.ws + 2 * a.P;
     // the timed-out wait, for the host's error message: bit 0, bit 1 + site (0 image flags, 1 norm granules, 2 parameter
-    // flags, 3 tagged parameter blocks), the awaited tag in bits 8..23, the workgroup (task, tower, part) from bit 24
+    // flags), the awaited tag in bits 8..23, the workgroup (task, tower, part) from bit 24
     auto fail_code = [&](int site, unsigned tg) -> unsigned long long {
         return 1ull | (2ull << site) | ((unsigned long long)(tg & 0xffff) << 8) |
                ((unsigned long long)((p * 2 + m) * NS + hs) << 24);
@@ -249,59 +250,18 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
     // and written into the image during the next one, each just before its first reader: W1 + vector block before
     // layer 1, W2 before layer 2, the head block before B2 (heads read every wave's); the own part's blocks are
     // written by their owners before the parameter hand-off
-    u32x4 pv[BPW], ph[PTAG ? BPW : 1];  // PTAG: pv = {p0, tag, p1, tag}, ph = {p2, tag, p3, tag}
-    auto pval = [&](int k, int r) -> float {
-        if constexpr (PTAG) {
-            const u32x4& v = r < 2 ? pv[k] : ph[k];
-            return __uint_as_float(v[2 * (r & 1)]);
-        } else {
-            return __uint_as_float(pv[k][r]);
-        }
-    };
+    u32x4 pv[BPW];
     auto put_block = [&](int k) {  // (the own part's blocks rewrite the values their owners already wrote)
         const int b = BPW * w + k;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int ii = frag_img<O, A, K>(b, l, r, m);
-            if (ii >= 0) Pf[ii] = pval(k, r);
+            if (ii >= 0) Pf[ii] = __uint_as_float(pv[k][r]);
         }
     };
     auto pload = [&](int k, int par_) {
         const int b = BPW * w + k, h = b % NS, jj = b / NS;  // (own part's blocks too: straight-line loads)
-        if constexpr (PTAG) {
-            pv[k] = __builtin_amdgcn_raw_buffer_load_b128(xr, pslot(h, par_) + (jj * 128 + 2 * l) * 16, 0, SC1);
-            ph[k] = __builtin_amdgcn_raw_buffer_load_b128(xr, pslot(h, par_) + (jj * 128 + 2 * l + 1) * 16, 0, SC1);
-        } else {
-            pv[k] = __builtin_amdgcn_raw_buffer_load_b128(xr, pslot(h, par_) + (jj * 64 + l) * 16, 0, SC1);
-        }
-    };
-    // PTAG: until every block of this wave carries step tag `tg`, re-load the blocks that do not (bounded)
-    auto pverify = [&](unsigned tg, int par_) {
-        if constexpr (PTAG) {
-            unsigned pending = (1u << BPW) - 1;
-            for (unsigned spins = 0; pending; ++spins) {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                unsigned bad = 0;
-#pragma unroll
-                for (int k = 0; k < BPW; ++k) {
-                    if (pending & (1u << k)) {
-                        const bool ok = pv[k][1] == tg && pv[k][3] == tg && ph[k][1] == tg && ph[k][3] == tg;
-                        if (__builtin_amdgcn_ballot_w64(!ok)) bad |= 1u << k;
-                    }
-                }
-                pending = bad;
-                if (!pending) break;
-                if (__hip_atomic_load(fail_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
-                if (spins > (1u << 22)) {
-                    __hip_atomic_store(fail_word, fail_code(3, tg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-                for (int k = 0; k < BPW; ++k)
-                    if (pending & (1u << k)) pload(k, par_);
-            }
-        }
+        pv[k] = __builtin_amdgcn_raw_buffer_load_b128(xr, pslot(h, par_) + (jj * 64 + l) * 16, 0, SC1);
     };
     for (int gp = 0; gp < npass; ++gp) {
         const int cur = gp & 1, par = gp & 1;
@@ -310,7 +270,6 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
         auto rt = [&](int ti) { return rb + ti * 16 * RSL; };
         // ================================================================ tiles
         if (gp > 0) {
-            pverify((unsigned)gp, (gp - 1) & 1);  // the previous step's parameters (tag = its step + 1)
 #pragma unroll
             for (int k = 0; k < K1B; ++k) put_block(k);
             put_block(K1B + 5);
@@ -736,31 +695,17 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
             // the part's owned block w + 4 i (slot position always valid: blocks past NB publish unused values, so every
             // wave issues the same number of stores)
             const int jj = w + 4 * i;
-            if constexpr (PTAG) {
-                const u32x4 u0 = {__float_as_uint(op[i][0]), tag, __float_as_uint(op[i][1]), tag};
-                const u32x4 u1 = {__float_as_uint(op[i][2]), tag, __float_as_uint(op[i][3]), tag};
-                __builtin_amdgcn_raw_buffer_store_b128(u0, xr, pslot(hs, par) + (jj * 128 + 2 * l) * 16, 0, SC1);
-                __builtin_amdgcn_raw_buffer_store_b128(u1, xr, pslot(hs, par) + (jj * 128 + 2 * l + 1) * 16, 0, SC1);
-            } else {
-                const u32x4 u = {__float_as_uint(op[i][0]), __float_as_uint(op[i][1]), __float_as_uint(op[i][2]),
-                                 __float_as_uint(op[i][3])};
-                __builtin_amdgcn_raw_buffer_store_b128(u, xr, pslot(hs, par) + (jj * 64 + l) * 16, 0, SC1);
-            }
+            const u32x4 u = {__float_as_uint(op[i][0]), __float_as_uint(op[i][1]), __float_as_uint(op[i][2]),
+                             __float_as_uint(op[i][3])};
+            __builtin_amdgcn_raw_buffer_store_b128(u, xr, pslot(hs, par) + (jj * 64 + l) * 16, 0, SC1);
         }
-        if constexpr (PTAG) {
-            // no drain: only the row DMA issued during the image poll must have landed (it is older than the 2 OWV
-            // stores just issued), for every wave, before the next step reads the rows
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * OWV) : "memory");
-            lds_sync_m();
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // + the row DMA issued during the image poll
-            lds_sync_m();
-            if (t == 0)
-                __hip_atomic_store(gran(2, m, hs, par), (unsigned long long)tag << 32, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            if (w == 0 && l < NS && l != hs) spin(gran(2, m, l, par), 2);
-            lds_sync_m();  // every part's blocks published; the next minibatch's rows landed
-        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // + the row DMA issued during the image poll
+        lds_sync_m();
+        if (t == 0)
+            __hip_atomic_store(gran(2, m, hs, par), (unsigned long long)tag << 32, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        if (w == 0 && l < NS && l != hs) spin(gran(2, m, l, par), 2);
+        lds_sync_m();  // every part's blocks published; the next minibatch's rows landed
         PGM_STAMP(9);
         // ---- the other parts' new blocks of this wave's feature block: loads in flight into the next step
         if (gp + 1 < npass) {
@@ -806,8 +751,7 @@ static int launch_fs_k(const pgm_dims* d, const MArgs& a, bool dual, int op, hip
         set_error("pgm_ppo_update (fs): LDS %zu bytes exceeds 160 KiB", smem);
         return op == 1 ? 0 : PGM_E_UNSUPPORTED;
     }
-    const char* pt = getenv("PGM_FS_PTAG");
-    auto kern = pt && pt[0] == '1' ? ppo_update_fs_kernel<O, A, K, NS, R, true> : ppo_update_fs_kernel<O, A, K, NS, R, false>;
+    auto kern = ppo_update_fs_kernel<O, A, K, NS, R>;
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return op == 1 ? 0 : hip_fail(e, "pgm_ppo_update (fs)");
     if (op == 1) {
@@ -833,43 +777,24 @@ int ppo_update_fs_op(const pgm_dims* d, const MArgs& a, int ns, bool dual, int o
 // 8 per part; 0 = the feature-split update does not apply.  *dual = 1: the grid (16 NS ceil(P/8) workgroups) exceeds
 // the CU count and runs two workgroups per CU, taken for R = 2 where both fit one CU (<= 80 KiB LDS, <= 256
 // registers): a step's three hand-offs then overlap the other workgroup's tiles (HalfCheetah P = 20: NS 4, R 4
-// 4.45 ms -> NS 8, R 2 4.01 ms; profiles/r04r_fs_dual_ab.json).  PGM_FS_DUAL=0 (A/B): one per CU only.
+// 4.45 ms -> NS 8, R 2 4.01 ms; profiles/r04r_fs_dual_ab.json).  PGM_FS_DUAL=0: one per CU only.  The occupancy of
+// the exact kernel is queried at every call (no cached answer: the library keeps no mutable state, pgm_abi.h).
 int fs_choose_ns(const pgm_dims* d, int mb, int* dual) {
     *dual = 0;
     if (d->O > 32) return 0;
     const int cus = device_cu_count();
-    const char* cap = getenv("PGM_FS_NS");  // A/B: at most this many parts per tower
-    const int nmax = cap && atoi(cap) >= 2 ? atoi(cap) : 16;
     const char* dsel = getenv("PGM_FS_DUAL");
     const bool dual_ok = !(dsel && dsel[0] == '0');
     for (int ns = fs_ns_cap(d->P); ns >= 2; ns >>= 1) {
-        if (ns > nmax) continue;
         if (mb % (16 * ns) != 0) continue;
         const int R = mb / (16 * ns);
         if (R < 1 || R > 8 || (R & (R - 1)) != 0) continue;
         const int grid = fs_grid(d->P, ns);
         if (grid <= cus) return ns;
         if (dual_ok && R == 2 && grid <= 2 * cus) {  // (R 4 -> 2 pays; R 2 -> 1 does not: Walker P = 10 3.18 -> 3.70 ms)
-            // the occupancy answer per (device, dims, NS), cached: this runs before every update launch
-            static int memo[16][8];  // [slot] = {device, O, A, K, ns, answer + 1, mb, tagged-hop variant}
-            int dev = 0;
-            (void)hipGetDevice(&dev);
-            const char* pt = getenv("PGM_FS_PTAG");  // (its kernel holds more registers)
-            const int ptag = pt && pt[0] == '1';
-            int ans = -1;
-            for (auto& m : memo)
-                if (m[5] && m[0] == dev && m[1] == d->O && m[2] == d->A && m[3] == d->K && m[4] == ns && m[6] == mb &&
-                    m[7] == ptag)
-                    ans = m[5] - 1;
-            if (ans < 0) {
-                MArgs q{};
-                q.hp.num_mini_batch = d->T * d->N / mb;
-                ans = ppo_update_fs_op(d, q, ns, true, 1, nullptr) == 1 ? 1 : 0;
-                static unsigned next = 0;
-                int* m = memo[next++ & 15];
-                m[0] = dev, m[1] = d->O, m[2] = d->A, m[3] = d->K, m[4] = ns, m[5] = ans + 1, m[6] = mb, m[7] = ptag;
-            }
-            if (ans == 1) {
+            MArgs q{};
+            q.hp.num_mini_batch = d->T * d->N / mb;
+            if (ppo_update_fs_op(d, q, ns, true, 1, nullptr) == 1) {
                 *dual = 1;
                 return ns;
             }

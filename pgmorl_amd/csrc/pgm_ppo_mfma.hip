@@ -34,60 +34,45 @@
 
 PGM_STAMP_UNIT(mfma)
 
-// unroll depths of the feature-contracting MFMA loops (A/B diagnostics: scripts/build_var.sh, -DPGM_EXP=n)
-#ifndef PGM_EXP
-#define PGM_EXP 0
-#endif
 #define PGM_PRAGMA(x) _Pragma(#x)
 #define PGM_UNROLL(n) PGM_PRAGMA(unroll n)
-// (measured, Walker: MODE 2 layer-2 / dH1 loops 8 -> 32: 6.54 -> 6.46 ms; VALU heads 4 -> 32: -> 6.48 ms; t16 loops
-// 4 -> 16: 5.40 -> 5.12 ms)
-#define PGM_U_L2 (PGM_EXP == 1 ? 8 : PGM_EXP == 2 ? 16 : 32)
-#define PGM_U_HEAD (PGM_EXP == 3 ? 4 : PGM_EXP == 4 ? 8 : 32)
-#define PGM_U16 (PGM_EXP == 5 ? 4 : PGM_EXP == 6 ? 8 : 16)
-// PGM_EXP 22 (A/B only): heads of the 32-row kernel on the 16x16x4 MFMA with the head OUTPUTS on the accumulator
-// rows and the samples on the columns (out^T = Wh . H2^T): a lane holds 4 outputs of one sample, one
-// v_permlane32_swap per register puts the two 16-sample blocks side by side, so every lane evaluates the loss of ONE
-// sample and the head-bias / logstd column sums become 16-lane DPP row sums.  Measured at Walker P = 40: update 6.33
-// ms against the VALU heads' 6.25 (the 32 chained MFMAs and their operand reads cost what the VALU FMAs did).
-// (Samples on the accumulator rows -- the 16-row kernel's orientation -- put 8 samples' losses on every lane: 6.72 ms.)
-#define PGM_HEADS_MFMA (PGM_EXP == 22)
+// unroll depths of the feature-contracting MFMA loops (measured, Walker: MODE 2 layer-2 / dH1 loops 8 -> 32: 6.54 ->
+// 6.46 ms; VALU heads 4 -> 32: -> 6.48 ms; t16 loops 4 -> 16: 5.40 -> 5.12 ms)
+#define PGM_U_L2 32
+#define PGM_U16 16
+// Measured and dropped (rounds 2-3): heads of the 32-row kernel on the 16x16x4 MFMA with the head outputs on the
+// accumulator rows (6.33 vs the VALU heads' 6.25 ms at Walker P = 40; samples on the accumulator rows: 6.72 ms); the
+// MODE 2 tower norms exchanged as a separate granule hand-off instead of gathered (below: 6.17 vs 6.10 ms); the
+// round-2 block maps (a tower's parts on one XCD, the towers on two: 5.90 vs 5.85 ms, 2.72 vs 2.44 GB per t16 launch);
+// ds_add_f32 image rounds (~20x slower on gfx950); elementwise tanh / tanh' one element per instruction (5.80 vs 5.77
+// ms); the next pass's rows staged at the top of a step or behind the layer-1 MFMAs; dW2 issued before dH1.
+//
 // MODE 2 global grad norm: every workgroup of a task gathers all three other half images (its partner half's and both
 // halves of the other tower) and forms the other tower's sum of squares itself, in exactly the owner's element order
 // and reduction tree, so the totals stay bitwise equal in the four workgroups and the separate norm-granule hand-off
-// (one more cross-CU round trip per Adam step) disappears.  PGM_EXP 24 (A/B): the granule hand-off.
-#define PGM_FUSED_NORM (PGM_EXP != 24)
-// block maps of the split launches: every workgroup of a task on ONE XCD (groups of 8 tasks; blocks b, b + 8, ... share
+// (one more cross-CU round trip per Adam step) disappears.
+//
+// Block maps of the split launches: every workgroup of a task on ONE XCD (groups of 8 tasks; blocks b, b + 8, ... share
 // an XCD under round-robin dispatch), so the per-step image hand-offs stay inside one L2: MODE 2 Walker P = 40 5.90 ->
 // 5.85-5.89 ms, t16 HalfCheetah P = 20 4.95 -> 4.88-4.90 ms, Walker P = 5 4.90 -> 4.85-4.87 ms (profiles/r03p_*).
-// PGM_EXP 48 / 49 (A/B): the round-2 maps (groups of 4 tasks, a tower's parts on one XCD, the towers on two)
-#define PGM_MODE2_XCD4 (PGM_EXP != 48)
-#define PGM_T16_XCD8 (PGM_EXP != 49)
 namespace pgm {
 // grids of the split launches (padding blocks of a partial group of tasks exit at once)
-inline int mode2_grid(int P) { return PGM_MODE2_XCD4 ? 32 * ((P + 7) / 8) : 16 * ((P + 3) / 4); }
-inline int t16_grid(int P, int NS) { return PGM_T16_XCD8 ? 16 * NS * ((P + 7) / 8) : 8 * NS * ((P + 3) / 4); }
+inline int mode2_grid(int P) { return 32 * ((P + 7) / 8); }
+inline int t16_grid(int P, int NS) { return 16 * NS * ((P + 7) / 8); }
 }  // namespace pgm
 
 namespace pgm {
 
+// the tiles' elementwisenamespace pgm {
+
 // the tiles' elementwise tanh(z + b) and tanh' products on register PAIRS through the packed fp32 ALU (v_pk_add /
 // v_pk_mul / v_pk_fma_f32; per element the same operations as tanh_fast): MODE 2 Walker P = 40 5.80 -> 5.76-5.77 ms,
-// t16 unchanged.  PGM_EXP 29 (A/B): one element per instruction.  (MODE 2's Adam on element pairs: no change, 5.76.)
-#define PGM_PK_ELEM (PGM_EXP != 29)
+// t16 unchanged.  (MODE 2's Adam on element pairs: no change, 5.76.)
 
 // The image reductions add exactly ONE partial onto a stored one per element per round (store and add ordered by a
-// barrier): a read + add + write in the wave.  PGM_EXP 23 (A/B only): ds_add_f32 instead (the same two-operand sum,
-// the read-modify-write in the LDS) -- measured ~20x slower on gfx950 (MODE 2 stage 1: 2.1 K -> 40.5 K cycles per
-// Adam step; t16 rounds 4.5 K -> 36 K)
-#define PGM_LDS_ADD (PGM_EXP == 23)
-__device__ __forceinline__ void lds_add(float* p, float v) {
-#if PGM_LDS_ADD
-    __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#else
-    *p += v;
-#endif
-}
+// barrier): a read + add + write in the wave (ds_add_f32 instead measured ~20x slower on gfx950: MODE 2 stage 1 2.1 K ->
+// 40.5 K cycles per Adam step)
+__device__ __forceinline__ void lds_add(float* p, float v) { *p += v; }
 
 
 // ---------------------------------------------------------------- packed sample table
@@ -170,13 +155,11 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
     constexpr int IMG = Sm::IMG, NT = Sm::NT, SBk = Sm::SBk, RS = Sm::RS;
     constexpr int NBUF = nbuf<O, A, K, SPLIT>();
     constexpr int RSL = Sm::RSL;
-    // single-tile MODE 2: the next pass's row DMA is issued by waves 1-3 while wave 0 polls the tower-norm granule
-    // (they wait at that barrier anyway) and retired by the step's last barrier, instead of at the top of the
-    // step; wave 0 keeps no DMA in its queue so its polls' vmcnt waits do not include it.  PGM_EXP 32: at the top
-    constexpr bool EARLY_STAGE = ONE && MODE == 2 && NBUF == 2 && PGM_EXP != 32;
-    // FUSED_NORM: the early row DMA goes out from waves 1-3 while wave 0 polls the image flags (no norm hand-off left
-    // to hide it under; measured 6.17 -> 6.10 ms against issuing it after the sum of squares, PGM_EXP 26)
-    constexpr bool DMA_POLL = PGM_FUSED_NORM && PGM_EXP != 26;
+    // single-tile MODE 2: the next pass's row DMA is issued by waves 1-3 while wave 0 polls the image flags (they
+    // wait at that barrier anyway) and retired by the step's last barrier, instead of at the top of the step; wave 0
+    // keeps no DMA in its queue so its polls' vmcnt waits do not include it (6.17 -> 6.10 ms against issuing it after
+    // the sum of squares)
+    constexpr bool EARLY_STAGE = ONE && MODE == 2 && NBUF == 2;
     constexpr int CR = RS / 4;                         // 16-B chunks per packed row
     constexpr int NDT = (SBk * RSL) / 256;             // LDS-DMA wave instructions per pass (1 KiB each)
     static_assert(NDT * 256 == SBk * RSL, "staging split");
@@ -186,18 +169,11 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
     // MODE 2 block map (speed only: the hand-off is correct under any placement; blocks b, b + 8, ... share an XCD
     // under round-robin dispatch)
     const int bx = (int)blockIdx.x;
-#if PGM_MODE2_XCD4
     // groups of 32 blocks for 8 tasks: block r holds half (r >> 4) & 1 of tower (r >> 3) & 1 of task 8g + (r & 7)
     const int p = MODE == 2 ? 8 * (bx >> 5) + (bx & 7) : SPLIT ? (bx >> 1) : bx;
-    const int hs = MODE == 2 ? (bx >> 4) & 1 : 0;
+    const int hs = MODE == 2 ? (bx >> 4) & 1 : 0;  // half of the minibatch rows
     if (p >= a.P) return;
-    const int m = MODE == 2 ? (bx >> 3) & 1 : SPLIT ? (bx & 1) : (w & 1);
-#else  // groups of 16 blocks for 4 tasks: block r holds half r >> 3 of tower r & 1 of task 4g + ((r & 7) >> 1)
-    const int p = MODE == 2 ? 4 * (bx >> 4) + ((bx & 7) >> 1) : SPLIT ? (bx >> 1) : bx;
-    const int hs = MODE == 2 ? (bx >> 3) & 1 : 0;  // half of the minibatch rows
-    if (p >= a.P) return;
-    const int m = MODE == 2 ? (bx & 1) : SPLIT ? (bx & 1) : (w & 1);  // tower of this wave
-#endif
+    const int m = MODE == 2 ? (bx >> 3) & 1 : SPLIT ? (bx & 1) : (w & 1);  // tower of this wave
     const int sh = SPLIT ? w : (w >> 1);                      // wave index within the tower
     const int NQ = m == 0 ? K : A;
     const int N = a.N, T = a.T, B = T * N;
@@ -300,8 +276,6 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
             f32x16 gW2[2][2], gW1[2];  // [in tile][out tile], [out tile] (O <= 32: one in tile)
             float gWh[2][Q], gB1[2], gB2[2];
             float gsm = 0.f;  // lanes q < Q: head-bias gradient q; lanes 32 + q (actor): logstd gradient q
-            // MFMA heads: per-lane partial head-bias / logstd sums of outputs q = 4 ((l >> 4) & 1) + r
-            float gbq[4] = {0.f, 0.f, 0.f, 0.f}, glq[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
 #pragma unroll
@@ -316,14 +290,11 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
             for (int s0 = 0; ONE ? s0 < 1 : s0 < mbs; s0 += (ONE ? 1 : SBk), ++gp) {
                 const int ns = ONE ? SBk : min(SBk, mbs - s0);
                 const int cur = NBUF == 2 ? (gp & 1) : 0;
-                // stage the next pass while this one computes; LATE_STAGE (single-tile A/B): issued behind the
-                // layer-1 MFMAs, so the index reads and DMA issue overlap the matrix pipe
-                constexpr bool LATE_STAGE = ONE && NBUF == 2 && PGM_EXP == 31;
-                auto stage_next = [&]() {
+                // stage the next pass while this one computes
+                if constexpr (NBUF == 2 && !EARLY_STAGE) {
                     if (gp + 1 < npass) issue_rows(cur ^ 1, (gp + 1) & 1);
                     if (gp + 2 < npass) issue_idx(gp + 2, gp & 1);
-                };
-                if constexpr (NBUF == 2 && !LATE_STAGE && !EARLY_STAGE) stage_next();
+                }
                 const float* rb = &S.RB[cur][0];
                 PGM_STAMP(0);
 
@@ -341,21 +312,12 @@ __global__ __launch_bounds__(MT) void ppo_update_mfma_kernel(MArgs a) {
 #pragma unroll
                         for (int hb = 0; hb < 2; ++hb) z[hb] = mfma(av, k < O ? W.W1t[k][hb * TS + c] : 0.f, z[hb]);
                     }
-                    if constexpr (LATE_STAGE) stage_next();
 #pragma unroll
                     for (int hb = 0; hb < 2; ++hb) {
                         const float bias = W.b1[hb * TS + c];
-#if PGM_PK_ELEM
                         tanh_bias_pk<16>(z[hb], bias, H1[hb]);
 #pragma unroll
                         for (int r = 0; r < 16; ++r) scr[rowof(r, h) * SCR + hb * TS + c] = H1[hb][r];
-#else
-#pragma unroll
-                        for (int r = 0; r < 16; ++r) {
-                            H1[hb][r] = tanh_fast(z[hb][r] + bias);
-                            scr[rowof(r, h) * SCR + hb * TS + c] = H1[hb][r];
-                        }
-#endif
                     }
                     wave_lds_fence();
                     // ---- layer 2: Z2[s][o] = H1[s][:] . W2t[:][o]   (A from the transpose tile)
@@ -371,12 +333,7 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
 #pragma unroll
                     for (int ob = 0; ob < 2; ++ob) {
                         const float bias = W.b2[ob * TS + c];
-#if PGM_PK_ELEM
                         tanh_bias_pk<16>(z[ob], bias, H2[ob]);
-#else
-#pragma unroll
-                        for (int r = 0; r < 16; ++r) H2[ob][r] = tanh_fast(z[ob][r] + bias);
-#endif
                     }
                     PGM_STAMP(4);
                     wave_lds_fence();  // every lane finished reading the H1 tile
@@ -385,117 +342,10 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
 #pragma unroll
                         for (int r = 0; r < 16; ++r) scr[rowof(r, h) * SCR + ob * TS + c] = H2[ob][r];
                     wave_lds_fence();
-#if PGM_HEADS_MFMA
-                    // ---- heads on the 16x16x4 MFMA: out^T[q][s] = Wh[q][:] . H2[s][:] for two 16-sample blocks sb
-                    // (A = Wh rows, zero for q >= Q; B = the H2 transpose tile).  C layout of block sb: lane l, register
-                    // r <-> output q = 4 (l >> 4) + r of sample 16 sb + (l & 15) (lane groups 2, 3: zero rows)
-                    const int g4 = l >> 4, c16 = l & 15;
-                    f32x4 ho[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-                    // operands in batches of 8 k-steps, all reads of a batch issued before its MFMAs (one LDS latency
-                    // per batch, not per MFMA); the Wh row read unconditionally (clamped) and masked after
-                    const float* whr = &W.Wh[c16 < Q ? c16 : Q - 1][g4];
-                    const float* h2r = scr + c16 * SCR + g4;
-                    const float qm = c16 < Q ? 1.f : 0.f;
-#pragma unroll
-                    for (int kb = 0; kb < H / 32; ++kb) {
-                        float aw[8], b0[8], b1[8];
-#pragma unroll
-                        for (int j = 0; j < 8; ++j) {
-                            const int u = 4 * (8 * kb + j);
-                            aw[j] = whr[u];
-                            b0[j] = h2r[u];
-                            b1[j] = h2r[16 * SCR + u];
-                        }
-                        // every read of the batch issued before its first MFMA (the MFMAs depend on this point)
-#pragma unroll
-                        for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(aw[j]), "+v"(b0[j]), "+v"(b1[j]));
-#pragma unroll
-                        for (int j = 0; j < 8; ++j) {
-                            ho[0] = mfma16(aw[j] * qm, b0[j], ho[0]);
-                            ho[1] = mfma16(aw[j] * qm, b1[j], ho[1]);
-                        }
-                    }
-                    // block 1's lane groups 0, 1 -> lanes 32-63: lane l now holds outputs q = 4 gq + r of sample sl
-                    const int gq = (l >> 4) & 1, sl = 16 * h + c16;
-                    float ov[4];
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(ho[0][r]), __float_as_uint(ho[1][r]),
-                                                                         false, false);
-                        ov[r] = __uint_as_float(sw[0]);
-                    }
-                    PGM_STAMP(16);
-                    // ---- per-sample loss gradients (ppo.py:80-96) of sample sl; lanes l and l ^ 16 share it
-                    const bool ok = ts0 + sl < ns;
-                    float dq[4];
-                    if (m == 0) {  // value loss over the K objectives (q = r of lane group 0)
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            const int q = 4 * gq + r;
-                            const bool qv = q < K;
-                            const float V = ov[r] + (qv ? W.bh[qv ? q : 0] : 0.f);
-                            const float Vo = rowf(rt, sl, O + A + 2 + (qv ? q : 0));
-                            const float R = rowf(rt, sl, O + A + 2 + K + (qv ? q : 0));
-                            float gv, ls;
-                            if (a.hp.use_clipped_value_loss) {
-                                const float dv = V - Vo;
-                                const float vc = Vo + fminf(fmaxf(dv, -clip), clip);
-                                const float l1 = (V - R) * (V - R), l2 = (vc - R) * (vc - R);
-                                const float inr = (dv >= -clip && dv <= clip) ? 1.f : 0.f;
-                                gv = wmax2(l1, l2) * 2.f * (V - R) + wmax2(l2, l1) * 2.f * (vc - R) * inr;
-                                ls = fmaxf(l1, l2);
-                            } else {
-                                gv = 2.f * (V - R);
-                                ls = (R - V) * (R - V);
-                            }
-                            dq[r] = ok && qv ? vscale * gv : 0.f;
-                            if (ok && qv) lsum += ls;  // every (sample, output) sits in exactly one lane
-                            gbq[r] += dq[r];
-                        }
-                    } else {  // clipped surrogate; the log-prob is the sum over the lane pair's outputs
-                        float diff[4], lpe = 0.f;
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            const int q = 4 * gq + r;
-                            const bool qv = q < A;
-                            diff[r] = qv ? rowf(rt, sl, O + (qv ? q : 0)) - (ov[r] + W.bh[qv ? q : 0]) : 0.f;
-                            lpe += qv ? -0.5f * diff[r] * diff[r] * S.aiv[qv ? q : 0] - lstd[qv ? q : 0] - LOG_SQRT_2PI
-                                      : 0.f;
-                        }
-                        const float lp = lpe + __shfl_xor(lpe, 16, 64);
-                        const float ratio = expf(lp - rowf(rt, sl, O + A));
-                        const float ad = rowf(rt, sl, O + A + 1);
-                        const float s1 = ratio * ad;
-                        const float s2 = fminf(fmaxf(ratio, 1.f - clip), 1.f + clip) * ad;
-                        const float inr = (ratio >= 1.f - clip && ratio <= 1.f + clip) ? 1.f : 0.f;
-                        const float gr = ad * (wmin2(s1, s2) + wmin2(s2, s1) * inr);
-                        const float dlp = ok ? ascale * gr * ratio : 0.f;
-                        if (ok && gq == 0) lsum += -fminf(s1, s2);
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            const int q = 4 * gq + r;
-                            const bool qv = q < A;
-                            const float iv = qv ? S.aiv[qv ? q : 0] : 0.f;
-                            dq[r] = qv ? dlp * diff[r] * iv : 0.f;
-                            gbq[r] += dq[r];
-                            glq[r] += qv ? dlp * (diff[r] * diff[r] * iv - 1.f) : 0.f;
-                        }
-                    }
-                    // dO tile [sample][q] (this wave's): the dH2 A operand (lane = sample) and the head-weight grads
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int q = 4 * gq + r;
-                        if (q < Q) S.dout[w][sl][q < Q ? q : 0] = dq[r];
-                    }
-                    PGM_STAMP(17);
-                    wave_lds_fence();
-                    PGM_STAMP(18);
-#else
                     // ---- heads on the VALU: lane = sample c, half h sums units [32h, 32h+32)
                     float outv[Q];
-#if PGM_EXP != 27
                     // packed: v_pk_fma_f32 over unit pairs (even / odd partial sums, added at the end; Walker P = 40
-                    // 5.845 -> 5.79-5.83 ms).  PGM_EXP 27 (A/B): one scalar FMA chain per output
+                    // 5.845 -> 5.79-5.83 ms against one scalar FMA chain per output)
                     f2v acc2[Q];
 #pragma unroll
                     for (int q = 0; q < Q; ++q) acc2[q] = f2v{0.f, 0.f};
@@ -509,16 +359,6 @@ PGM_UNROLL(16)
                     }
 #pragma unroll
                     for (int q = 0; q < Q; ++q) outv[q] = acc2[q].x + acc2[q].y;
-#else
-#pragma unroll
-                    for (int q = 0; q < Q; ++q) outv[q] = 0.f;
-PGM_UNROLL(ONE ? PGM_U_HEAD : 4)
-                    for (int u = 0; u < TS; ++u) {
-                        const float hv = scr[c * SCR + h * TS + u];
-#pragma unroll
-                        for (int q = 0; q < Q; ++q) outv[q] = fmaf(hv, W.Wh[q][h * TS + u], outv[q]);
-                    }
-#endif
 #pragma unroll
                     for (int q = 0; q < Q; ++q) outv[q] = half_sum(outv[q]) + W.bh[q];
                     PGM_STAMP(16);
@@ -586,11 +426,10 @@ PGM_UNROLL(ONE ? PGM_U_HEAD : 4)
 #pragma unroll 8
                         for (int cc = 0; cc < TS; ++cc) gsm += src[cc * Q];
                     }
-#endif
                     PGM_STAMP(5);
                     // ---- head-weight grads (VALU, C layout): gWh[ob][q] += sum_r H2[s][u] dO[s][q]; output pairs on the
-                    // packed ALU (each output still sums over r in order: the same values).  PGM_EXP 33 (A/B): scalar
-                    constexpr bool GWH_PK = Q % 2 == 0 && PGM_EXP != 33;
+                    // packed ALU (each output still sums over r in order: the same values)
+                    constexpr bool GWH_PK = Q % 2 == 0;
 #pragma unroll
                     for (int ob = 0; ob < 2; ++ob)
 #pragma unroll
@@ -615,28 +454,16 @@ PGM_UNROLL(ONE ? PGM_U_HEAD : 4)
 #pragma unroll
                     for (int ks = 0; ks < (Q + 1) / 2; ++ks) {
                         const int q = 2 * ks + h;
-#if PGM_HEADS_MFMA
-                        const float av = q < Q ? S.dout[w][c][q < Q ? q : 0] : 0.f;  // lane = sample c, k = output q
-#else
                         const float av = h ? (2 * ks + 1 < Q ? dO[2 * ks + 1] : 0.f) : dO[2 * ks];
-#endif
 #pragma unroll
                         for (int ob = 0; ob < 2; ++ob) z[ob] = mfma(av, q < Q ? W.Wh[q][ob * TS + c] : 0.f, z[ob]);
                     }
                     f32x16 dZ2[2];
 #pragma unroll
                     for (int ob = 0; ob < 2; ++ob) {
-#if PGM_PK_ELEM
                         dtanh_pk<16>(z[ob], H2[ob], dZ2[ob]);
 #pragma unroll
                         for (int r = 0; r < 16; ++r) gB2[ob] += dZ2[ob][r];
-#else
-#pragma unroll
-                        for (int r = 0; r < 16; ++r) {
-                            dZ2[ob][r] = z[ob][r] * (1.f - H2[ob][r] * H2[ob][r]);
-                            gB2[ob] += dZ2[ob][r];
-                        }
-#endif
                     }
                     PGM_STAMP(6);
                     // ---- dH1 = dZ2 W2  (A = dZ2 through the transpose tile, B = W2t[in][o] column); the critical
@@ -646,19 +473,6 @@ PGM_UNROLL(ONE ? PGM_U_HEAD : 4)
                     for (int ob = 0; ob < 2; ++ob)
 #pragma unroll
                         for (int r = 0; r < 16; ++r) scr[rowof(r, h) * SCR + ob * TS + c] = dZ2[ob][r];
-                    // ---- dW2^T[in][o] += H1^T dZ2: straight from the C-layout registers.  GW2_FIRST: issued while the
-                    // dZ2 transpose tile lands (its MFMAs cover the LDS round trip); otherwise behind dH1, in the
-                    // MFMA pipe while the VALU forms dZ1 from the dH1 results
-                    constexpr bool GW2_FIRST = PGM_EXP == 11;
-                    auto gw2 = [&]() {
-#pragma unroll
-                        for (int r = 0; r < 16; ++r)
-#pragma unroll
-                            for (int ib = 0; ib < 2; ++ib)
-#pragma unroll
-                                for (int ob = 0; ob < 2; ++ob) gW2[ib][ob] = mfma(H1[ib][r], dZ2[ob][r], gW2[ib][ob]);
-                    };
-                    if constexpr (GW2_FIRST) gw2();
                     wave_lds_fence();
                     z[0] = z[1] = f32x16{0};
 PGM_UNROLL(ONE ? PGM_U_L2 : 8)
@@ -668,21 +482,20 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
 #pragma unroll
                         for (int ib = 0; ib < 2; ++ib) z[ib] = mfma(av, W.W2t[ib * TS + c][k], z[ib]);
                     }
-                    if constexpr (!GW2_FIRST) gw2();
+                    // ---- dW2^T[in][o] += H1^T dZ2: straight from the C-layout registers, behind dH1 in the MFMA pipe
+                    // while the VALU forms dZ1 from the dH1 results
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+#pragma unroll
+                        for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+                            for (int ob = 0; ob < 2; ++ob) gW2[ib][ob] = mfma(H1[ib][r], dZ2[ob][r], gW2[ib][ob]);
                     f32x16 dZ1[2];
 #pragma unroll
                     for (int ib = 0; ib < 2; ++ib) {
-#if PGM_PK_ELEM
                         dtanh_pk<16>(z[ib], H1[ib], dZ1[ib]);
 #pragma unroll
                         for (int r = 0; r < 16; ++r) gB1[ib] += dZ1[ib][r];
-#else
-#pragma unroll
-                        for (int r = 0; r < 16; ++r) {
-                            dZ1[ib][r] = z[ib][r] * (1.f - H1[ib][r] * H1[ib][r]);
-                            gB1[ib] += dZ1[ib][r];
-                        }
-#endif
                     }
                     // ---- dW1^T[k][h] += X^T dZ1  (A = X[s(r)][k = lane], B = dZ1 reg r)
 #pragma unroll
@@ -719,14 +532,6 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
                 for (int q = 0; q < Q; ++q) gWh[i][q] = half_sum(gWh[i][q]);
             }
             lsum = wave_sum64(lsum);
-#if PGM_HEADS_MFMA
-            // column sums over the samples: 16-lane rows (one sample block each), then the two blocks
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                gbq[r] = half_sum(row_sum16(gbq[r]));
-                glq[r] = half_sum(row_sum16(glq[r]));
-            }
-#endif
             // entropy with the logstd of this step (before Adam)
             float ent = 0.f;
 #pragma unroll
@@ -793,24 +598,11 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
                         }
                     }
                     if (half == 1) {
-#if PGM_HEADS_MFMA
-                        if (l == 0 || l == 16) {  // lane 16 gq holds the sums of outputs 4 gq .. 4 gq + 3
-                            const float ec = add || hs != 0 || (w >> 1) != 0 ? 0.f : a.hp.entropy_coef;  // once per tower: part 0, image 0
-#pragma unroll
-                            for (int r = 0; r < 4; ++r) {
-                                const int q = 4 * (l >> 4) + r;
-                                if (q < NQ) acc(oBh + q, gbq[r]);
-                                // -entropy_coef * d(mean entropy)/d logstd enters once (ppo.py:98)
-                                if (m == 1 && q < A) acc(oLs + q, glq[r] - ec);
-                            }
-                        }
-#else
                         if (h == 0 && c < NQ) acc(oBh + c, gsm);
                         if (m == 1 && h == 1 && c < A) {  // -entropy_coef * d(mean entropy)/d logstd enters once (ppo.py:98)
                             const float ec = add || hs != 0 || (w >> 1) != 0 ? 0.f : a.hp.entropy_coef;  // once per tower: part 0, image 0
                             acc(oLs + c, gsm - ec);
                         }
-#endif
                         if (!add) {  // padding slots of a freshly written image
                             Gt[oW2 + l * SCR + H] = 0.f;
                             for (int q = NQ; q < Q; ++q) Gt[oWh + q * H + l] = 0.f;
@@ -865,17 +657,16 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
                 lds_sync_m();
                 PGM_STAMP(10);
-                if constexpr (EARLY_STAGE && DMA_POLL) {  // next pass: rows by waves 1-3 while wave 0 polls
+                if constexpr (EARLY_STAGE) {  // next pass: rows by waves 1-3 while wave 0 polls
                     if (w != 0) {
                         if (gp < npass) issue_rows_n(gp & 1, gp & 1, w - 1, ic<3>{});
                         if (gp + 1 < npass) issue_idx(gp + 1, (gp + 1) & 1, w - 1, 3);
                     }
                 }
-                // the other tower's half slots (FUSED_NORM: their images are gathered too)
+                // the other tower's half slots (their images are gathered too)
                 const int slot_t0 = ((p * 2 + (1 - m)) * 2 + 0) * 2 + par;
                 const int off_t0 = slot_t0 * a.xslot * 8, off_t1 = (slot_t0 + 2) * a.xslot * 8;
-                constexpr int NPOLL = PGM_FUSED_NORM ? 3 : 1;
-                if (t < NPOLL) {  // lane 0: the partner half; FUSED_NORM lanes 1, 2: the other tower's halves
+                if (t < 3) {  // lane 0: the partner half; lanes 1, 2: the other tower's halves
                     if (t == 0) {
                         unsigned long long* flag_mine = a.xb + (size_t)slot_mine * a.xslot + a.xslot - 1;
                         __hip_atomic_store(flag_mine, ((unsigned long long)tag << 32) | __float_as_uint(lsum_wg),
@@ -901,8 +692,7 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
                     }
                 }
                 lds_sync_m();  // the polling lanes matched: every wave may load the partners' images
-                // every image load of this thread first (the partner half's; FUSED_NORM: both halves of the other
-                // tower).  (Issuing the next pass's row DMA right behind them, all four waves: 6.16 -> 6.25 ms.)
+                // every image load of this thread first (the partner half's and both halves of the other tower).  (Issuing the next pass's row DMA right behind them, all four waves: 6.16 -> 6.25 ms.)
                 u32x4 vo[NG4];
 #pragma unroll
                 for (int k = 0; k < NG4; ++k)
@@ -910,7 +700,6 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
                 float ovt = 0.f;
                 if (t < TAIL)
                     ovt = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, off_other + 16 * NV4 + 4 * t, 0, SC1));
-#if PGM_FUSED_NORM
                 u32x4 o0[NG4], o1[NG4];
 #pragma unroll
                 for (int k = 0; k < NG4; ++k) {
@@ -923,7 +712,6 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
                     ot0 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, off_t0 + 16 * NV4 + 4 * t, 0, SC1));
                     ot1 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, off_t1 + 16 * NV4 + 4 * t, 0, SC1));
                 }
-#endif
                 // g = half0 + half1 of this thread's float4 groups i = t + k*MT stays in registers (no LDS
                 // round trip); the sum of squares is fused in
 #pragma unroll
@@ -943,7 +731,6 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
                     agt = hs == 0 ? mine + ovt : ovt + mine;
                     sq2 = fmaf(agt, agt, sq2);
                 }
-#if PGM_FUSED_NORM
                 // the other tower's g = half0 + half1 and its sum of squares, element by element in the owner's order
                 // (the owner forms the same sums from its own half and this very slot pair)
                 {
@@ -962,7 +749,6 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
                     sqo = wave_sum64(sqo);
                     if (l == 0) S.red[4 + w] = sqo;
                 }
-#endif
                 // the Adam operands of the same groups
 #pragma unroll
                 for (int k = 0; k < NG4; ++k) {
@@ -991,13 +777,7 @@ PGM_UNROLL(ONE ? PGM_U_L2 : 8)
             lds_sync_m();
             PGM_STAMP(8);
             float total = (S.red[0] + S.red[1]) + (S.red[2] + S.red[3]);
-            if constexpr (EARLY_STAGE && !DMA_POLL) {  // next pass: rows by waves 1-3 (retired by the step's last barrier)
-                if (w != 0) {
-                    if (gp < npass) issue_rows_n(gp & 1, gp & 1, w - 1, ic<3>{});
-                    if (gp + 1 < npass) issue_idx(gp + 1, (gp + 1) & 1, w - 1, 3);
-                }
-            }
-            if constexpr (SPLIT && NS == 2 && PGM_FUSED_NORM) {  // the other tower's total, formed here
+            if constexpr (SPLIT && NS == 2) {  // the other tower's total, formed here
                 const float other = (S.red[4] + S.red[5]) + (S.red[6] + S.red[7]);
                 total = m == 0 ? total + other : other + total;  // critic + actor in all four workgroups
             } else if constexpr (SPLIT) {  // tagged 8-byte granule hand-off with the other tower's workgroup
@@ -1238,8 +1018,8 @@ __global__ __launch_bounds__(64 * W) void ppo_update_t16_kernel(MArgs a) {
     constexpr int NBUF = t16_nbuf<O, A, K, W>();
     constexpr int CR = RS / 4;
     // single-tile: the next pass's row DMA by waves 1..W-1 while wave 0 polls the tower-norm granule, retired by the
-    // step's last barrier (as in the 32-row kernel); PGM_EXP 32: at the top of the step
-    constexpr bool EARLY_STAGE = ONE && NBUF == 2 && W > 1 && PGM_EXP != 32;
+    // step's last barrier (as in the 32-row kernel)
+    constexpr bool EARLY_STAGE = ONE && NBUF == 2 && W > 1;
     constexpr int NDT = (SBk * RSL) / 256;
     static_assert(NDT * 256 == SBk * RSL, "staging split");
     constexpr int oW2 = O * H, oWh = oW2 + H * SCR, oB1 = oWh + Q * H, oB2 = oB1 + H, oBh = oB2 + H, oLs = oBh + Q;
@@ -1248,16 +1028,10 @@ __global__ __launch_bounds__(64 * W) void ppo_update_t16_kernel(MArgs a) {
     // block map (speed only: the hand-offs are correct under any placement; blocks b, b + 8, ... share an XCD under
     // round-robin dispatch)
     const int bx = (int)blockIdx.x;
-#if PGM_T16_XCD8
     // groups of 16 NS blocks for 8 tasks: block r holds part (r >> 4) % NS of tower (r >> 3) & 1 of task 8 G + (r & 7)
     const int j16 = (bx >> 3) % (2 * NS);
     const int p = 8 * (bx / (16 * NS)) + (bx & 7);
     const int hs = j16 >> 1, m = j16 & 1;
-#else  // groups of 8 NS blocks for 4 tasks: block r holds part r >> 3 of tower r & 1 of task 4 G + ((r & 7) >> 1)
-    const int r8 = bx % (8 * NS);
-    const int p = 4 * (bx / (8 * NS)) + ((r8 & 7) >> 1);
-    const int hs = r8 >> 3, m = r8 & 1;
-#endif
     if (p >= a.P) return;
     const int NQ = m == 0 ? K : A;
     const int N = a.N, T = a.T, B = T * N;
@@ -1377,17 +1151,9 @@ __global__ __launch_bounds__(64 * W) void ppo_update_t16_kernel(MArgs a) {
 #pragma unroll
                     for (int hb = 0; hb < 4; ++hb) {
                         const float bias = Wt.b1[hb * T16 + c];
-#if PGM_PK_ELEM
                         tanh_bias_pk<4>(z[hb], bias, H1[hb]);
 #pragma unroll
                         for (int r = 0; r < 4; ++r) scr[(4 * g + r) * S16 + hb * T16 + c] = H1[hb][r];
-#else
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            H1[hb][r] = tanh_fast(z[hb][r] + bias);
-                            scr[(4 * g + r) * S16 + hb * T16 + c] = H1[hb][r];
-                        }
-#endif
                     }
                     wave_lds_fence();
                     // ---- layer 2: Z2[s][o] = H1[s][:] . W2t[:][o]  (A from the transpose tile)
@@ -1404,12 +1170,7 @@ PGM_UNROLL(ONE ? PGM_U16 : 4)
 #pragma unroll
                     for (int ob = 0; ob < 4; ++ob) {
                         const float bias = Wt.b2[ob * T16 + c];
-#if PGM_PK_ELEM
                         tanh_bias_pk<4>(z[ob], bias, H2[ob]);
-#else
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) H2[ob][r] = tanh_fast(z[ob][r] + bias);
-#endif
                     }
                     PGM_STAMP(4);
                     wave_lds_fence();  // every lane finished reading the H1 tile
@@ -1500,35 +1261,15 @@ PGM_UNROLL(ONE ? PGM_U16 : 4)
                     f32x4 dZ2[4];
 #pragma unroll
                     for (int ob = 0; ob < 4; ++ob) {
-#if PGM_PK_ELEM
                         dtanh_pk<4>(z[ob], H2[ob], dZ2[ob]);
 #pragma unroll
                         for (int r = 0; r < 4; ++r) gB2[ob] += dZ2[ob][r];
-#else
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            dZ2[ob][r] = z[ob][r] * (1.f - H2[ob][r] * H2[ob][r]);
-                            gB2[ob] += dZ2[ob][r];
-                        }
-#endif
                     }
                     PGM_STAMP(6);
 #pragma unroll
                     for (int ob = 0; ob < 4; ++ob)
 #pragma unroll
                         for (int r = 0; r < 4; ++r) scr[(4 * g + r) * S16 + ob * T16 + c] = dZ2[ob][r];
-                    // ---- dW2^T[in][o] += H1^T dZ2 straight from the C registers.  GW2_FIRST: issued while the dZ2
-                    // transpose tile lands; otherwise behind dH1 (whose MFMAs then go into the pipe first)
-                    constexpr bool GW2_FIRST = PGM_EXP == 12;
-                    auto gw2 = [&]() {
-#pragma unroll
-                        for (int r = 0; r < 4; ++r)
-#pragma unroll
-                            for (int ib = 0; ib < 4; ++ib)
-#pragma unroll
-                                for (int ob = 0; ob < 4; ++ob) gW2[ib][ob] = mfma16(H1[ib][r], dZ2[ob][r], gW2[ib][ob]);
-                    };
-                    if constexpr (GW2_FIRST) gw2();
                     wave_lds_fence();
                     // ---- dH1 = dZ2 W2 (A = dZ2 through the transpose tile, B = W2t[in][o] column)
 #pragma unroll
@@ -1540,21 +1281,19 @@ PGM_UNROLL(ONE ? PGM_U16 : 4)
 #pragma unroll
                         for (int ib = 0; ib < 4; ++ib) z[ib] = mfma16(av, Wt.W2t[ib * T16 + c][k], z[ib]);
                     }
-                    if constexpr (!GW2_FIRST) gw2();
+                    // ---- dW2^T[in][o] += H1^T dZ2 straight from the C registers, behind dH1 (whose MFMAs go first)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+#pragma unroll
+                        for (int ib = 0; ib < 4; ++ib)
+#pragma unroll
+                            for (int ob = 0; ob < 4; ++ob) gW2[ib][ob] = mfma16(H1[ib][r], dZ2[ob][r], gW2[ib][ob]);
                     f32x4 dZ1[4];
 #pragma unroll
                     for (int ib = 0; ib < 4; ++ib) {
-#if PGM_PK_ELEM
                         dtanh_pk<4>(z[ib], H1[ib], dZ1[ib]);
 #pragma unroll
                         for (int r = 0; r < 4; ++r) gB1[ib] += dZ1[ib][r];
-#else
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            dZ1[ib][r] = z[ib][r] * (1.f - H1[ib][r] * H1[ib][r]);
-                            gB1[ib] += dZ1[ib][r];
-                        }
-#endif
                     }
                     // ---- dW1^T[k][h] += X^T dZ1  (A = X[sample 4g + r][feature 16 kb + c], B = dZ1 register r)
 #pragma unroll
@@ -2023,7 +1762,7 @@ static int launch_t16_k(const pgm_dims* d, const MArgs& a, hipStream_t stream) {
 template <int O, int A, int K, int NS, int W>
 int launch_t16(const pgm_dims* d, const MArgs& a, hipStream_t stream) {
     const int mb = d->T * d->N / a.hp.num_mini_batch;
-    if (mb == NS * W * T16 && !getenv("PGM_NO_ONE")) return launch_t16_k<O, A, K, NS, W, true>(d, a, stream);
+    if (mb == NS * W * T16) return launch_t16_k<O, A, K, NS, W, true>(d, a, stream);
     return launch_t16_k<O, A, K, NS, W, false>(d, a, stream);
 }
 
@@ -2059,7 +1798,7 @@ template <int O, int A, int K, int MODE>
 int launch_mode(const pgm_dims* d, const MArgs& a, hipStream_t stream) {
     using Sm = MSmem<O, A, K, true>;
     if constexpr (MODE == 2) {  // 2 workgroups x 4 waves x one 32-row tile = the minibatch, in one pass
-        if (d->T * d->N / a.hp.num_mini_batch == 2 * 4 * TS && Sm::SBk >= 4 * TS && !getenv("PGM_NO_ONE"))
+        if (d->T * d->N / a.hp.num_mini_batch == 2 * 4 * TS && Sm::SBk >= 4 * TS)
             return launch_mode_k<O, A, K, MODE, true>(d, a, stream);
     }
     return launch_mode_k<O, A, K, MODE, false>(d, a, stream);
@@ -2072,9 +1811,9 @@ int ppo_update_fs(const pgm_dims* d, const MArgs& a, int ns, bool dual, hipStrea
 //   * feature-split with the reduce-scattered Adam (pgm_ppo_fs.hip) while it gets >= FS_AUTO_NS parts per tower
 //     (small per-GPU populations: the latency form), or always with PGM_UPDATE_KERNEL=fs;
 //   * else the row-split kernels, PGM_UPDATE_SPLIT capping them: 4 (default) = 16-row tiles on 4 workgroups per
-//     tower (8 CUs per task, while t16_grid(P, 4) <= CUs), 3 = 16-row tiles on 2 workgroups of 8 waves (A/B only,
-//     selected only explicitly), 2 = 32-row tiles on 2 workgroups per tower (MODE 2, while mode2_grid(P) <= CUs),
-//     1 = one workgroup per tower (2P <= CUs), 0 = one per task; each falls back to the next one down.
+//     tower (8 CUs per task, while t16_grid(P, 4) <= CUs), 2 = 32-row tiles on 2 workgroups per tower (MODE 2, while
+//     mode2_grid(P) <= CUs), 1 = one workgroup per tower (2P <= CUs), 0 = one per task; each falls back to the next
+//     one down.  (16-row tiles on 2 workgroups of 8 waves measured slower than MODE 2 everywhere: 7.37 vs 6.55 ms.)
 // PGM_UPDATE_KERNEL other than fs / auto (e.g. "mfma", the tests' row-split A/B) or any PGM_UPDATE_SPLIT keeps the
 // row-split kernels.
 constexpr int FS_AUTO_NS = 4;
@@ -2093,7 +1832,6 @@ static UpdateChoice choose_update(const pgm_dims* d, int mb) {
     const int cap = sel && sel[0] >= '0' && sel[0] <= '4' ? sel[0] - '0' : 4;
     const int cus = device_cu_count();
     if (cap >= 4 && t16_grid(d->P, 4) <= cus) return {1, 4, 4, 0, 0};
-    if (cap == 3 && t16_grid(d->P, 2) <= cus) return {1, 2, 8, 0, 0};
     if (cap >= 2 && mode2_grid(d->P) <= cus) return {0, 2, 4, 2, 0};
     if (cap >= 1 && 2 * d->P <= cus) return {0, 1, 4, 1, 0};
     return {0, 1, 4, 0, 0};
@@ -2124,7 +1862,7 @@ int launch_ppo_update_mfma(const pgm_dims* d, const MArgs& a, const pgm_rollout_
     static_assert(sizeof(MSmem<O, A, K, true>) > 80 * 1024, "split residency argument needs > 80 KiB LDS");
     const UpdateChoice c = choose_update(d, d->T * d->N / a.hp.num_mini_batch);
     if (c.kind == 2) return ppo_update_fs(d, a, c.ns, c.dual != 0, stream);
-    if (c.kind == 1) return c.ns == 4 ? launch_t16<O, A, K, 4, 4>(d, a, stream) : launch_t16<O, A, K, 2, 8>(d, a, stream);
+    if (c.kind == 1) return launch_t16<O, A, K, 4, 4>(d, a, stream);
     if (c.mode == 2) return launch_mode<O, A, K, 2>(d, a, stream);
     if (c.mode == 1) return launch_mode<O, A, K, 1>(d, a, stream);
     return launch_mode<O, A, K, 0>(d, a, stream);

@@ -32,18 +32,14 @@
 
 PGM_STAMP_UNIT(wupd)
 
-// unroll depths of the layer-2 / dH1 and VALU-head loops (A/B: scripts/build_var.sh, -DPGM_EXP=n)
-#ifndef PGM_EXP
-#define PGM_EXP 0
-#endif
+// unroll depths of the layer-2 / dH1 and VALU-head loops (deeper unrolls: spills unchanged or higher)
 #define PGM_PRAGMA_W(x) _Pragma(#x)
 #define PGM_UNROLL_W(n) PGM_PRAGMA_W(unroll n)
-#define PGM_UW_L2 (PGM_EXP == 7 || PGM_EXP == 9 ? 32 : 8)
-#define PGM_UW_HEAD (PGM_EXP == 8 || PGM_EXP == 9 ? 32 : 4)
+#define PGM_UW_L2 8
+#define PGM_UW_HEAD 4
 // block map: the two towers of a row part on one XCD (they read the same observation rows in the same phase, so the
-// second read hits that XCD's L2): Humanoid P = 20 update 31.1 -> 30.4 ms, 56.2 -> 47.8 GB per launch
-// (profiles/r03o_*).  PGM_EXP 50 (A/B): the round-2 map (the NS parts of one tower on one XCD)
-#define PGM_WIDE_COLOC (PGM_EXP != 50)
+// second read hits that XCD's L2): Humanoid P = 20 update 31.1 -> 30.4 ms, 56.2 -> 47.8 GB per launch against the
+// round-2 map, the NS parts of one tower on one XCD (profiles/r03o_*)
 // (the VALU heads and elementwise tanh on register pairs through the packed fp32 ALU, as in the narrow kernels, made
 // this kernel slower: 30.4 -> 33.3 ms at Humanoid P = 20, it already runs at the 512-register limit)
 // (all 2 NS workgroups of a task on one XCD, groups of 8 tasks: 30.4 -> 30.6-30.7 ms, kept out)
@@ -167,7 +163,6 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
     // dispatch (speed only: every hand-off is correct under any placement)
     const int bx = (int)blockIdx.x;
     const int r8 = bx % (8 * NS);
-#if PGM_WIDE_COLOC
     // co-located map (NS > 1): XCD slot x = r8 & 7 holds task 4g + (x >> 1) and BOTH towers of its parts
     // (NS = 4: parts 2 (x & 1), 2 (x & 1) + 1; NS = 2: part x & 1), so the critic and actor workgroups of a row part --
     // which read the same observation rows in the same phase, kept in step by the per-step norm hand-off -- share one L2
@@ -176,12 +171,6 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
     const int hs = NS == 4 ? 2 * (x8 & 1) + (j8 >> 1) : NS == 2 ? (x8 & 1) : 0;
     if (p >= a.P) return;
     const int m = NS > 1 ? (j8 & 1) : (bx & 1);
-#else  // block r holds part r >> 3 of tower r & 1 of task 4g + ((r & 7) >> 1): a tower's parts on one XCD
-    const int p = NS > 1 ? 4 * (bx / (8 * NS)) + ((r8 & 7) >> 1) : (bx >> 1);
-    const int hs = NS > 1 ? r8 >> 3 : 0;
-    if (p >= a.P) return;
-    const int m = bx & 1;
-#endif
     const int NQ = m == 0 ? K : A;
     const int N = a.N, T = a.T, B = T * N;
     const int E = a.hp.ppo_epoch, M = a.hp.num_mini_batch;

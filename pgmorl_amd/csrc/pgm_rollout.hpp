@@ -92,23 +92,15 @@ __device__ __forceinline__ V tree_sum(const V (&x)[M]) {
 // (tests/hip/f64_rcp_rsq_probe.hip, profiles/r03d_f64_rcp_rsq_probe.txt): the estimates are good to ~5e-8, one
 // step to <= 2.2e-15 (rcp) / 4.3e-15 (rsq) relative, two steps to <= 1.2 ulp.  Two steps: one step measured no
 // faster (Walker P = 40 iteration 8.036 vs 8.028 ms, profiles/r03e_*), so the chain keeps full fp64 precision.
-// PGM_EXP 43 (A/B): one step.
-#ifndef PGM_EXP
-#define PGM_EXP 0
-#endif
-#define PGM_FP64_NEWTON (PGM_EXP == 43 ? 1 : 2)
 
-// 1 / sqrt(x) in fp64: hardware estimate + PGM_FP64_NEWTON Newton steps (the IEEE sqrt + divide pair is a
-// ~25-instruction dependent chain on the per-step critical path)
+// 1 / sqrt(x) in fp64: hardware estimate + two Newton steps (the IEEE sqrt + divide pair is a ~25-instruction
+// dependent chain on the per-step critical path)
 __device__ __forceinline__ double rsqrt_d(double x) {
     double r = __builtin_amdgcn_rsq(x);
     double e = fma(-x * r, r, 1.0);
     r = fma(r * e, 0.5, r);
-    if constexpr (PGM_FP64_NEWTON > 1) {
-        e = fma(-x * r, r, 1.0);
-        r = fma(r * e, 0.5, r);
-    }
-    return r;
+    e = fma(-x * r, r, 1.0);
+    return fma(r * e, 0.5, r);
 }
 
 // fp64 tanh for the SynthMO dynamics: 1 - 2 / (exp(2|y|) + 1) with the sign restored; exp through
@@ -139,7 +131,7 @@ __device__ __forceinline__ double tanh_d3(double y, const double* t2) {
     const double e = __builtin_ldexp(tj * p, k >> 5) + 1.0;
     double q = __builtin_amdgcn_rcp(e);
     q = fma(q, fma(-e, q, 1.0), q);
-    if constexpr (PGM_FP64_NEWTON > 1) q = fma(q, fma(-e, q, 1.0), q);
+    q = fma(q, fma(-e, q, 1.0), q);
     return copysign(fma(-2.0, q, 1.0), y);
 }
 
@@ -203,10 +195,6 @@ struct RolloutArgs {
     const float* noise;
     uint64_t seed;
     int carry;
-    // split lane rollout only (set by its launcher): the chain -> objective stream of the task (progress words, states,
-    // action-mean rows, done flags) and this launch's epoch (the progress words are never reset)
-    void* scratch = nullptr;
-    unsigned epoch = 0;
 };
 
 struct EvalArgs {

@@ -38,15 +38,6 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 template <int O, int K>
 constexpr bool lanes_fit() { return O <= 48 && O + K + 1 <= 64; }
 
-#ifndef PGM_ROLL_L2_LDS
-#define PGM_ROLL_L2_LDS 0  // 1: layer-2 inputs through the per-wave LDS row (A/B)
-#endif
-#ifndef PGM_EXP
-#define PGM_EXP 0
-#endif
-// Policy forward with both layers' inputs broadcast by DPP from registers (row_copies + row_newbcast) instead of
-// the LDS input row (layer 1) and 64 v_readlane (layer 2).  PGM_EXP 40 (A/B): the LDS / readlane forward.
-#define PGM_ROLL_DPP (PGM_EXP != 40)
 
 template <class F, int... I>
 __device__ __forceinline__ void static_for_impl(F& f, std::integer_sequence<int, I...>) {
@@ -73,19 +64,10 @@ __device__ __forceinline__ void row_copies(float v, float (&V)[NR]) {
         if constexpr (NR > 3) V[3] = __uint_as_float(q1[1]);
     }
 }
-// acc[i % NA] += (lane i of this lane's 16-lane row of v) * w[i], i = 0..NK-1: v_fmac_f32 with a DPP row_newbcast:i
-// source operand (gfx90a+; the compiler's DPP combiner does not fold a row_newbcast mov into fmac).  NA = 4 (the
-// shipped kernels): ONE asm block per row, whose leading s_nop covers the VALU-write -> DPP-read hazard on v (the asm
-// hides the DPP read from the hazard recognizer; inside one block nothing can write v).  Other NA (A/B builds only):
-// one asm statement per lane, each behind its own s_nop.
-template <int I, int NK, int NA>
-__device__ __forceinline__ void fmac_one(float (&acc)[NA], float v, const float (&wv)[16]) {
-    if constexpr (I < NK) {
-        asm("s_nop 1\n\tv_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
-            : "+v"(acc[I % NA]) : "v"(v), "v"(wv[I]), "i"(I));
-        fmac_one<I + 1, NK, NA>(acc, v, wv);
-    }
-}
+// acc[i % 4] += (lane i of this lane's 16-lane row of v) * w[i], i = 0..NK-1: v_fmac_f32 with a DPP row_newbcast:i
+// source operand (gfx90a+; the compiler's DPP combiner does not fold a row_newbcast mov into fmac), ONE asm block per
+// row, whose leading s_nop covers the VALU-write -> DPP-read hazard on v (the asm hides the DPP read from the hazard
+// recognizer; inside one block nothing can write v).  Four accumulator chains.
 #define PGM_FL0 "v_fmac_f32_dpp %0, %4, %5 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
 #define PGM_FL1 "v_fmac_f32_dpp %1, %4, %6 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
 #define PGM_FL2 "v_fmac_f32_dpp %2, %4, %7 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
@@ -151,13 +133,13 @@ __device__ __forceinline__ void fmac_one(float (&acc)[NA], float v, const float 
 #define PGM_FF14 PGM_FF13 PGM_FL13
 #define PGM_FF15 PGM_FF14 PGM_FL14
 #define PGM_FF16 PGM_FF15 PGM_FL15
-template <int NK, int NA, bool FIRST = false>
-__device__ __forceinline__ void fmac_row_bcast(float (&acc)[NA], float v, const float* w) {
+template <int NK, bool FIRST = false>
+__device__ __forceinline__ void fmac_row_bcast(float (&acc)[4], float v, const float* w) {
     static_assert(NK >= 1 && NK <= 16, "1..16 lanes");
     float wv[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) wv[i] = i < NK ? w[i] : 0.f;
-    if constexpr (FIRST && NA == 4 && NK >= 4 && PGM_EXP != 61) {  // (61, A/B: zeroed accumulators, 2.02 vs 1.90 ms)
+    if constexpr (FIRST && NK >= 4) {
         if constexpr (NK == 4) PGM_FMAC_ASM_FIRST(PGM_FF4);
         else if constexpr (NK == 5) PGM_FMAC_ASM_FIRST(PGM_FF5);
         else if constexpr (NK == 6) PGM_FMAC_ASM_FIRST(PGM_FF6);
@@ -173,8 +155,8 @@ __device__ __forceinline__ void fmac_row_bcast(float (&acc)[NA], float v, const 
         else PGM_FMAC_ASM_FIRST(PGM_FF16);
     } else if constexpr (FIRST) {
         acc[1] = acc[2] = acc[3] = 0.f;  // (NK < 4: zeroed, then accumulated)
-        fmac_row_bcast<NK, NA, false>(acc, v, w);
-    } else if constexpr (NA == 4) {
+        fmac_row_bcast<NK, false>(acc, v, w);
+    } else {
         if constexpr (NK == 1) PGM_FMAC_ASM(PGM_FU1);
         else if constexpr (NK == 2) PGM_FMAC_ASM(PGM_FU2);
         else if constexpr (NK == 3) PGM_FMAC_ASM(PGM_FU3);
@@ -191,8 +173,6 @@ __device__ __forceinline__ void fmac_row_bcast(float (&acc)[NA], float v, const 
         else if constexpr (NK == 14) PGM_FMAC_ASM(PGM_FU14);
         else if constexpr (NK == 15) PGM_FMAC_ASM(PGM_FU15);
         else PGM_FMAC_ASM(PGM_FU16);
-    } else {
-        fmac_one<0, NK, NA>(acc, v, wv);
     }
 }
 
@@ -226,58 +206,12 @@ struct ActorLane {
             asm volatile("" : "+v"(rsd[j]));
         }
     }
-    // action mean of the fp32 row x (LDS, read by every lane) -> mu[A], wave-uniform.  h1 is this wave's
-    // [H] LDS exchange row.  Ends with h1 free for reuse.
-    __device__ void forward(const float* x, float* h1, int l, float (&mu)[A]) const {
-        constexpr int OP = opad<O>();
-        float z0 = b1, z1 = 0.f;  // two chains over the inputs
-#pragma unroll
-        for (int k = 0; k < OP; k += 4) {
-            const float4 v = *reinterpret_cast<const float4*>(x + k);
-            z0 = fmaf(v.x, w1[k], z0);
-            if (k + 1 < O) z1 = fmaf(v.y, w1[k + 1], z1);
-            if (k + 2 < O) z0 = fmaf(v.z, w1[k + 2], z0);
-            if (k + 3 < O) z1 = fmaf(v.w, w1[k + 3], z1);
-        }
-        const float hl = tanh_fast(z0 + z1);
-#if PGM_ROLL_L2_LDS
-        h1[l] = hl;
-        wave_lds_fence_r();
-#endif
-        // packed fp32 FMAs over unit pairs (v_pk_fma_f32: two MACs per instruction), two chains of 16; unit k's
-        // activation reaches every lane by v_readlane (no LDS round trip on the chain)
-        f2 a01 = f2{b2, 0.f}, a23 = f2{0.f, 0.f};
-#pragma unroll
-        for (int k = 0; k < H; k += 4) {
-#if PGM_ROLL_L2_LDS
-            const float4 h = *reinterpret_cast<const float4*>(h1 + k);
-#else
-            const int hi = __float_as_int(hl);
-            const float4 h = make_float4(__int_as_float(__builtin_amdgcn_readlane(hi, k)),
-                                         __int_as_float(__builtin_amdgcn_readlane(hi, k + 1)),
-                                         __int_as_float(__builtin_amdgcn_readlane(hi, k + 2)),
-                                         __int_as_float(__builtin_amdgcn_readlane(hi, k + 3)));
-#endif
-            a01 = __builtin_elementwise_fma(f2{h.x, h.y}, f2{w2[k], w2[k + 1]}, a01);
-            a23 = __builtin_elementwise_fma(f2{h.z, h.w}, f2{w2[k + 2], w2[k + 3]}, a23);
-        }
-        const float h2 = tanh_fast((a01.x + a01.y) + (a23.x + a23.y));
-        float pr[A];
-#pragma unroll
-        for (int j = 0; j < A; ++j) pr[j] = h2 * wm[j];
-        wave_sum64_multi<A>(pr, mu);
-#pragma unroll
-        for (int j = 0; j < A; ++j) mu[j] += bm[j];
-#if PGM_ROLL_L2_LDS
-        wave_lds_fence_r();  // every lane's h1 reads done before the row is rewritten
-#endif
-    }
-    // the same action mean from registers: lane k < O holds input feature k (other lanes: anything).  Every input
-    // reaches every lane by a row copy + row_newbcast DPP operand of the FMA (no LDS round trip, no v_readlane);
-    // four accumulator chains per layer.
+    // action mean of this lane's input: lane k < O holds input feature k (other lanes: anything), -> mu[A],
+    // wave-uniform.  Every input reaches every lane by a row copy + row_newbcast
+    // DPP operand of the FMA (no LDS round trip, no v_readlane); four accumulator chains per layer.  (Measured and
+    // dropped: the LDS input row with 64 v_readlane for layer 2, and layer-2 inputs by an LDS row into packed FMAs.)
     // murow (optional): the head sums' two reduced rows for another wave (wave_sum64_multi rows)
-    __device__ void forward_reg(float xv, int l, float (&mu)[A], float* h1row = nullptr, float* murow = nullptr,
-                                float* mugrow = nullptr) const {
+    __device__ void forward_reg(float xv, float (&mu)[A], float* murow = nullptr) const {
         constexpr int R1 = (O + 15) / 16;
         float X[R1];
         row_copies<R1>(xv, X);
@@ -285,55 +219,21 @@ struct ActorLane {
         z[0] = b1;
         static_for<R1>([&](auto jc) {
             constexpr int j = decltype(jc)::value;
-            fmac_row_bcast<(O - 16 * j < 16 ? O - 16 * j : 16), 4, j == 0>(z, X[j], &w1[16 * j]);
+            fmac_row_bcast<(O - 16 * j < 16 ? O - 16 * j : 16), j == 0>(z, X[j], &w1[16 * j]);
         });
         const float hl = tanh_fast((z[0] + z[1]) + (z[2] + z[3]));
-        float h2;
-        if constexpr (PGM_EXP == 44 || PGM_EXP == 45) {
-            // A/B: layer-2 inputs by an LDS row broadcast (44) or v_readlane (45) into packed FMAs
-            f2 a01 = f2{b2, 0.f}, a23 = f2{0.f, 0.f};
-            if constexpr (PGM_EXP == 44) {
-                h1row[l] = hl;
-                wave_lds_fence_r();
-            }
+        float Hc[4];
+        row_copies<4>(hl, Hc);
+        float y[4];
+        y[0] = b2;
+        fmac_row_bcast<16, true>(y, Hc[0], &w2[0]);
 #pragma unroll
-            for (int k = 0; k < H; k += 4) {
-                float4 h;
-                if constexpr (PGM_EXP == 44) {
-                    h = *reinterpret_cast<const float4*>(h1row + k);
-                } else {
-                    const int hi = __float_as_int(hl);
-                    h = make_float4(__int_as_float(__builtin_amdgcn_readlane(hi, k)),
-                                    __int_as_float(__builtin_amdgcn_readlane(hi, k + 1)),
-                                    __int_as_float(__builtin_amdgcn_readlane(hi, k + 2)),
-                                    __int_as_float(__builtin_amdgcn_readlane(hi, k + 3)));
-                }
-                a01 = __builtin_elementwise_fma(f2{h.x, h.y}, f2{w2[k], w2[k + 1]}, a01);
-                a23 = __builtin_elementwise_fma(f2{h.z, h.w}, f2{w2[k + 2], w2[k + 3]}, a23);
-            }
-            if constexpr (PGM_EXP == 44) wave_lds_fence_r();
-            h2 = tanh_fast((a01.x + a01.y) + (a23.x + a23.y));
-        } else {
-            float Hc[4];
-            row_copies<4>(hl, Hc);
-            constexpr int NA2 = PGM_EXP == 41 ? 8 : 4;  // layer-2 accumulator chains (A/B)
-            float y[NA2];
-            y[0] = b2;
-            if constexpr (NA2 != 4) {
-#pragma unroll
-                for (int i = 1; i < NA2; ++i) y[i] = 0.f;
-            }
-            fmac_row_bcast<16, NA2, NA2 == 4>(y, Hc[0], &w2[0]);
-#pragma unroll
-            for (int j = 1; j < 4; ++j) fmac_row_bcast<16, NA2>(y, Hc[j], &w2[16 * j]);
-#pragma unroll
-            for (int i = 4; i < NA2; ++i) y[i - 4] += y[i];
-            h2 = tanh_fast((y[0] + y[1]) + (y[2] + y[3]));
-        }
+        for (int j = 1; j < 4; ++j) fmac_row_bcast<16>(y, Hc[j], &w2[16 * j]);
+        const float h2 = tanh_fast((y[0] + y[1]) + (y[2] + y[3]));
         float pr[A];
 #pragma unroll
         for (int j = 0; j < A; ++j) pr[j] = h2 * wm[j];
-        wave_sum64_multi<A>(pr, mu, murow, mugrow);
+        wave_sum64_multi<A>(pr, mu, murow);
 #pragma unroll
         for (int j = 0; j < A; ++j) mu[j] += bm[j];
     }
@@ -405,20 +305,15 @@ struct EnvLane {
 
 // ------------------------------------------------------------------------------------------ rollout
 constexpr int NCH = 32;  // rollout steps per staged noise chunk
-// The step's action side off the chain (default): the chain waves draw the action and step the dynamics only; the
-// objective waves redo the draw from the head sums' rows (same fp32 operations, so the same action), and own the
-// log-prob, |clip(a)|^2, the action / log-prob / mask stores.  A single wave issues at most one VALU instruction per
-// ~4 cycles, and the chain wave is the one whose instruction count sets the step time (two waves per SIMD).
-// PGM_EXP 48 (A/B): everything on the chain waves.
-#define PGM_ROLL_OBJ_SIDE (PGM_EXP != 48)
+// The step's action side is off the chain: the chain waves draw the action and step the dynamics only; the objective
+// waves redo the draw from the head sums' rows (same fp32 operations, so the same action), and own the log-prob,
+// |clip(a)|^2, the action / log-prob / mask stores.  A single wave issues at most one VALU instruction per ~4 cycles,
+// and the chain wave is the one whose instruction count sets the step time (two waves per SIMD).
 
 template <int O, int A, int NN>
 struct LaneSmem {
-    alignas(16) float x[NN][opad<O>()];  // normalised fp32 obs row of env n (written / read by its wave)
-    alignas(16) float h1[4][H];          // per-wave layer-1 exchange row
     double sr[2][NN][64];                // statistics rows, double-buffered by step parity
     double sn[2][NN][64];                // pre-reset next state of env n (feature lanes), by step parity
-    double e2[2][NN];                    // |clip(a)|^2 of env n, by step parity
     int dn[2][NN];                       // done of env n, by step parity
     double t2[32];                       // 2^(j/32): tanh_d3's exp table
     double rinv[2][64];                  // the chain's merged 1 / sqrt(var + eps) per statistic lane, by step parity
@@ -435,12 +330,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t out_rsrc(const void* base, siz
 __device__ __forceinline__ void store_lane(__amdgpu_buffer_rsrc_t r, uint32_t off, float v) {
     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (int)off, 0, 0);
 }
-// SPLIT scratch layout (bytes): the P progress words (256-B aligned), then states, mean rows, done flags
-__host__ __device__ inline size_t split_hdr_bytes(int P) { return ((size_t)P * 8 + 255) / 256 * 256; }
-__host__ __device__ inline size_t split_scratch_bytes(int P, int T, int N, int O) {
-    return split_hdr_bytes(P) + (size_t)P * T * N * (O * 8 + 32 + 4);
-}
-
 // clip as two bare v_max_f64 / v_min_f64 that the scheduler may move (clipd_hw is a volatile asm barrier)
 __device__ __forceinline__ double clipd_s(double x, double lo, double hi) {
     double r;
@@ -461,32 +350,20 @@ __device__ __forceinline__ double clipd_s(double x, double lo, double hi) {
 //    reciprocal std goes to LDS, and step t's reward leaves after barrier t + 2.
 // Both roles execute the same barriers (one per step plus two drain barriers).
 //
-// SPLIT: the two roles in two workgroups per task (blocks p and P + p), so the chain waves have their SIMDs to
-// themselves (objective waves idle measured 1.95 -> 1.81 ms per Walker P = 40 rollout).  The objective side only needs
-// the chain's per-step states (pre-reset, fp64), action-mean rows and done flags: the chain workgroup streams them to the
-// scratch with sc1 stores and publishes its progress every NCH / 2 steps (every storing wave's vmcnt(0), a workgroup
-// barrier, one relaxed agent store of epoch << 32 | steps); the objective workgroup polls it, loads with sc1 (the
-// validated hand-off: MI355X_MICROARCH.md, first row of the sc1 table), redoes the action side, and runs the obj_rms /
-// ret_rms merge itself right after each step (its rewards no longer wait for the chain's barriers).
-template <int O, int A, int K, int NN, bool SPLIT>
-__global__ __launch_bounds__(SPLIT ? 256 : 512) void rollout_lane_kernel(RolloutArgs a) {
+// (Measured and dropped: the two roles in two workgroups per task, the chain streaming its states, action-mean rows and
+// done flags to a scratch with sc1 stores and publishing every 16 steps -- 2.31 vs 1.91 ms per Walker P = 40 rollout:
+// every publish drains the chain's sc1 stores and each chunk's loads pay a memory round trip.)
+template <int O, int A, int K, int NN>
+__global__ __launch_bounds__(512) void rollout_lane_kernel(RolloutArgs a) {
     static_assert(lanes_fit<O, K>(), "lane roles need O + K + 1 <= 64");
     constexpr int NW = NN < 4 ? NN : 4;  // waves per role
     constexpr int NE = (NN + 3) / 4;     // env slots per wave
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     auto& S = *reinterpret_cast<LaneSmem<O, A, NN>*>(smem_raw);
-    const int p = SPLIT ? (int)blockIdx.x % a.P : (int)blockIdx.x, l = threadIdx.x & 63;
+    const int p = (int)blockIdx.x, l = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const bool chain = SPLIT ? (int)blockIdx.x < a.P : wv < NW;
-    const int w = SPLIT ? wv : chain ? wv : wv - NW;  // env slot base of this wave
-    // SPLIT scratch of task p: progress word, pre-reset states [T][NN][O], action-mean rows [T][NN][8], done flags [T][NN]
-    unsigned long long* const prog = reinterpret_cast<unsigned long long*>(a.scratch) + p;
-    double* const snb = reinterpret_cast<double*>(reinterpret_cast<char*>(a.scratch) + split_hdr_bytes(a.P)) +
-                        (size_t)p * a.T * NN * O;
-    float* const mub = reinterpret_cast<float*>(reinterpret_cast<char*>(a.scratch) + split_hdr_bytes(a.P) +
-                                                (size_t)a.P * a.T * NN * O * 8) + (size_t)p * a.T * NN * 8;
-    int* const dnbuf = reinterpret_cast<int*>(reinterpret_cast<char*>(a.scratch) + split_hdr_bytes(a.P) +
-                                              (size_t)a.P * a.T * NN * (O * 8 + 32)) + (size_t)p * a.T * NN;
+    const bool chain = wv < NW;
+    const int w = chain ? wv : wv - NW;  // env slot base of this wave
     const int T = a.T;
     const NormCfg nc = norm_cfg(a.ns);
     const Layout& L = a.L;
@@ -553,8 +430,7 @@ __global__ __launch_bounds__(SPLIT ? 256 : 512) void rollout_lane_kernel(Rollout
             mean = mean + delta * (double)NN * itot;
             var = (var * cnt + (sq * rn) * (double)NN + delta * delta * cnt * (double)NN * itot) * itot;
             cnt += (double)NN;
-            // PGM_EXP 62 (A/B): two Newton steps (2.02 vs 1.90 ms per Walker P = 40 rollout)
-            inv = PGM_EXP == 62 ? rsqrt_d(var + nc.eps) : rsqrt_1(var + nc.eps);
+            inv = rsqrt_1(var + nc.eps);  // (two Newton steps measured 2.02 vs 1.90 ms per Walker P = 40 rollout)
         }
     };
     if (threadIdx.x < 32) S.t2[threadIdx.x] = exp2((double)threadIdx.x / 32.0);
@@ -563,18 +439,11 @@ __global__ __launch_bounds__(SPLIT ? 256 : 512) void rollout_lane_kernel(Rollout
 
     if (chain) {
         // =========================================================== chain waves
-        // issue priority over the objective waves that share their SIMDs (those only fill the chain's stalls).
-        // PGM_EXP 42 (A/B): equal priority
-        if constexpr (PGM_EXP != 42) __builtin_amdgcn_s_setprio(3);
+        // issue priority over the objective waves that share their SIMDs (those only fill the chain's stalls)
+        __builtin_amdgcn_s_setprio(3);
         const float* prm = a.params + (size_t)p * L.total;
-        float* act = a.rb.actions + (size_t)p * T * NN * A;
-        float* logp = a.rb.logp + (size_t)p * T * NN;
         const int maxs = a.spec.max_episode_steps;
         const auto r_obs = out_rsrc(obs, (size_t)(T + 1) * NN * O * 4);
-        const auto r_act = out_rsrc(act, (size_t)T * NN * A * 4);
-        const auto r_logp = out_rsrc(logp, (size_t)T * NN * 4);
-        const auto r_msk = out_rsrc(masks, (size_t)(T + 1) * NN * 4);
-        const auto r_bad = out_rsrc(bad, (size_t)(T + 1) * NN * 4);
         ActorLane<O, A> pol;
         pol.load(prm, L, l);
         // per-lane SynthMO constants of feature l (the dynamics; the objective constants live in the
@@ -604,7 +473,7 @@ __global__ __launch_bounds__(SPLIT ? 256 : 512) void rollout_lane_kernel(Rollout
         }
 
         // ---- slot 0: after_update() carry (storage.py:71-75) and the first policy input
-        float xr[NE];  // PGM_ROLL_DPP: normalised input feature l of env slot e (lanes < O), else S.x
+        float xr[NE];  // normalised input feature l of env slot e (lanes < O)
 #pragma unroll
         for (int e = 0; e < NE; ++e) {
             xr[e] = 0.f;
@@ -613,8 +482,7 @@ __global__ __launch_bounds__(SPLIT ? 256 : 512) void rollout_lane_kernel(Rollout
             if (fl) {
                 float v = obs[(size_t)(a.carry ? T : 0) * NN * O + n * O + l];
                 if (a.carry) obs[n * O + l] = v;
-                if (PGM_ROLL_DPP) xr[e] = v;
-                else S.x[n][l] = v;
+                xr[e] = v;
             }
             if (a.carry && l == 0) {
                 masks[n] = masks[(size_t)T * NN + n];
@@ -683,7 +551,7 @@ __global__ __launch_bounds__(SPLIT ? 256 : 512) void rollout_lane_kernel(Rollout
             }
             // 1 / (count + N) of this step's merge: the counts are known since the last merge, and formed here its
             // fp64 reciprocal and Newton steps interleave with the forward instead of stalling before the barrier
-            if constexpr (PGM_EXP != 63) prep_merge();
+            prep_merge();
             float ejc[A];  // PREF: this step's noise of env slot 0 (from ejn); the next step's goes into ejn
             if constexpr (PREF) {
                 const int n = min(w, NN - 1), s1 = step + 1 < T ? step + 1 : step;
@@ -702,45 +570,18 @@ __global__ __launch_bounds__(SPLIT ? 256 : 512) void rollout_lane_kernel(Rollout
 #pragma unroll
                 for (int j = 0; j < A; ++j) ej[j] = PREF ? ejc[j] : S.eps[(step / NCH) & 1][n][cs * A + j];
                 float mu[A];
-                if constexpr (PGM_EXP == 51) {  // timing ablation only (wrong results): no policy forward
-#pragma unroll
-                    for (int j = 0; j < A; ++j) mu[j] = xr[e] * 1e-3f;
-                } else if constexpr (PGM_ROLL_DPP) {
-                    if constexpr (SPLIT) pol.forward_reg(xr[e], l, mu, S.h1[w], nullptr, mub + ((size_t)step * NN + n) * 8);
-                    else pol.forward_reg(xr[e], l, mu, S.h1[w], PGM_ROLL_OBJ_SIDE ? &S.mur[buf][n][0] : nullptr);
-                }
-                else pol.forward(S.x[n], S.h1[w], l, mu);
+                pol.forward_reg(xr[e], mu, &S.mur[buf][n][0]);
                 PGM_STAMP(1);
                 // Gaussian draw (torch.normal(mean, std) = eps * std + mean) and clipped action, wave-uniform
-                // (PGM_EXP 48: also the log-prob and |clip(a)|^2 here; lanes 0..A-1 store the action row, lane 0 its
-                // log-prob)
-                float lpt[A], avs[A];
-                double ac[A], sq[A], pu[A];
+                double ac[A], pu[A];
 #pragma unroll
                 for (int j = 0; j < A; ++j) {
                     const float av = fmaf(ej[j], pol.sd[j], mu[j]);
                     ac[j] = clipd_s((double)av, alo[j], ahi[j]);
                     pu[j] = U[j] * ac[j];
-                    if constexpr (!PGM_ROLL_OBJ_SIDE) {
-                        const float dz = (av - mu[j]) * pol.rsd[j];
-                        lpt[j] = -0.5f * dz * dz - pol.ls[j] - LOG_SQRT_2PI;
-                        avs[j] = av;
-                        sq[j] = ac[j] * ac[j];
-                    }
-                }
-                double e2v = 0.0;
-                if constexpr (!PGM_ROLL_OBJ_SIDE) {  // |clip(a)|^2 for the objective side
-                    e2v = tree_sum(sq);
-                    asm volatile("" : "+v"(e2v));
                 }
                 // dynamics (fp64, lane = feature): s' = tanh(d s + U clip(a) + c)
-                const double sn = PGM_EXP == 53 ? dd * s_o[e] + tree_sum(pu) + cc  // (53: timing ablation, no tanh)
-                                                : tanh_d3(dd * s_o[e] + tree_sum(pu) + cc, S.t2);
-                if constexpr (!PGM_ROLL_OBJ_SIDE) {
-                    const float lp = tree_sum(lpt);
-                    store_lane(r_act, l < A ? (uint32_t)(((size_t)step * NN + n) * A + l) * 4 : OOB_OFF, sel_lane(avs, l));
-                    store_lane(r_logp, l == 0 ? (uint32_t)((size_t)step * NN + n) * 4 : OOB_OFF, lp);
-                }
+                const double sn = tanh_d3(dd * s_o[e] + tree_sum(pu) + cc, S.t2);
                 PGM_STAMP(6);
                 // time limit, auto-reset; the objective side's inputs (s', |a|^2, done) to the parity rows
                 const int el = elapsed[e] + 1;
@@ -749,37 +590,16 @@ __global__ __launch_bounds__(SPLIT ? 256 : 512) void rollout_lane_kernel(Rollout
                 elapsed[e] = dn ? 0 : el;
                 s_o[e] = dn ? s0_o[e] : sn;
                 if (role == 0) S.sr[buf][n][l] = s_o[e];  // lanes O.. of the row belong to the objective waves
-                if constexpr (SPLIT) {  // to the objective workgroup (sc1 stores, published below)
-                    if (fl) __hip_atomic_store(snb + ((size_t)step * NN + n) * O + l, sn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (l == 0) __hip_atomic_store(dnbuf + (size_t)step * NN + n, dn | bf << 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                } else {
-                    S.sn[buf][n][l] = sn;
-                    if (l == 0) {
-                        if constexpr (!PGM_ROLL_OBJ_SIDE) S.e2[buf][n] = e2v;
-                        S.dn[buf][n] = dn | bf << 1;
-                    }
-                }
-                if constexpr (!PGM_ROLL_OBJ_SIDE) {
-                    const uint32_t moff = (uint32_t)((size_t)(step + 1) * NN + n) * 4;
-                    store_lane(r_msk, l == 0 ? moff : OOB_OFF, dn ? 0.f : 1.f);
-                    store_lane(r_bad, l == 0 ? moff : OOB_OFF, bf ? 0.f : 1.f);
-                }
+                S.sn[buf][n][l] = sn;
+                if (l == 0) S.dn[buf][n] = dn | bf << 1;
                 if (e == 0) PGM_STAMP(2);
             }
-            if constexpr (PGM_EXP == 63) prep_merge();  // (63, A/B: formed just before the barrier)
-            // SPLIT: publish steps [0, step] to the objective workgroup every NCH / 2 steps (not at the chunk ends, where the
-            // next noise chunk's loads were just issued: vmcnt(0) would wait for them) and after the last step
-            const bool publish = SPLIT && (step % NCH == NCH / 2 - 1 || step == T - 1);
-            if (publish) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             lds_sync();
-            if (publish && w == 0 && l == 0)
-                __hip_atomic_store(prog, ((unsigned long long)a.epoch << 32) | (unsigned)(step + 1), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
             PGM_STAMP(3);
             // every statistic of the row: ob_rms (lanes < O, this step's states) and, for the objective waves, obj_rms /
             // ret_rms (their accumulators of the previous step; nothing in step 0's row).  The chain waves execute all
             // 64 lanes of the merge anyway; the objective waves read the reciprocal std from S.rinv a barrier later.
-            if constexpr (PGM_EXP != 52) merge(buf, SPLIT ? role == 0 : role == 0 || step > 0);  // (52: ablation, no merge)
+            merge(buf, role == 0 || step > 0);
             PGM_STAMP(4);
             // ---- normalised fp32 obs: the next input and the rollout buffer
 #pragma unroll
@@ -789,22 +609,18 @@ __global__ __launch_bounds__(SPLIT ? 256 : 512) void rollout_lane_kernel(Rollout
                 double v = s_o[e];
                 if (nc.use_ob) v = clipd_s((v - mean) * inv, -nc.clipob, nc.clipob);
                 const float f = (float)v;  // VecPyTorch .float() (envs.py:192)
-                if constexpr (PGM_ROLL_DPP) xr[e] = f;
-                else if (role == 0) S.x[n][l] = f;
+                xr[e] = f;
                 store_lane(r_obs, role == 0 ? (uint32_t)(((size_t)(step + 1) * NN + n) * O + l) * 4 : OOB_OFF, f);
             }
-            if constexpr (!PGM_ROLL_DPP) wave_lds_fence_r();
-            if (!SPLIT && w == 0) S.rinv[buf][l] = inv;  // read after the next barrier (off this wave's chain)
+            if (w == 0) S.rinv[buf][l] = inv;  // read after the next barrier (off this wave's chain)
             PGM_STAMP(5);
         }
         // drain: the last step's objective / ret accumulators (row T & 1), then one more barrier for their reward
-        if constexpr (!SPLIT) {
-            prep_merge();  // (the counts after step T - 1's merge)
-            lds_sync();
-            merge(T & 1, role == 1 || role == 2);
-            if (w == 0) S.rinv[T & 1][l] = inv;
-            lds_sync();
-        }
+        prep_merge();  // (the counts after step T - 1's merge)
+        lds_sync();
+        merge(T & 1, role == 1 || role == 2);
+        if (w == 0) S.rinv[T & 1][l] = inv;
+        lds_sync();
         // ---- env state and observation statistics back to HBM
 #pragma unroll
         for (int e = 0; e < NE; ++e) {
@@ -818,190 +634,7 @@ __global__ __launch_bounds__(SPLIT ? 256 : 512) void rollout_lane_kernel(Rollout
                 a.ns.ob_mean[(size_t)p * O + l] = mean;
                 a.ns.ob_var[(size_t)p * O + l] = var;
                 if (l == 0) a.ns.ob_count[p] = cnt;
-            } else if (role == 1 && !SPLIT) {
-                a.ns.obj_mean[p * K + ko] = mean;
-                a.ns.obj_var[p * K + ko] = var;
-                if (ko == 0) a.ns.obj_count[p] = cnt;
-            } else if (role == 2 && !SPLIT) {
-                a.ns.ret_mean[p] = mean;
-                a.ns.ret_var[p] = var;
-                a.ns.ret_count[p] = cnt;
-            }
-        }
-    } else if constexpr (SPLIT) {
-        // =========================================================== objective workgroup (SPLIT)
-        float* rew = a.rb.rewards + (size_t)p * T * NN * K;
-        const auto r_rew = out_rsrc(rew, (size_t)T * NN * K * 4);
-        const auto r_act = out_rsrc(a.rb.actions + (size_t)p * T * NN * A, (size_t)T * NN * A * 4);
-        const auto r_logp = out_rsrc(a.rb.logp + (size_t)p * T * NN, (size_t)T * NN * 4);
-        const auto r_msk = out_rsrc(masks, (size_t)(T + 1) * NN * 4);
-        const auto r_bad = out_rsrc(bad, (size_t)(T + 1) * NN * 4);
-        double V[K], ebase[K], ecoef[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            V[k] = fl ? a.spec.V[k * O + lo] : 0.0;
-            ebase[k] = a.spec.ebase[k];
-            ecoef[k] = a.spec.ecoef[k];
-            asm volatile("" : "+v"(ebase[k]), "+v"(ecoef[k]));
-        }
-        float bm[A], ls[A], sd[A], rsd[A];
-        double alo[A], ahi[A];
-        {
-            const float* prm = a.params + (size_t)p * L.total;
-#pragma unroll
-            for (int j = 0; j < A; ++j) {
-                bm[j] = prm[L.off[PGM_P_MEAN_B] + j];
-                ls[j] = prm[L.off[PGM_P_LOGSTD] + j];
-                sd[j] = expf(ls[j]);
-                rsd[j] = 1.0f / sd[j];
-                alo[j] = a.spec.act_lo[j];
-                ahi[j] = a.spec.act_hi[j];
-                asm volatile("" : "+v"(bm[j]), "+v"(ls[j]), "+v"(sd[j]), "+v"(rsd[j]));
-                asm volatile("" : "+v"(alo[j]), "+v"(ahi[j]));
-            }
-        }
-        double objacc[NE][K], ret[NE], objraw[NE][K];
-        int dprev[NE];
-#pragma unroll
-        for (int e = 0; e < NE; ++e) {
-            const int n = min(w + 4 * e, NN - 1);
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                objacc[e][k] = a.st.obj_acc[((size_t)p * NN + n) * K + k];
-                objraw[e][k] = 0.0;
-            }
-            ret[e] = a.st.ret[p * NN + n];
-            dprev[e] = 0;
-        }
-        int obj_valid = a.st.obj_acc_valid[p];
-        double clip_lo = -nc.cliprew, clip_hi = nc.cliprew, gam = nc.gamma;
-        asm volatile("" : "+v"(clip_lo), "+v"(clip_hi), "+v"(gam));
-        const bool scale_out = nc.use_obj != 0;
-        const unsigned long long base = (unsigned long long)a.epoch << 32;
-        unsigned long long avail = 0;  // steps [0, avail) of this launch published by the chain workgroup
-        // steps in chunks of CHK: once the chain has published a chunk, every load of it is issued at once into registers
-        // (one load latency per chunk, not per step; the chain publishes every NCH / 2 steps)
-        constexpr int CHK = NE == 1 ? 8 : 4;
-        constexpr int pos[4] = {0, 2, 1, 3};
-        for (int c0 = 0; c0 < T; c0 += CHK) {
-            const int cend = min(c0 + CHK, T);
-            if (avail < (unsigned long long)cend) {  // wave-uniform: this wave polls, then loads what the poll covers
-                for (unsigned spins = 0;; ++spins) {
-                    const unsigned long long x = __hip_atomic_load(prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (x >= base + (unsigned long long)cend) {
-                        avail = x - base;
-                        break;
-                    }
-                    if (spins > (1u << 24)) {  // bounded (the grid is checked co-resident): garbage, never a hang
-                        avail = (unsigned long long)T;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(2);
-                }
-            }
-            double psn[CHK][NE];
-            int pdn[CHK][NE];
-            float pmr[CHK][NE][A], pej[CHK][NE][A];
-#pragma unroll
-            for (int i = 0; i < CHK; ++i) {
-                const int st = min(c0 + i, T - 1);
-#pragma unroll
-                for (int e = 0; e < NE; ++e) {
-                    const int n = min(w + 4 * e, NN - 1);
-                    const size_t sn_i = (size_t)st * NN + n;
-                    psn[i][e] = __hip_atomic_load(snb + sn_i * O + lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    pdn[i][e] = __hip_atomic_load(dnbuf + sn_i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-                    for (int j = 0; j < A; ++j) {
-                        pmr[i][e][j] = __hip_atomic_load(mub + sn_i * 8 + (j >> 2) * 4 + pos[j & 3], __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT);
-                        const size_t ei = sn_i * A + j;
-                        pej[i][e][j] = a.noise ? a.noise[ei] : counter_normal(a.seed, ei);
-                    }
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < CHK; ++i) {
-                const int step = c0 + i;
-                if (step >= T) break;
-                const int buf = step & 1;
-                prep_merge();
-#pragma unroll
-                for (int e = 0; e < NE; ++e) {
-                    const int n = w + 4 * e;
-                    if (n >= NN) break;
-                    const size_t sn_i = (size_t)step * NN + n;
-                    const double sn = fl ? psn[i][e] : 0.0;
-                    const int dnb = pdn[i][e];
-                    // the chain's Gaussian draw again (same fp32 operations on the same mean and noise), the log-prob,
-                    // |clip(a)|^2 and the action / log-prob / mask stores of step `step`
-                    float lpt[A], avs[A];
-                    double sq[A];
-#pragma unroll
-                    for (int j = 0; j < A; ++j) {
-                        const float muj = pmr[i][e][j] + bm[j];
-                        const float av = fmaf(pej[i][e][j], sd[j], muj);
-                        const float dz = (av - muj) * rsd[j];
-                        lpt[j] = -0.5f * dz * dz - ls[j] - LOG_SQRT_2PI;
-                        avs[j] = av;
-                        const double ac = clipd_s((double)av, alo[j], ahi[j]);
-                        sq[j] = ac * ac;
-                    }
-                    const double e2 = tree_sum(sq);
-                    const float lp = tree_sum(lpt);
-                    store_lane(r_act, l < A ? (uint32_t)(sn_i * A + l) * 4 : OOB_OFF, sel_lane(avs, l));
-                    store_lane(r_logp, l == 0 ? (uint32_t)sn_i * 4 : OOB_OFF, lp);
-                    const uint32_t moff = (uint32_t)((size_t)(step + 1) * NN + n) * 4;
-                    store_lane(r_msk, l == 0 ? moff : OOB_OFF, (dnb & 1) ? 0.f : 1.f);
-                    store_lane(r_bad, l == 0 ? moff : OOB_OFF, (dnb & 2) ? 0.f : 1.f);
-                    // objective side: reset by done_{t-1}, raw objectives (wave sums), discounted accumulators
-                    if (dprev[e]) {
-#pragma unroll
-                        for (int k = 0; k < K; ++k) objacc[e][k] = 0.0;
-                        ret[e] = 0.0;
-                    }
-                    dprev[e] = dnb & 1;
-                    double ob[K];
-#pragma unroll
-                    for (int k = 0; k < K; ++k) ob[k] = V[k] * sn;
-                    wave_sum64_d_multi<K>(ob, ob);
-#pragma unroll
-                    for (int k = 0; k < K; ++k) {
-                        ob[k] += ebase[k] - ecoef[k] * e2;
-                        objraw[e][k] = ob[k];
-                        objacc[e][k] = obj_valid ? objacc[e][k] * gam + ob[k] : ob[k];
-                    }
-                    ret[e] = ret[e] * gam + 0.0;  // SynthMO's scalar reward is 0 (vec_normalize.py:32)
-                    const double rv = role == 1 ? sel_lane_d(objacc[e], ko) : role == 2 ? ret[e] : 0.0;
-                    if (role == 1 || role == 2) S.sr[buf][n][l] = rv;
-                }
-                obj_valid = 1;
-                lds_sync();  // every env's accumulators of this step
-                merge(buf, role == 1 || role == 2);
-#pragma unroll
-                for (int e = 0; e < NE; ++e) {
-                    const int n = w + 4 * e;
-                    if (n >= NN) break;
-                    double r = sel_lane_d(objraw[e], ko);
-                    if (scale_out) r = clipd_s(r * inv, clip_lo, clip_hi);
-                    store_lane(r_rew, role == 1 ? (uint32_t)((((size_t)step * NN + n) * K + ko) * 4) : OOB_OFF, (float)r);
-                }
-            }
-        }
-#pragma unroll
-        for (int e = 0; e < NE; ++e) {
-            const int n = w + 4 * e;
-            if (n >= NN) break;
-            if (dprev[e]) {
-#pragma unroll
-                for (int k = 0; k < K; ++k) objacc[e][k] = 0.0;
-                ret[e] = 0.0;
-            }
-            if (l < K) a.st.obj_acc[((size_t)p * NN + n) * K + l] = sel_lane_d(objacc[e], l);
-            if (l == 0) a.st.ret[p * NN + n] = ret[e];
-        }
-        if (w == 0) {
-            if (role == 1) {
+            } else if (role == 1) {
                 a.ns.obj_mean[p * K + ko] = mean;
                 a.ns.obj_var[p * K + ko] = var;
                 if (ko == 0) a.ns.obj_count[p] = cnt;
@@ -1010,7 +643,6 @@ __global__ __launch_bounds__(SPLIT ? 256 : 512) void rollout_lane_kernel(Rollout
                 a.ns.ret_var[p] = var;
                 a.ns.ret_count[p] = cnt;
             }
-            if (l == 0) a.st.obj_acc_valid[p] = obj_valid;
         }
     } else {
         // =========================================================== objective waves
@@ -1020,7 +652,7 @@ __global__ __launch_bounds__(SPLIT ? 256 : 512) void rollout_lane_kernel(Rollout
         const auto r_logp = out_rsrc(a.rb.logp + (size_t)p * T * NN, (size_t)T * NN * 4);
         const auto r_msk = out_rsrc(masks, (size_t)(T + 1) * NN * 4);
         const auto r_bad = out_rsrc(bad, (size_t)(T + 1) * NN * 4);
-        // the action side (PGM_ROLL_OBJ_SIDE): the policy's per-action constants as the chain's ActorLane holds them
+        // the action side: the policy's per-action constants as the chain's ActorLane holds them
         float bm[A], ls[A], sd[A], rsd[A];
         double alo[A], ahi[A];
         {
@@ -1079,7 +711,6 @@ __global__ __launch_bounds__(SPLIT ? 256 : 512) void rollout_lane_kernel(Rollout
         for (int step = 0; step < T; ++step) {
             const int buf = step & 1;
             lds_sync();
-            if constexpr (PGM_EXP == 50) continue;  // timing ablation only (wrong results): objective waves idle
             const double rinv = S.rinv[buf ^ 1][l];  // the chain's merge after barrier step - 1
 #pragma unroll
             for (int e = 0; e < NE; ++e) {
@@ -1098,7 +729,7 @@ __global__ __launch_bounds__(SPLIT ? 256 : 512) void rollout_lane_kernel(Rollout
                 const double sn = S.sn[buf][n][l];
                 const int dnb = S.dn[buf][n];
                 double e2;
-                if constexpr (PGM_ROLL_OBJ_SIDE) {
+                {
                     // the chain's Gaussian draw again (same fp32 operations on the same mean and noise), the log-prob,
                     // |clip(a)|^2 and the action / log-prob / mask stores of step `step`
                     constexpr int lane_of[4] = {0, 32, 16, 48};
@@ -1122,8 +753,6 @@ __global__ __launch_bounds__(SPLIT ? 256 : 512) void rollout_lane_kernel(Rollout
                     const uint32_t moff = (uint32_t)((size_t)(step + 1) * NN + n) * 4;
                     store_lane(r_msk, l == 0 ? moff : OOB_OFF, (dnb & 1) ? 0.f : 1.f);
                     store_lane(r_bad, l == 0 ? moff : OOB_OFF, (dnb & 2) ? 0.f : 1.f);
-                } else {
-                    e2 = S.e2[buf][n];
                 }
                 dprev[e] = dnb & 1;
                 double ob[K];
@@ -1259,7 +888,7 @@ __global__ __launch_bounds__(256) void value_kernel(ValueArgs a) {
 // in the update kernel's forward), the next tile's observation rows prefetched into registers during the current
 // one.  Layer 1 from a per-wave LDS copy of the tile's rows, layer 2 through a [32][65] transpose tile, the K value
 // outputs on the VALU (lane = sample, half h = units 32h..32h+31).  fp32 and tanh_fast as value_kernel, a different
-// summation order.  PGM_EXP 46 (A/B): value_kernel.
+// summation order (81 vs 84 us per Walker P = 40 launch against value_kernel, which Humanoid keeps).
 template <int O, int K>
 struct CriticMSmem {
     static constexpr int XS = O | 1;  // odd row stride: the tile's column reads are conflict-free
@@ -1371,8 +1000,6 @@ __global__ __launch_bounds__(256) void value_mfma_kernel(ValueArgs a) {
 // ------------------------------------------------------------------------------------------ evaluation
 template <int O>
 struct EvalSmem {
-    alignas(16) float x[8][opad<O>()];
-    alignas(16) float h1[8][H];
     double epi[64][4];  // per-episode objective sums
 };
 constexpr int EVAL_MAX_WAVES = 8, EVAL_MAX_EPISODES = 64;
@@ -1403,19 +1030,9 @@ __global__ __launch_bounds__(64 * EVAL_MAX_WAVES) void eval_wave_kernel(EvalArgs
         for (int k = 0; k < K; ++k) acc[k] = 0.0;
         for (int st = 0; st < maxs; ++st) {  // SynthMO episodes end at the time limit
             float mu[A];
-            if constexpr (PGM_ROLL_DPP) {
-                double v = s;  // (lanes >= O: ignored by the broadcast)
-                if (a.use_ob) v = clipd((v - mean) * inv, -10.0, 10.0);
-                pol.forward_reg((float)v, l, mu, S.h1[w]);
-            } else {
-                if (fl) {
-                    double v = s;
-                    if (a.use_ob) v = clipd((v - mean) * inv, -10.0, 10.0);
-                    S.x[w][l] = (float)v;
-                }
-                wave_lds_fence_r();
-                pol.forward(S.x[w], S.h1[w], l, mu);
-            }
+            double v = s;  // (lanes >= O: ignored by the broadcast)
+            if (a.use_ob) v = clipd((v - mean) * inv, -10.0, 10.0);
+            pol.forward_reg((float)v, mu);
             double ac[A], sq[A];
 #pragma unroll
             for (int j = 0; j < A; ++j) {  // deterministic action = mean, clipped by the env
@@ -1454,42 +1071,6 @@ static int launch_k(Kern k, dim3 grid, dim3 block, size_t smem, hipStream_t s, c
 
 static bool lanes_dims(int O, int K) { return O <= 48 && O + K + 1 <= 64; }
 
-// The split rollout's chain -> objective scratch, one per device, grown on demand (a library-internal buffer: the
-// rollout ABI has no workspace argument), and the launch epoch its progress words carry (never reset: a word from an
-// earlier launch is below every value this launch waits for).  Rollouts on one device run in stream order (the
-// drop-in issues them on one stream), which the shared scratch relies on.
-static void* split_scratch(size_t bytes, int P, hipStream_t s, unsigned* epoch) {
-    static void* ptr[64];
-    static size_t cap[64];
-    static unsigned ep[64];
-    static int hdr_p[64];  // the task count whose progress words were last zeroed (the layout depends on P)
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
-        set_error("pgm_rollout: no current device for the split scratch");
-        return nullptr;
-    }
-    if (cap[dev] < bytes) {
-        if (ptr[dev]) (void)hipFree(ptr[dev]);  // (synchronises: growth is rare)
-        ptr[dev] = nullptr;
-        cap[dev] = 0;
-        hdr_p[dev] = 0;
-        if (hipMalloc(&ptr[dev], bytes) != hipSuccess) {
-            set_error("pgm_rollout: split scratch of %zu bytes", bytes);
-            return nullptr;
-        }
-        cap[dev] = bytes;
-    }
-    if (hdr_p[dev] != P) {  // zero the progress words once per layout; the epoch orders every later launch
-        if (hipMemsetAsync(ptr[dev], 0, split_hdr_bytes(P), s) != hipSuccess) {
-            set_error("pgm_rollout: split scratch reset");
-            return nullptr;
-        }
-        hdr_p[dev] = P;
-    }
-    *epoch = ++ep[dev];
-    return ptr[dev];
-}
-
 bool rollout_lanes_supported(const pgm_dims* d) {
     return lanes_dims(d->O, d->K) && (d->N == 1 || d->N == 2 || d->N == 4 || d->N == 8);
 }
@@ -1501,26 +1082,9 @@ bool eval_waves_supported(const pgm_dims* d, int eval_num) {
 template <int O, int A, int K, int NN>
 static int launch_rollout_n(const pgm_dims* d, const RolloutArgs& a, hipStream_t s) {
     constexpr int NW = NN < 4 ? NN : 4;
-    // PGM_ROLL_SPLIT=1 (A/B): the roles in two workgroups per task.  Measured slower, Walker P = 40 2.31 vs 1.90 ms per
-    // rollout + critic values: every published chunk costs the chain a drain of its sc1 stores (~1.5 us per publish),
-    // and the objective workgroup's loads of each chunk pay a memory round trip (the sc1 stores dropped the lines from L2)
-    const char* sel = getenv("PGM_ROLL_SPLIT");
-    const bool split = sel && sel[0] == '1' && 2 * d->P <= device_cu_count();
-    if (split) {
-        RolloutArgs b = a;
-        b.scratch = split_scratch(split_scratch_bytes(d->P, d->T, NN, O), d->P, s, &b.epoch);
-        if (!b.scratch) return PGM_E_HIP;
-        auto kern = rollout_lane_kernel<O, A, K, NN, true>;
-        const size_t smem = sizeof(LaneSmem<O, A, NN>);
-        hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-        if (e != hipSuccess) return hip_fail(e, "pgm_rollout");
-        // the objective workgroups spin on the chain workgroups' progress: the whole grid must be resident
-        if (int rc = check_coresident((const void*)kern, 64 * NW, smem, 2 * d->P, "pgm_rollout (split)")) return rc;
-        if (int rc = launch_k(kern, dim3(2 * d->P), dim3(64 * NW), smem, s, b, "pgm_rollout")) return rc;
-    } else if (int rc = launch_k(rollout_lane_kernel<O, A, K, NN, false>, dim3(d->P), dim3(2 * 64 * NW),
-                                 sizeof(LaneSmem<O, A, NN>), s, a, "pgm_rollout")) {
+    if (int rc = launch_k(rollout_lane_kernel<O, A, K, NN>, dim3(d->P), dim3(2 * 64 * NW), sizeof(LaneSmem<O, A, NN>), s,
+                          a, "pgm_rollout"))
         return rc;
-    }
     return launch_critic_values(d, a, s);
 }
 
@@ -1529,11 +1093,9 @@ int launch_critic_values(const pgm_dims* d, const RolloutArgs& a, hipStream_t s)
         constexpr int O = decltype(o)::value, K = decltype(k)::value;
         const int R = (d->T + 1) * d->N;
         ValueArgs va{R, a.L, a.params, a.rb.obs, a.rb.values};
-        if constexpr (O <= 32 && PGM_EXP != 46) {
-            // persistent workgroups: VM_PER_CU per CU over the tasks (>= 1 per task), at most one per 4 tiles.
-            // PGM_EXP 47 (A/B): two per CU (two waves per SIMD)
-            constexpr int VM_PER_CU = PGM_EXP == 47 ? 2 : 1;
-            const int wg = max(1, min(VM_PER_CU * device_cu_count() / d->P, (R + 127) / 128));
+        if constexpr (O <= 32) {
+            // persistent workgroups: one per CU over the tasks (>= 1 per task), at most one per 4 tiles
+            const int wg = max(1, min(device_cu_count() / d->P, (R + 127) / 128));
             return launch_k(value_mfma_kernel<O, K>, dim3(wg, d->P), dim3(256), sizeof(CriticMSmem<O, K>), s, va,
                             "pgm_rollout (critic values)");
         }

@@ -282,8 +282,9 @@ class _StateDictWriter:
     the first is saved by torch.save into memory; every later file is that zip image with the tensor records' bytes
     replaced (torch.save stores them uncompressed, 64-B aligned, one record per storage in state_dict order) and each
     patched record's CRC-32 recomputed (zlib.crc32, local header and central directory), so every file is a valid zip
-    exactly like torch.save's.  The first templated file is read back with torch.load(weights_only=True) and
-    compared; any mismatch falls back to torch.save for every file."""
+    exactly like torch.save's.  Before the writer is used, a templated image of a probe state_dict (same keys, shapes
+    and dtypes, different values) is read back with torch.load(weights_only=True) and compared, synchronously; any
+    mismatch makes ``ok`` False and every file goes through torch.save."""
 
     def __init__(self, sd):
         import io
@@ -317,8 +318,20 @@ class _StateDictWriter:
                     return
                 self.rec.append((h + 30 + fl + el, zi.file_size, h + 14, cd[zi.filename] + 16))
             self.ok = True
+            self._self_check(sd)
         except Exception:
             self.ok = False
+
+    def _self_check(self, sd):
+        """The templated image of a probe state_dict must torch.load to exactly that state_dict."""
+        import io
+        probe = {}
+        for i, key in enumerate(self.keys):
+            t = sd[key].detach()
+            probe[key] = (torch.arange(t.numel(), dtype=torch.float64).reshape(t.shape) * 0.5 + i + 1).to(t.dtype)
+        got = torch.load(io.BytesIO(bytes(self._render([probe[k].numpy() for k in self.keys]))), weights_only=True)
+        self.ok = list(got) == self.keys and all(torch.equal(got[k], probe[k]) and got[k].dtype == probe[k].dtype
+                                                 for k in self.keys)
 
     def save(self, sd, path):
         if not self.ok:
@@ -328,6 +341,11 @@ class _StateDictWriter:
 
     def save_records(self, arrays, path):
         """The templated file from the state_dict's tensors as numpy arrays (state_dict order, exact dtypes)."""
+        buf = self._render(arrays)
+        with open(path, 'wb') as fp:
+            fp.write(buf)
+
+    def _render(self, arrays):
         import zlib
         buf = bytearray(self.tmpl)
         for (off, size, lcrc, ccrc), arr in zip(self.rec, arrays):
@@ -337,8 +355,7 @@ class _StateDictWriter:
                 crc = zlib.crc32(data).to_bytes(4, 'little')
                 buf[lcrc:lcrc + 4] = crc
                 buf[ccrc:ccrc + 4] = crc
-        with open(path, 'wb') as fp:
-            fp.write(buf)
+        return buf
 
     def verify(self, sd, path):
         """torch.load of a templated file must equal its state_dict bit for bit (else: torch.save from now on)."""
@@ -388,22 +405,19 @@ class EPFileCache:
             flats = torch.stack([smp.snapshot.params for _, smp in new])
             if self.sdw is None:
                 self.sdw = _StateDictWriter(layout.unflatten(flats[0]))
-            sdw = self.sdw
+            sdw = self.sdw  # (its template was verified when it was built: the path chosen here is final)
             blocks = layout.unflatten_batch(flats) if sdw.ok else None
             sds = None if blocks is not None else [layout.unflatten(f) for f in flats]
             envs = [smp.env_params for _, smp in new]
             paths = [self._paths(uid) for uid, _ in new]
             for (uid, _), pp in zip(new, paths):
                 self.files[uid] = pp
-            first = not os.path.isdir(self.dir)
 
             def job():
                 os.makedirs(self.dir, exist_ok=True)
                 for i, (pt, pkl) in enumerate(paths):
                     if blocks is not None:
                         sdw.save_records([b[i] for b in blocks], pt)
-                        if first and i == 0:
-                            sdw.verify({k: torch.from_numpy(b[0]) for k, b in zip(sdw.keys, blocks)}, pt)
                     else:
                         sdw.save(sds[i], pt)
                     with open(pkl, 'wb') as fp:

@@ -1,13 +1,19 @@
 """Reduce rocprofv3 --pmc counter_collection CSVs to per-launch HBM bytes per kernel.
 
 FETCH_SIZE (KB) is doubled on gfx950 (MI355X_MICROARCH.md: it reports half the bytes of wide coalesced reads);
-WRITE_SIZE (KB) is taken as is.  Usage: pmc_summary.py DIR [bench args]; prints one JSON object.
+WRITE_SIZE (KB) is taken as is.  Usage: pmc_summary.py DIR [bench args]; prints one JSON object.  It records the
+update variant the profiled bench launched (its JSON line in DIR/FETCH_SIZE.log: roofline.kernel, the
+pgm_ppo_update_variant string) and the hash of that kernel's sources (bench.kernel_source_hash): bench.py quotes the
+summary only for the same variant and sources.
 """
 import csv
 import glob
 import json
+import os
 import sys
 from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def per_dispatch(d, counter):
@@ -45,7 +51,13 @@ def main():
     upd = sorted((k for k in kernels if 'ppo_update_' in k), key=lambda k: (-kernels[k]['launches'], k))
     env, P, N = opt('--env-name', 'MO-Walker2d-v2'), opt('--tasks', '40'), opt('--num-processes', '4')
     T, E, M = opt('--num-steps', '2048'), opt('--ppo-epoch', '10'), opt('--num-mini-batch', '32')
+    variant = None
+    for line in open(os.path.join(d, 'FETCH_SIZE.log')):
+        if line.startswith('{'):
+            variant = json.loads(line)['roofline']['kernel']
+    from bench import kernel_source_hash
     out = {'workload': f'{env}/P{P}/N{N}/T{T}/E{E}/M{M}',
+           'variant': variant, 'source_hash': kernel_source_hash(variant),
            'kernel': upd[0] if upd else None,
            'hbm_bytes_per_launch': kernels[upd[0]]['hbm_bytes_per_launch'] if upd else None,
            'method': 'rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes, per-dispatch sums; '

@@ -71,3 +71,38 @@ def test_failing_rank_ends_the_run():
     assert r.returncode != 0
     assert 'rank 1 exited with 3' in r.stderr
     assert not [l for l in r.stdout.splitlines() if l.startswith('{')]
+
+
+def _bench_module():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location('pgm_bench', BENCH)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_pmc_traffic_is_quoted_only_for_the_same_variant_and_sources(tmp_path):
+    """roofline.traffic comes from a PMC summary of exactly the launch the bench ran: the full
+    pgm_ppo_update_variant string (family, NS, R, two per CU) and the hash of that kernel's sources.  A summary of
+    another variant of the same family, or of older sources, is refused with a reason."""
+    import argparse
+    import json
+    b = _bench_module()
+    wl = 'MO-HalfCheetah-v2/P20/N4/T2048/E10/M32'
+    variant = 'ppo_update_fs_kernel (NS=8, R=2, 2 per CU)'
+    good = {'workload': wl, 'variant': variant, 'source_hash': b.kernel_source_hash(variant),
+            'hbm_bytes_per_launch': 123.0}
+    f = tmp_path / 'pmc.json'
+    args = argparse.Namespace(traffic_file=str(f))
+    f.write_text(json.dumps(good))
+    assert b.pmc_traffic(args, wl, variant) == (123.0, str(f))
+    for bad, why in ((dict(good, variant='ppo_update_fs_kernel (NS=4, R=4)'), 'not'),
+                     (dict(good, source_hash='0' * 16), 'stale'),
+                     (dict(good, workload='MO-HalfCheetah-v2/P10/N4/T2048/E10/M32'), 'no PMC summary')):
+        f.write_text(json.dumps(bad))
+        got, reason = b.pmc_traffic(args, wl, variant)
+        assert got is None and why in reason, (bad, reason)
+    # the committed index: every entry names its variant and source hash
+    idx = json.load(open(os.path.join(ROOT, 'profiles', 'pmc_head.json')))['entries']
+    for w, ent in idx.items():
+        assert ent.get('variant') and ent.get('source_hash'), w

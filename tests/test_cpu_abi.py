@@ -118,8 +118,8 @@ def test_update_workspace_covers_every_split(env, P, N, T):
     tower): tagged granules (the row-split updates' norm granules, 2 towers x 4 parts x 2 step parities x P + 1, then
     from granule 16 P + 8 the feature-split update's [3 kinds][P][2 towers][<= 16 parts][2 parities]; 256-B padded),
     exchange slots [P][2 towers][4 parts][2 parities], and the packed sample table + the feature-split payload
-    (obs_dim <= 32: [P][2][NS][2] image slots of NB KiB and parameter slots of 8 ceil(ceil(NB / NS) / 4) KiB, NS the largest
-    power of two <= 16 with 16 NS ceil(P / 8) <= 512, NB = 4 (ceil(O / 16) + 6)) or the parts' private parameter
+    (obs_dim <= 32: [P][2][NS][2] image slots of NB KiB and parameter slots of 4 ceil(ceil(NB / NS) / 4) KiB, NS = 16,
+    the largest a launch with P' <= P tasks may pick, NB = 4 (ceil(O / 16) + 6)) or the parts' private parameter
     rows (wide)."""
     from pgmorl_amd import envspec
     spec = envspec.make_spec(env)
@@ -134,10 +134,8 @@ def test_update_workspace_covers_every_split(env, P, N, T):
         n = O + A + 2 + 2 * K
         rs = 16 if n <= 16 else 32 if n <= 32 else 64 if n <= 64 else 128
         ns = 16
-        while ns > 1 and 16 * ns * -(-P // 8) > 512:  # two workgroups per CU where they fit (fs_choose_ns)
-            ns //= 2
         nb = 4 * (-(-O // 16) + 6)
-        fs = P * 2 * ns * 2 * (nb + 2 * 4 * -(-(-(-nb // ns)) // 4)) * 1024 if ns >= 2 else 0
+        fs = P * 2 * ns * 2 * (nb + 4 * -(-(-(-nb // ns)) // 4)) * 1024
         want = flags + P * 2 * 4 * 2 * xslot * 8 + P * T * N * rs * 4 + fs
     else:
         img = H * (H + 1) + Q * H + 2 * H + Q + A
@@ -147,3 +145,42 @@ def test_update_workspace_covers_every_split(env, P, N, T):
         L = ParamLayout(O, A, K).total
         want = flags + P * 2 * 4 * 2 * xslot * 8 + P * 3 * L * 4
     assert got == want, (got, want)
+
+
+def _fs_need(P, O):
+    """Feature-split payload a launch with P tasks uses (pgm_ppo_fs.hip): NS = the largest power of two <= 16 with
+    16 NS ceil(P / 8) <= 512, [P][2][NS][2] slots of NB + 4 ceil(ceil(NB / NS) / 4) KiB."""
+    ns = 16
+    while ns > 1 and 16 * ns * -(-P // 8) > 512:
+        ns //= 2
+    nb = 4 * (-(-O // 16) + 6)
+    return P * 2 * ns * 2 * (nb + 4 * -(-(-(-nb // ns)) // 4)) * 1024 if ns >= 2 else 0
+
+
+@pytest.mark.parametrize('env', ['MO-Walker2d-v2', 'MO-Hopper-v3', 'MO-Ant-v2', 'MO-Humanoid-v2'])
+def test_update_workspace_is_monotone_in_tasks(env):
+    """A workspace sized for a capacity of P tasks serves every launch with P' <= P active tasks (TaskBatch allocates
+    once for its capacity and set_active() launches fewer): the byte count is monotone in P and covers the payload of
+    the feature-split NS that P' tasks pick, which can exceed the one P tasks pick (8 parts at P' = 32, 4 at P = 33)."""
+    from pgmorl_amd import envspec
+    spec = envspec.make_spec(env)
+    O, A, K = spec['obs_dim'], spec['act_dim'], spec['obj_num']
+    L = _lib.lib()
+    prev = 0
+    sizes = []
+    for P in range(1, 130):
+        got = L.pgm_ppo_update_workspace_bytes(_lib.Dims(P, 4, 2048, O, A, K, 64))
+        assert got >= prev, (P, got, prev)
+        prev = got
+        sizes.append(got)
+    if O <= 32:
+        n = O + A + 2 + 2 * K
+        rs = 16 if n <= 16 else 32 if n <= 32 else 64 if n <= 64 else 128
+        for cap in (33, 41, 65, 129):
+            fixed = sizes[cap - 1]
+            for P in range(1, cap + 1):  # the active launch's own layout: everything before the payload, then it
+                flags = -(-(16 * P + 8 + 3 * P * 2 * 16 * 2) * 8 // 256) * 256
+                img = O * 64 + 64 * 65 + max(A, K) * 64 + 2 * 64 + max(A, K) + A
+                xslot = -(-(img + 1) // 32) * 32
+                need = flags + P * 2 * 4 * 2 * xslot * 8 + P * 2048 * 4 * rs * 4 + _fs_need(P, O)
+                assert need <= fixed, (cap, P, need, fixed)

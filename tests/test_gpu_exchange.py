@@ -27,9 +27,8 @@ DELAY = 4_000_000  # shader cycles (~2 ms): far beyond one Adam step, far below 
 
 
 def _run_update(env, P, T, N, E, M, split, delay, monkeypatch):
-    if split in ('fs', 'fst'):  # fst: the tagged parameter hop
+    if split == 'fs':
         monkeypatch.setenv('PGM_UPDATE_KERNEL', 'fs')
-        monkeypatch.setenv('PGM_FS_PTAG', '1' if split == 'fst' else '0')
     else:
         monkeypatch.setenv('PGM_UPDATE_SPLIT', split)
     if delay is not None:
@@ -59,7 +58,7 @@ def _run_update(env, P, T, N, E, M, split, delay, monkeypatch):
 
 def block_of(kernel, task, tower, part, ns=4):
     """blockIdx.x of (task, tower 0 = critic / 1 = actor, row part) under the HEAD block maps: every workgroup of a
-    task on blocks b, b + 8, ... (one XCD) -- MODE 2 (pgm_ppo_mfma.hip ppo_update_mfma_kernel, PGM_MODE2_XCD4): groups
+    task on blocks b, b + 8, ... (one XCD) -- MODE 2 (pgm_ppo_mfma.hip ppo_update_mfma_kernel): groups
     of 32 blocks per 8 tasks, block r = half (r >> 4) & 1 of tower (r >> 3) & 1 of task 8 G + (r & 7); t16 (NS = 4)
     and the feature-split kernel (pgm_ppo_fs.hip, NS parts): groups of 16 NS blocks per 8 tasks, block r = part
     ((r >> 3) % 2 NS) >> 1 of tower (r >> 3) & 1 of task 8 G + (r & 7)."""
@@ -97,17 +96,17 @@ CASES = [('2', 0, 0, 0, 0), ('2', 0, 1, 1, 0), ('2', 0, 0, 1, 1), ('2', 0, 1, 0,
 def test_delayed_handoff_keeps_parity(gpu, split, task, tower, part, where, monkeypatch):
     # Walker, 2 tasks, mb = 256 (the single-tile specialisations of MODE 2 / t16; fs: 16 parts of one 16-row tile),
     # 4 Adam steps; the stall hits step 1 (both parities are exercised before and after it)
-    block = block_of(split, task, tower, part, 16 if split in ('fs', 'fst') else 4)
+    block = block_of(split, task, tower, part, 16 if split == 'fs' else 4)
     _run_update('MO-Walker2d-v2', 2, 256, 4, 1, 4, split, (1, block, where, DELAY), monkeypatch)
 
 
-@pytest.mark.parametrize('split', ['2', '4', 'fs', 'fst'])
+@pytest.mark.parametrize('split', ['2', '4', 'fs'])
 def test_delay_on_last_step_and_ragged_grid(gpu, split, monkeypatch):
     # Hopper-v3 (3 objectives), 5 tasks (a partial group of 8 tasks in the block map), multi-pass minibatches for
     # MODE 2 / t16 (mb = 128 with N = 2: not the single-tile path; fs: 8 parts of one tile); stall the last task's
     # actor part 0 on the last step
     P = 5
-    block = block_of(split, P - 1, 1, 0, 8 if split in ('fs', 'fst') else 4)
+    block = block_of(split, P - 1, 1, 0, 8 if split == 'fs' else 4)
     _run_update('MO-Hopper-v3', P, 128, 2, 1, 2, split, (1, block, 2, DELAY), monkeypatch)
 
 

@@ -15,9 +15,11 @@ from .test_gpu_kernels import _close, _update_setup
 pytestmark = pytest.mark.gpu
 
 
-def _check_update(env, P, N, E, M, mb, seed, entropy_coef=0.0):
+def _check_update(env, P, N, E, M, mb, seed, entropy_coef=0.0, capacity=None, variant=None):
     T = mb * M // N
-    args, spec, tb, pols, data, perms = _update_setup(env, P, T, N, E, M, seed=seed)
+    args, spec, tb, pols, data, perms = _update_setup(env, P, T, N, E, M, seed=seed, capacity=capacity)
+    if variant is not None:
+        assert tb.update_variant() == variant
     obs, actions, logp, values, returns, adv = data
     lr = 3e-4
     tb.lr.fill_(lr)
@@ -59,13 +61,20 @@ def _check_update(env, P, N, E, M, mb, seed, entropy_coef=0.0):
                                              ('MO-Hopper-v3', 27, 4, 256, '1'),      # NS 8, R 2, 2 per CU, 3 objectives
                                              ('MO-Hopper-v2', 5, 1, 64, '1'),        # NS 4, R 1 (config 0)
                                              ('MO-Ant-v2', 3, 2, 128, '1')])         # NS 8, R 1, O = 27 (two dW1 blocks)
-@pytest.mark.parametrize('ptag', ['0', '1'])
-def test_fs_update_all_tasks(gpu, monkeypatch, env, P, N, mb, dual, ptag):
-    # ptag 1: the parameter hop as tagged {value, step} granules, readers re-loading until the tags match
+def test_fs_update_all_tasks(gpu, monkeypatch, env, P, N, mb, dual):
     monkeypatch.setenv('PGM_UPDATE_KERNEL', 'fs')
-    monkeypatch.setenv('PGM_FS_PTAG', ptag)
     monkeypatch.setenv('PGM_FS_DUAL', dual)
     _check_update(env, P, N, E=2, M=2, mb=mb, seed=41)  # 4 Adam steps: both slot parities twice
+
+
+def test_fs_update_capacity_above_active_tasks(gpu, monkeypatch):
+    """A batch allocated for 33 task slots running 32 (TaskBatch.set_active): at 32 tasks the feature-split update
+    takes 8 parts per tower (16 NS ceil(P / 8) = 512, two per CU), at 33 only 4, and its exchange payload grows with
+    NS -- the workspace of the 33-slot batch must hold the 32-task launch's (it was sized by the cap at the
+    capacity).  Every task vs the oracle, and the exchange-timeout word."""
+    monkeypatch.setenv('PGM_UPDATE_KERNEL', 'fs')
+    _check_update('MO-Walker2d-v2', 32, 4, E=1, M=2, mb=256, seed=47, capacity=33,
+                  variant='ppo_update_fs_kernel (NS=8, R=2, 2 per CU)')
 
 
 def test_fs_two_workgroups_per_cu_variant(gpu):

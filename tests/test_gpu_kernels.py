@@ -141,9 +141,9 @@ def test_adv_normalize(gpu, use_obj_rms):
         _close(got[p], ref.numpy(), 1e-5, 1e-5, 'advantages')
 
 
-def _update_setup(env, P, T, N, E, M, seed):
+def _update_setup(env, P, T, N, E, M, seed, **kw):
     args = small_args(env, num_steps=T, num_processes=N, ppo_epoch=E, num_mini_batch=M)
-    spec, tb, pols = _batch_with_policies(env, P, N, T, seed=seed, scale=0.05, ppo_epoch=E, num_mini_batch=M)
+    spec, tb, pols = _batch_with_policies(env, P, N, T, seed=seed, scale=0.05, ppo_epoch=E, num_mini_batch=M, **kw)
     O, A, K, B = spec['obs_dim'], spec['act_dim'], spec['obj_num'], T * N
     rng = np.random.RandomState(seed)
     obs = np.clip(rng.randn(P, T + 1, N, O), -3, 3).astype(np.float32)
@@ -167,16 +167,16 @@ def _update_setup(env, P, T, N, E, M, seed):
     return args, spec, tb, pols, (obs, actions, logp, values, returns, adv), perms
 
 
-@pytest.mark.parametrize('kernel', ['t16x4', 't16x2', 'mfma', 'mfma-tower', 'mfma-joint', 'valu'])
+@pytest.mark.parametrize('kernel', ['t16x4', 'mfma', 'mfma-tower', 'mfma-joint', 'valu'])
 @pytest.mark.parametrize('env,T,N,E,M', [('MO-Hopper-v2', 64, 4, 2, 4), ('MO-Walker2d-v2', 128, 4, 2, 2),
                                          ('MO-Hopper-v3', 50, 3, 1, 3), ('MO-Swimmer-v2', 64, 1, 1, 1),
                                          ('MO-Ant-v2', 160, 4, 1, 2), ('MO-Walker2d-v2', 2048, 4, 1, 32)])
 def test_ppo_update(gpu, env, T, N, E, M, kernel, monkeypatch):
-    # t16x4 / t16x2: 16-row tiles, each tower on 4 workgroups of 4 waves / 2 workgroups of 8 waves; mfma: 32-row
+    # t16x4: 16-row tiles, each tower on 4 workgroups of 4 waves; mfma: 32-row
     # tiles, each tower on two workgroups, half the minibatch rows each; mfma-tower: one workgroup per tower;
     # mfma-joint: one workgroup per task
     monkeypatch.setenv('PGM_UPDATE_KERNEL', 'valu' if kernel == 'valu' else 'mfma')
-    monkeypatch.setenv('PGM_UPDATE_SPLIT', {'t16x4': '4', 't16x2': '3', 'mfma': '2', 'mfma-tower': '1',
+    monkeypatch.setenv('PGM_UPDATE_SPLIT', {'t16x4': '4', 'mfma': '2', 'mfma-tower': '1',
                                             'mfma-joint': '0'}.get(kernel, '2'))
     P, lr = 2, 3e-4
     args, spec, tb, pols, data, perms = _update_setup(env, P, T, N, E, M, seed=11)
@@ -275,7 +275,7 @@ def _teacher_forced_check(tb, p, pol, spec, s0, noise):
     _close(tb.ob_var[p].cpu(), envs.ob_rms.var, 1e-9, 1e-6, 'ob_rms.var')
 
 
-@pytest.mark.parametrize('kernel', ['lanes', 'block', 'split'])
+@pytest.mark.parametrize('kernel', ['lanes', 'block'])
 @pytest.mark.parametrize('env,N,T', [('MO-Hopper-v2', 4, 48), ('MO-Walker2d-v2', 2, 520), ('MO-Hopper-v3', 6, 40),
                                      ('MO-Hopper-v3', 8, 40), ('MO-Walker2d-v2', 1, 33), ('MO-Ant-v2', 4, 24),
                                      ('MO-Humanoid-v2', 8, 40), ('MO-Humanoid-v2', 8, 1003), ('MO-Humanoid-v2', 4, 33),
@@ -287,10 +287,7 @@ def test_rollout(gpu, env, N, T, kernel, monkeypatch):
     # lanes: one wave per env + batched critic values (default for N in 1/2/4/8; obs_dim > 48 takes the wide
     # kernel: k-sliced layer 1 over 4 waves, feature-per-lane dynamics); block: workgroup per step.
     # Humanoid T = 1003 crosses the 1000-step time limit (auto-reset, bad_transition) and 31 noise chunks
-    # split (A/B): the lane kernel's chain and objective roles in two workgroups per task (PGM_ROLL_SPLIT=1)
-    if kernel == 'split':
-        monkeypatch.setenv('PGM_ROLL_SPLIT', '1')
-    monkeypatch.setenv('PGM_ROLLOUT_KERNEL', 'lanes' if kernel == 'split' else kernel)
+    monkeypatch.setenv('PGM_ROLLOUT_KERNEL', kernel)
     P = 2
     spec, tb, pols = _batch_with_policies(env, P, N, T, seed=3, scale=0.05)
     s0 = envspec.reset_table(spec['obs_dim'], 0, N)

@@ -44,11 +44,20 @@ CONFIGS = {  # pop and the reference's per-env flags (scripts/*.py), iterations 
     # scripts/hopper-v3.py: 3 objectives, delta 0.25 (15 warm-up tasks), pbuffer-num 20, sparsity 1e6
     'MO-Hopper-v3': dict(delta='0.25', tasks=15, N=4, warmup=4, update=3, gens=3,
                          extra=['--pbuffer-num', '20', '--sparsity', '1000000.0']),
+    # config 4 reduced (scripts/humanoid-v2.py: N = 8, gamma 0.99, eval_num 6, warm-up 200 / update 40 iterations at
+    # delta 0.2): 5 tasks (delta 0.25), warm-up 40 + 2 generations x 10 = 60 iterations, past the iteration (~34)
+    # where the archive of non-negative points first fills (profiles/r04_humanoid_hv.json)
+    'MO-Humanoid-v2': dict(delta='0.25', tasks=5, N=8, warmup=40, update=10, gens=2,
+                           extra=['--gamma', '0.99', '--eval-num', '6']),
+    # config 1 at 3.3x the comparison budget (4 + 3 x 15 iterations): does the device-vs-oracle difference grow?
+    'MO-Walker2d-v2-long': dict(env='MO-Walker2d-v2', delta=str(1.0 / 39.0), tasks=40, N=4, warmup=4, update=15,
+                                gens=3, extra=[]),
 }
 
 
 def make_args(env, seed, save_dir):
     c = CONFIGS[env]
+    env = c.get('env', env)  # (a config key may name a budget variant of an env)
     T = 2048
     iters = c['warmup'] + c['gens'] * c['update']
     spec = envspec.make_spec(env)

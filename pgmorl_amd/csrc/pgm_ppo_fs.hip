@@ -54,14 +54,18 @@ constexpr int fs_pslots(int O, int NS) { return 4 * ((fs_nown(O, NS) + 3) / 4); 
 inline size_t fs_payload_bytes(int P, int O, int NS) {
     return (size_t)P * 2 * NS * 2 * (size_t)(fs_nb(O) + fs_pslots(O, NS)) * 1024;
 }
-// NS sized by the workspace: the largest power of two with 16 NS ceil(P/8) <= 512 (a 256-CU MI355X with two
-// workgroups per CU where R <= 2 lets them share one, fs_choose_ns), at most 16
-inline int fs_ns_cap(int P) {
-    const int groups = (P + 7) / 8;
-    int ns = 16;
-    while (ns > 1 && 16 * ns * groups > 512) ns >>= 1;
-    return ns;
+// parts per tower the update is built for, largest first (6: 96 blocks per group of 8 tasks, so that five groups --
+// 33..40 tasks -- fit a 256-CU MI355X twice over with two workgroups per CU)
+constexpr int FS_NS_LIST[] = {16, 8, 6, 4, 2};
+// (parts, 16-row tiles per part) pairs the library is built for: minibatches of 64 / 128 / 256 / 512 rows on power-of-two
+// parts and tiles, and 6 parts of 3 tiles
+constexpr bool fs_built(int ns, int R) {
+    const int mb = 16 * ns * R;
+    return (ns == 6 && R == 3) ||
+           (ns != 6 && (R == 1 || R == 2 || R == 4 || R == 8) && (mb == 64 || mb == 128 || mb == 256 || mb == 512));
 }
+// 16-row tiles of the part with the most (parts 0 .. (mb / 16) % NS - 1 take one more than the others)
+inline int fs_tiles(int mb, int ns) { return (mb / 16 + ns - 1) / ns; }
 inline int fs_grid(int P, int NS) { return 16 * NS * ((P + 7) / 8); }
 // tagged granules of the exchange, in the zeroed flag region after the norm granules of the other updates:
 // kind 0 = image flag, 1 = squared-norm granule, 2 = parameter flag
@@ -69,7 +73,7 @@ __host__ __device__ inline int fs_gran(int P, int NS, int kind, int p, int m, in
     return 16 * P + 8 + ((((kind * P + p) * 2 + m) * NS + hs) * 2 + par);
 }
 
-// Sized for the largest NS (16), not fs_ns_cap(P): a caller may allocate the workspace for a capacity P and launch
+// Sized for the largest NS (16), not the NS a launch with P tasks picks: a caller may allocate the workspace for a capacity P and launch
 // with fewer active tasks (TaskBatch.set_active), whose cap can be LARGER (8 parts at P = 32, 4 at P = 33), and
 // NS (NB + pslots(NS)) grows with NS, so this bounds the payload of every launch with P' <= P tasks.
 size_t fs_workspace_extra(const pgm_dims* d) {
@@ -108,14 +112,15 @@ struct FsSmem {
     static constexpr int NDT = (SB * RSL + 255) / 256;         // 1-KiB LDS-DMA pieces per staged pass
     static constexpr int SBI = 64 * ((SB + 63) / 64);          // index slots (one 64-lane DMA per wave)
     // dZ2 tile aliases the H2 tile (LDS budget: R = 8 for 160 KiB; R = 2 to stay under 80 KiB, two workgroups per CU)
-    static constexpr bool ZA = R >= 8 || R == 2;
+    static constexpr bool ZA = R >= 8 || R == 2 || R == 3;
     static constexpr int NHP = R >= 4 ? 1 : 4;                 // partial head outputs (R < 4: one tile per wave)
     TowerImg<O, A, K> Pm;                                      // parameters (working copy of every part)
     alignas(16) float RB[2][NDT * 256];                        // packed rows of this / the next minibatch
     int32_t IB[2][SBI];                                        // sample indices of the next two minibatches
     // activation tiles [sample][feature], row stride SF = 72 floats (= 8 mod 64): the feature-contracting products read
     // 4 consecutive features per lane with ds_read_b128 (16-B aligned, conflict-free for the 16-row tiles)
-    static constexpr bool HT = R <= 4;                         // H1 also [feature][sample] (the dW2 A operand)
+    static constexpr bool HT = R <= 4 && R != 3;               // H1 also [feature][sample] (the dW2 A operand;
+                                                               // R = 3: not, to fit two workgroups per CU)
     static constexpr int STT = HT ? 72 : 4;                    // its row stride (16 R <= 64 samples, = 8 mod 64)
     alignas(16) float H1s[SB][SF];                             // H1 of all tiles, all 64 features
     alignas(16) float H2s[SB][SF];                             // H2 (R >= 8: then dZ2)
@@ -137,7 +142,7 @@ constexpr size_t fs_smem_bytes(bool dual) {
 // granule, readers re-loading a block until all its tags are this step's: P = 5 3.45 vs 2.93 ms, P = 20 5.06 vs 4.38 ms.)
 template <int O, int A, int K, int NS, int R>
 __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
-    static_assert(O <= 32 && R >= 1 && R <= 8 && (R & (R - 1)) == 0, "fs tiles");
+    static_assert(O <= 32 && (R == 1 || R == 2 || R == 3 || R == 4 || R == 8), "fs tiles");
     using Sm = FsSmem<O, A, K, R>;
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     auto& S = *reinterpret_cast<Sm*>(smem_raw);
@@ -166,7 +171,12 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
     const int N = a.N, T = a.T, B = T * N;
     const int E = a.hp.ppo_epoch, M = a.hp.num_mini_batch;
     const int mb = B / M, nb = B / mb;
-    const int r0 = hs * mb / NS;
+    // this part's rows of every minibatch: the mb / 16 row tiles dealt over the NS parts, the first (mb / 16) % NS parts
+    // one more (NS = 6 on a 256-row minibatch: 3 / 3 / 3 / 3 / 2 / 2); tiles past the part's own count are dummies
+    // (their rows repeat its last one) whose loss gradients and loss terms are zeroed, so they add exact zeros
+    const int ntl = mb >> 4, tb0 = ntl / NS, tex = ntl - tb0 * NS;
+    const int rown = 16 * (tb0 + (hs < tex ? 1 : 0));
+    const int r0 = 16 * (hs * tb0 + min(hs, tex));
     const int npass = E * nb;
     const float clip = a.hp.clip_param;
     const Layout& L = a.L;
@@ -194,7 +204,7 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
         const int e = gi / nb, bb = gi - e * nb;
         const int32_t* src = a.perms + (size_t)e * B + bb * mb + r0;
         for (int q0 = wi * 64; q0 < SB; q0 += 64 * nwv)
-            __builtin_amdgcn_global_load_lds((const void*)(src + min(q0 + l, SB - 1)), (lds_void_t*)&S.IB[buf][q0], 4,
+            __builtin_amdgcn_global_load_lds((const void*)(src + min(q0 + l, rown - 1)), (lds_void_t*)&S.IB[buf][q0], 4,
                                              0, 0);
     };
     auto issue_rows = [&](int buf, int ibuf, int wi, int nwv) {
@@ -356,10 +366,11 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
         const bool qv = c < Q;
         const float bhb = qv ? Wt.bh[c] : 0.f;
         float gbh = 0.f, gls = 0.f, lsum = 0.f;
-        // dL/d(head output) of sample s, output c (this lane), from the head output `out` (bias included)
-        auto loss1 = [&](const float* rr, int s, float out) -> float {
+        // dL/d(head output) of sample s, output c (this lane), from the head output `out` (bias included); tv = the
+        // tile is one of this part's own (a dummy tile's gradients and loss terms are zero)
+        auto loss1 = [&](const float* rr, int s, float out, bool tv) -> float {
             if (m == 0) {  // value loss over the K objectives
-                const bool ok = c < K;
+                const bool ok = c < K && tv;
                 const float Vold = rr[s * RSL + O + A + 2 + (c < K ? c : 0)];
                 const float Rt = rr[s * RSL + O + A + 2 + K + (c < K ? c : 0)];
                 float gv, ls;
@@ -389,8 +400,8 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
             const float s2 = fminf(fmaxf(ratio, 1.f - clip), 1.f + clip) * ad;
             const float inr = (ratio >= 1.f - clip && ratio <= 1.f + clip) ? 1.f : 0.f;
             const float gr = ad * (wmin2(s1, s2) + wmin2(s2, s1) * inr);
-            const float dlp = ascale * gr * ratio;
-            lsum += c == 0 ? -fminf(s1, s2) : 0.f;
+            const float dlp = tv ? ascale * gr * ratio : 0.f;
+            lsum += c == 0 && tv ? -fminf(s1, s2) : 0.f;
             gls += av_ ? dlp * (diff * diff * aiv - 1.f) : 0.f;
             return av_ ? dlp * diff * aiv : 0.f;
         };
@@ -417,7 +428,7 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
                 PGM_STAMP(14);
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const float d = loss1(rt(ti), 4 * g + r, ho[0][r] + bhb);
+                    const float d = loss1(rt(ti), 4 * g + r, ho[0][r] + bhb, 16 * ti < rown);
                     gbh += d;
                     if (c < DQ) dt[(16 * ti + 4 * g + r) * DQS + c] = d;
                 }
@@ -444,7 +455,7 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
                 const int s = 4 * g + w, row = 16 * ti + s;
                 const int cq = c < DQ ? c : 0;
                 const float out = c < DQ ? ((S.HP[0][row][cq] + S.HP[1][row][cq]) + S.HP[2][row][cq]) + S.HP[3][row][cq] : 0.f;
-                const float d = loss1(rt(ti), s, out + bhb);
+                const float d = loss1(rt(ti), s, out + bhb, 16 * ti < rown);
                 gbh += d;
                 if (c < DQ) dt[row * DQS + c] = d;
             }
@@ -785,13 +796,17 @@ int fs_choose_ns(const pgm_dims* d, int mb, int* dual) {
     const int cus = device_cu_count();
     const char* dsel = getenv("PGM_FS_DUAL");
     const bool dual_ok = !(dsel && dsel[0] == '0');
-    for (int ns = fs_ns_cap(d->P); ns >= 2; ns >>= 1) {
-        if (mb % (16 * ns) != 0) continue;
-        const int R = mb / (16 * ns);
-        if (R < 1 || R > 8 || (R & (R - 1)) != 0) continue;
+    if (mb % 16 != 0) return 0;
+    for (const int ns : FS_NS_LIST) {
+        // (6 parts: the row tiles dealt raggedly, at most 3 per part; other counts: an exact split)
+        if (ns != 6 && mb % (16 * ns) != 0) continue;
+        const int R = fs_tiles(mb, ns);
+        if (!fs_built(ns, R)) continue;
         const int grid = fs_grid(d->P, ns);
+        if (grid > 2 * cus) continue;
         if (grid <= cus) return ns;
-        if (dual_ok && R == 2 && grid <= 2 * cus) {  // (R 4 -> 2 pays; R 2 -> 1 does not: Walker P = 10 3.18 -> 3.70 ms)
+        // two workgroups per CU for R = 2 / 3 (R 4 -> 2 pays; R 2 -> 1 does not: Walker P = 10 3.18 -> 3.70 ms)
+        if (dual_ok && (R == 2 || R == 3)) {
             MArgs q{};
             q.hp.num_mini_batch = d->T * d->N / mb;
             if (ppo_update_fs_op(d, q, ns, true, 1, nullptr) == 1) {
@@ -808,13 +823,14 @@ static int launch_fs_ns(const pgm_dims* d, const MArgs& a, int R, bool dual, int
     // minibatches of 64 / 128 / 256 / 512 rows (N = 1 / 2 / 4 / 8 at T = 2048, M = 32): 16 NS R = mb
     auto one = [&](auto rc) -> int {
         constexpr int RR = decltype(rc)::value, MB = 16 * NS * RR;
-        if constexpr (MB == 64 || MB == 128 || MB == 256 || MB == 512) return launch_fs_k<O, A, K, NS, RR>(d, a, dual, op, stream);
+        if constexpr (fs_built(NS, RR)) return launch_fs_k<O, A, K, NS, RR>(d, a, dual, op, stream);
         set_error("pgm_ppo_update (fs): minibatch of %d rows unsupported", MB);
         return PGM_E_UNSUPPORTED;
     };
     switch (R) {
         case 1: return one(ic<1>{});
         case 2: return one(ic<2>{});
+        case 3: return one(ic<3>{});
         case 4: return one(ic<4>{});
         case 8: return one(ic<8>{});
     }
@@ -828,7 +844,7 @@ int ppo_update_fs(const pgm_dims* d, const MArgs& a, int ns, bool dual, hipStrea
 }
 int ppo_update_fs_op(const pgm_dims* d, const MArgs& a, int ns, bool dual, int op, hipStream_t stream) {
     const int mb = d->T * d->N / a.hp.num_mini_batch;
-    const int R = mb / (16 * ns);
+    const int R = fs_tiles(mb, ns);
     return dispatch_dims(d->O, d->A, d->K, "pgm_ppo_update (fs)", [&](auto o, auto aa, auto k) -> int {
         constexpr int O = decltype(o)::value, A = decltype(aa)::value, K = decltype(k)::value;
 #ifdef PGM_STAMPS
@@ -842,6 +858,7 @@ int ppo_update_fs_op(const pgm_dims* d, const MArgs& a, int ns, bool dual, int o
             switch (ns) {
                 case 2: return launch_fs_ns<O, A, K, 2>(d, a, R, dual, op, stream);
                 case 4: return launch_fs_ns<O, A, K, 4>(d, a, R, dual, op, stream);
+                case 6: return launch_fs_ns<O, A, K, 6>(d, a, R, dual, op, stream);
                 case 8: return launch_fs_ns<O, A, K, 8>(d, a, R, dual, op, stream);
                 case 16: return launch_fs_ns<O, A, K, 16>(d, a, R, dual, op, stream);
             }

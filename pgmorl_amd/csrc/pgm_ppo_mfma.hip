@@ -1841,7 +1841,8 @@ int describe_update_mfma(const pgm_dims* d, const pgm_ppo_hparams* hp, char* buf
     const int mb = d->T * d->N / hp->num_mini_batch;
     const UpdateChoice c = choose_update(d, mb);
     if (c.kind == 2)
-        return snprintf(buf, n, "ppo_update_fs_kernel (NS=%d, R=%d%s)", c.ns, mb / (16 * c.ns), c.dual ? ", 2 per CU" : "");
+        return snprintf(buf, n, "ppo_update_fs_kernel (NS=%d, R=%d%s)", c.ns, (mb / 16 + c.ns - 1) / c.ns,
+                        c.dual ? ", 2 per CU" : "");
     if (c.kind == 1) return snprintf(buf, n, "ppo_update_t16_kernel (NS=%d, W=%d)", c.ns, c.w);
     return snprintf(buf, n, "ppo_update_mfma_kernel (MODE %d)", c.mode);
 }

@@ -14,7 +14,7 @@ from pgmorl_amd.runtime import TaskBatch
 
 ENV = os.environ.get('ENV', 'MO-Walker2d-v2')
 HUM = 'Humanoid' in ENV
-P, N, T = int(os.environ.get('P', 20 if HUM else 40)), 8 if HUM else 4, 2048
+P, N, T = int(os.environ.get('P', 20 if HUM else 40)), 8 if HUM else 4, int(os.environ.get('T', 2048))
 tb = TaskBatch(ENV, P, num_processes=N, num_steps=T)
 for p in range(P):
     tb.set_task(p, new_policy(tb.O, tb.A, tb.K).state_dict(), {}, None, [0.5, 0.5])

@@ -119,6 +119,14 @@ def test_delay_two_workgroups_per_cu(gpu, task, tower, part, where, monkeypatch)
     _run_update('MO-Walker2d-v2', 20, 256, 4, 1, 4, 'fs', (1, block, where, DELAY), monkeypatch)
 
 
+@pytest.mark.parametrize('task,tower,part,where', [(39, 1, 5, 1), (0, 0, 0, 3), (21, 1, 3, 2), (34, 0, 4, 0)])
+def test_delay_six_ragged_parts(gpu, task, tower, part, where, monkeypatch):
+    # Walker P = 40, 256-row minibatches over 6 parts of 3 / 3 / 3 / 3 / 2 / 2 row tiles (dummy tiles in parts 4, 5):
+    # 480 workgroups, two per CU; stalls in a 3-tile and in a 2-tile part
+    block = block_of('fs', task, tower, part, 6)
+    _run_update('MO-Walker2d-v2', 40, 256, 4, 1, 4, 'fs', (1, block, where, DELAY), monkeypatch)
+
+
 def test_coresidency_check_refuses_an_oversized_grid(gpu, monkeypatch):
     """The launcher refuses (PGM_E_UNSUPPORTED -> PGMError) a grid whose workgroups cannot all be resident:
     PGM_TEST_RESIDENT_CUS pretends the device has fewer CUs than the grid's workgroups (one per CU)."""

@@ -57,7 +57,10 @@ def _check_update(env, P, N, E, M, mb, seed, entropy_coef=0.0, capacity=None, va
                                              ('MO-Walker2d-v2', 10, 4, 256, '1'),    # NS 8, R 2 (pop 40 / 4: R 1 not doubled)
                                              ('MO-HalfCheetah-v2', 20, 4, 256, '1'),  # NS 8, R 2, 2 per CU (config 2)
                                              ('MO-HalfCheetah-v2', 20, 4, 256, '0'),  # NS 4, R 4
-                                             ('MO-Walker2d-v2', 40, 4, 256, '1'),    # NS 2, R 8 (config 1)
+                                             ('MO-Walker2d-v2', 40, 4, 256, '0'),    # NS 2, R 8 (one per CU)
+                                             ('MO-Walker2d-v2', 40, 4, 288, '1'),    # NS 6, R 3, 2 per CU
+                                             ('MO-Walker2d-v2', 40, 4, 256, '1'),    # NS 6, R 3/3/3/3/2/2, 2 per CU
+                                             ('MO-HalfCheetah-v2', 35, 4, 256, '1'),  # the same, a partial group
                                              ('MO-Hopper-v3', 27, 4, 256, '1'),      # NS 8, R 2, 2 per CU, 3 objectives
                                              ('MO-Hopper-v2', 5, 1, 64, '1'),        # NS 4, R 1 (config 0)
                                              ('MO-Ant-v2', 3, 2, 128, '1')])         # NS 8, R 1, O = 27 (two dW1 blocks)
@@ -86,9 +89,11 @@ def test_fs_two_workgroups_per_cu_variant(gpu):
     assert tb.update_variant() == 'ppo_update_fs_kernel (NS=16, R=1)'
     tb = TaskBatch('MO-Walker2d-v2', 10, num_processes=4, num_steps=2048)
     assert tb.update_variant() == 'ppo_update_fs_kernel (NS=8, R=2)'
+    tb = TaskBatch('MO-Walker2d-v2', 40, num_processes=4, num_steps=2048)  # config 1: 256 rows over 6 parts
+    assert tb.update_variant() == 'ppo_update_fs_kernel (NS=6, R=3, 2 per CU)'
 
 
-@pytest.mark.parametrize('kernel', ['fs', 'default'])
+@pytest.mark.parametrize('kernel', ['fs', 'default', 'mfma'])
 @pytest.mark.parametrize('env,P,N,mb', [('MO-Walker2d-v2', 5, 4, 256), ('MO-Walker2d-v2', 40, 4, 256),
                                         ('MO-Humanoid-v2', 3, 8, 512)])
 def test_entropy_coef_enters_once(gpu, monkeypatch, kernel, env, P, N, mb):
@@ -97,6 +102,6 @@ def test_entropy_coef_enters_once(gpu, monkeypatch, kernel, env, P, N, mb):
     wide kernel's NS = 4 for Humanoid, fs NS = 16 / 2)."""
     if kernel == 'fs' and env == 'MO-Humanoid-v2':
         pytest.skip('the feature-split update covers obs_dim <= 32')
-    if kernel == 'fs':
-        monkeypatch.setenv('PGM_UPDATE_KERNEL', 'fs')
+    if kernel in ('fs', 'mfma'):  # mfma: the row-split kernels (MODE 2 at P = 40, t16 at P = 5)
+        monkeypatch.setenv('PGM_UPDATE_KERNEL', kernel)
     _check_update(env, P, N, E=1, M=2, mb=mb, seed=43, entropy_coef=0.01)

@@ -141,7 +141,8 @@ constexpr size_t fs_smem_bytes(bool dual) {
 // (Measured and dropped: the parameter hop without a flag -- owners storing every new value as an 8-B {value, tag}
 // granule, readers re-loading a block until all its tags are this step's: P = 5 3.45 vs 2.93 ms, P = 20 5.06 vs 4.38 ms.)
 template <int O, int A, int K, int NS, int R>
-__global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
+// R = 3: held to 256 registers, so that two workgroups share a CU (fs_choose_ns dual; R = 2 fits by itself)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 3 ? 2 : 1))) void ppo_update_fs_kernel(MArgs a) {
     static_assert(O <= 32 && (R == 1 || R == 2 || R == 3 || R == 4 || R == 8), "fs tiles");
     using Sm = FsSmem<O, A, K, R>;
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -620,21 +621,26 @@ __global__ __launch_bounds__(256) void ppo_update_fs_kernel(MArgs a) {
         for (int h = 0; h < NS; ++h) lsum_all += S.red[h];  // part order
         PGM_STAMP(6);
         // ---- 2. reduce-scatter: this part's blocks summed over the NS parts in part order, squared norm
+        // (every fragment load of the wave in flight at once: a block past NB loads from beyond the buffer's range,
+        // which returns zeros, so there is no branch between the batches)
         f32x4 gr_[OWV];
         float sq = 0.f;
+        {
+            u32x4 pl[OWV][NS];
 #pragma unroll
-        for (int i = 0; i < OWV; ++i) {
-            const int b = hs + NS * (w + 4 * i);
-            gr_[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (b < NB) {
-                u32x4 pl[NS];
+            for (int i = 0; i < OWV; ++i) {
+                const int b = hs + NS * (w + 4 * i);
 #pragma unroll
                 for (int h = 0; h < NS; ++h)
-                    pl[h] = __builtin_amdgcn_raw_buffer_load_b128(xr, islot(h, par) + (b * 64 + l) * 16, 0, SC1);
+                    pl[i][h] = __builtin_amdgcn_raw_buffer_load_b128(
+                        xr, b < NB ? islot(h, par) + (b * 64 + l) * 16 : 0x7ffffff0, 0, SC1);
+            }
+#pragma unroll
+            for (int i = 0; i < OWV; ++i) {
 #pragma unroll
                 for (int h = 0; h < NS; ++h) {
-                    const f32x4 v = f32x4{__uint_as_float(pl[h][0]), __uint_as_float(pl[h][1]),
-                                          __uint_as_float(pl[h][2]), __uint_as_float(pl[h][3])};
+                    const f32x4 v = f32x4{__uint_as_float(pl[i][h][0]), __uint_as_float(pl[i][h][1]),
+                                          __uint_as_float(pl[i][h][2]), __uint_as_float(pl[i][h][3])};
                     gr_[i] = h == 0 ? v : gr_[i] + v;
                 }
 #pragma unroll

@@ -1,21 +1,22 @@
-# A/B variants of one source without stamps: bash scripts/build_var.sh <source.hip> <n>... -> pgmorl_amd/libpgm_var<n>.so
+# A/B variant library: libpgm.so with ONE translation unit replaced by another version of it.
+#   bash scripts/build_var.sh NAME UNIT.hip VARIANT_SOURCE   -> pgmorl_amd/libpgm_NAME.so
+# e.g. bash scripts/build_var.sh prev pgm_ppo_fs.hip <(git show HEAD~1:pgmorl_amd/csrc/pgm_ppo_fs.hip)
+# (run python -m pgmorl_amd.build first: the other objects come from pgmorl_amd/build)
 set -e
-src=$1; shift
+name=$1; unit=$2; src=$3
 cd "$(dirname "$0")/.."
-# (run python -m pgmorl_amd.build once beforehand: parallel invocations of this script must not race on it)
-for n in "$@"; do
-  mkdir -p pgmorl_amd/build_var$n
-  objs=""
-  for o in pgmorl_amd/build/*.o; do
-    b=$(basename $o)
-    if [ "$b" = "$src.o" ]; then
-      /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I include -DPGM_EXP=$n $EXTRA -c pgmorl_amd/csrc/$src -o pgmorl_amd/build_var$n/$b &
-      objs="$objs pgmorl_amd/build_var$n/$b"
-    else
-      objs="$objs $o"
-    fi
-  done
-  wait
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $objs -o pgmorl_amd/libpgm_var$n.so
-  echo pgmorl_amd/libpgm_var$n.so
+mkdir -p pgmorl_amd/build_var_$name
+cp "$src" pgmorl_amd/build_var_$name/$unit
+objs=""
+for o in pgmorl_amd/build/*.o; do
+  b=$(basename $o)
+  if [ "$b" = "$unit.o" ]; then
+    /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I include -I pgmorl_amd/csrc $EXTRA \
+        -c pgmorl_amd/build_var_$name/$unit -o pgmorl_amd/build_var_$name/$b
+    objs="$objs pgmorl_amd/build_var_$name/$b"
+  else
+    objs="$objs $o"
+  fi
 done
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $objs -o pgmorl_amd/libpgm_$name.so
+echo pgmorl_amd/libpgm_$name.so

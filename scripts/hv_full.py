@@ -99,7 +99,7 @@ def _oracle_job(job):
             r.mean, r.var, r.count = np.array(val[0], dtype=np.float64), np.array(val[1], dtype=np.float64), float(val[2])
             s.env_params[k] = r
     s0_train = envspec.reset_table(spec['obs_dim'], 0, args.num_processes)
-    s0_eval = envspec.reset_table(spec['obs_dim'], 0, 1)
+    s0_eval = envspec.reset_table(spec['obs_dim'], 0, args.eval_num)
     fn = _draws(args.num_steps, args.num_processes, spec['act_dim'], args.ppo_epoch)
     offs = mopg_worker(args, spec, s0_train, s0_eval, s, np.asarray(w), iteration, num_updates, noise_fn=fn)
     out = []

@@ -1,11 +1,11 @@
 """Parity at the PRODUCTION per-GPU populations of every BASELINE.json config (MI355X, fp32, vs the fp64 CPU
 oracle), with short horizons so the oracle finishes in seconds:
 
-  * MO-Walker2d-v2   P = 40            (config 1: one GPU; the update's MODE-2 grid = 160 co-resident
-                                         workgroups, 4 per task, XCD-paired block map)
-  * MO-HalfCheetah-v2 P = 20           (config 2: pop 160 sharded over 8 GPUs)
-  * MO-Hopper-v3     P = 27, 3 objectives (config 3: pop 210 over 8 GPUs -> blocks of 27 / 26; a ragged
-                                         last group of the MODE-2 grid)
+  * MO-Walker2d-v2   P = 40            (config 1: one GPU; the feature-split update on 6 parts per tower,
+                                         ragged 3 / 3 / 3 / 3 / 2 / 2 row tiles, 480 workgroups two per CU)
+  * MO-HalfCheetah-v2 P = 20           (config 2: pop 160 sharded over 8 GPUs; feature-split, 8 parts, two per CU)
+  * MO-Hopper-v3     P = 27, 3 objectives (config 3: pop 210 over 8 GPUs -> blocks of 27 / 26; a partial last
+                                         group of 8 tasks in the block map; feature-split, 8 parts, two per CU)
   * MO-Humanoid-v2   P = 20, N = 8     (config 4: pop 160 over 8 GPUs; wide update = 80 workgroups,
                                          minibatch 512 rows as in production)
 
@@ -103,10 +103,11 @@ def test_production_rollout_all_tasks(gpu, env, P, N):
 
 @pytest.mark.parametrize('env,P,N', [('MO-Walker2d-v2', 40, 4), ('MO-Hopper-v3', 27, 4), ('MO-Hopper-v2', 5, 1)])
 def test_production_iteration(gpu, env, P, N):
-    """A full MOPG iteration (rollout, GAE, advantages, the update kernel the launcher picks for this P -- MODE 2
-    for Walker P = 40, 16-row tiles on four workgroups per tower for Hopper-v3 P = 27 and config 0's Hopper-v2
-    P = 5 -- and the evaluation) at the production population with the reference's RNG draws; tasks spread
-    over the grid vs the oracle MOPG_worker (morl/mopg.py:60-182)."""
+    """A full MOPG iteration (rollout, GAE, advantages, the update kernel the launcher picks for this P -- the
+    feature-split update on 6 parts per tower for Walker P = 40 (mb = 256: ragged 3 / 3 / 3 / 3 / 2 / 2 row tiles), on 8
+    parts two per CU for Hopper-v3 P = 27, on 4 parts for config 0's Hopper-v2 P = 5 (mb = 64) -- and the
+    evaluation) at the production population with the reference's RNG draws; tasks spread over the grid vs the
+    oracle MOPG_worker (morl/mopg.py:60-182)."""
     T, E, M = 64, 1, 1  # one production-size minibatch (mb = T * N: 256 rows, config 0's N = 1: 64), one Adam step
     args = small_args(env, num_steps=T, num_processes=N, ppo_epoch=E, num_mini_batch=M, num_env_steps=T * N * 10)
     spec = envspec.make_spec(env)
@@ -173,8 +174,8 @@ def test_production_eval_all_tasks(gpu, env, P, eval_num):
 
 
 def test_config0_full_iteration_shape(gpu):
-    """Config 0 at its real shape -- Hopper-v2, P = 5, N = 1, T = 2048, M = 32 (minibatch 64: the t16 path with
-    one 16-row tile per row part, not the single-tile specialisation), two epochs -- one launch of pgm_ppo_update
+    """Config 0 at its real shape -- Hopper-v2, P = 5, N = 1, T = 2048, M = 32 (minibatch 64: the feature-split update
+    on 4 parts per tower, one 16-row tile each), two epochs -- one launch of pgm_ppo_update
     for every task vs the oracle, then a full TaskBatch.iteration (rollout of 2,048 steps, GAE, advantages, that
     update, evaluation) for every task vs oracle.mopg.mopg_worker (scripts/hopper-v2.py:38, morl/mopg.py:60-182)."""
     env, P, N, T, E, M = 'MO-Hopper-v2', 5, 1, 2048, 2, 32

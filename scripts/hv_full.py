@@ -174,8 +174,11 @@ class OracleMOPG:
                   for k, r in (t.sample.env_params or {}).items()}
             jobs.append((a, sn.params.double().numpy(), sn.adam_m.double().numpy(), sn.adam_v.double().numpy(),
                          sn.adam_step, ep, t.scalarization.weights.numpy(), iteration, num_updates))
+        t0 = time.time()
         with mp.get_context('fork').Pool(min(self.procs, max(1, len(jobs)))) as pool:
             res = pool.map(_oracle_job, jobs)
+        print(f'oracle generation: {len(jobs)} tasks x {num_updates} iterations from {iteration}, '
+              f'{time.time() - t0:.0f} s', file=sys.stderr, flush=True)
         offspring = []
         for task_res in res:
             offs = []
@@ -211,6 +214,8 @@ def main():
     ap.add_argument('--ref', help='oracle JSON (device side)')
     ap.add_argument('--out', required=True)
     a = ap.parse_args()
+    if a.side != 'device':
+        torch.set_num_threads(1)  # the host loop's own torch work (the warm-up evaluation): the pool has the cores
     if a.side == 'oracle_f32':  # before anything imports oracle.mopg (the pool workers fork from this process)
         os.environ['PGM_ORACLE_NET_DTYPE'] = 'float32'
     if a.ref:

@@ -168,7 +168,8 @@ def cpu_baseline(args, spec, tasks):
 def hv_comparison(env_name):
     """The newest committed full-algorithm device-vs-oracle HV comparison at an equal budget for this env
     (scripts/hv_full.py: warm-up + prediction-guided generations on both sides, per seed), summarised."""
-    key = {'MO-Walker2d-v2': 'walker', 'MO-Hopper-v2': 'hopper', 'MO-Hopper-v3': 'hopper3'}.get(env_name)
+    key = {'MO-Walker2d-v2': 'walker', 'MO-Hopper-v2': 'hopper', 'MO-Hopper-v3': 'hopper3',
+           'MO-Humanoid-v2': 'humanoid'}.get(env_name)
     if key is None:
         return None
     import re
@@ -182,10 +183,14 @@ def hv_comparison(env_name):
             continue
         d, o = json.load(open(dev)), json.load(open(orc))
         ho = {r['seed']: r['hv'] for r in o['runs']}
-        rel = [(r['hv'] - ho[r['seed']]) / ho[r['seed']] for r in d['runs'] if r['seed'] in ho]
-        if not rel:
+        pairs = [(r['hv'], ho[r['seed']]) for r in d['runs'] if r['seed'] in ho]
+        if not pairs:
             continue
-        rel = np.array(rel)
+        hd_, ho_ = np.array(pairs).T
+        # per-seed relative difference; when an oracle seed ends with an empty archive (HV 0: no point with every
+        # objective >= 0 at this budget, Humanoid), every difference is taken relative to the oracle's mean HV
+        scale = ho_ if (ho_ > 0).all() else np.full_like(ho_, ho_.mean())
+        rel = (hd_ - ho_) / scale
         half = None
         if len(rel) > 1:  # Student-t 95% interval of the mean per-seed difference
             from scipy import stats
@@ -193,7 +198,10 @@ def hv_comparison(env_name):
         return {'source': [os.path.relpath(dev, ROOT), os.path.relpath(orc, ROOT)], 'config': d.get('config'),
                 'seeds': len(rel), 'hv_rel_diff_per_seed': [float(x) for x in rel],
                 'hv_rel_diff_mean': float(rel.mean()), 'ci95_half_width': half,
-                'within_1pct_at_95': None if half is None else bool(abs(rel.mean()) + half < 0.01)}
+                'within_1pct_at_95': None if half is None else bool(abs(rel.mean()) + half < 0.01),
+                'hv_mean': {'device': float(hd_.mean()), 'oracle': float(ho_.mean())},
+                'empty_archive_seeds': {'device': int((hd_ == 0).sum()), 'oracle': int((ho_ == 0).sum())},
+                'normalised_by': 'per-seed oracle HV' if (ho_ > 0).all() else 'mean oracle HV'}
     return None
 
 

@@ -345,16 +345,17 @@ def launch_ranks(n):
         procs.append(subprocess.Popen([sys.executable, '-u', os.path.abspath(__file__), *sys.argv[1:]], env=env))
     rc, t_fail, live = 0, None, list(procs)
     while live:
-        for p in list(live):
-            c = p.poll()
-            if c is None:
-                continue
+        done = [(p, p.poll()) for p in live]
+        done = [(p, c) for p, c in done if c is not None]
+        for p, _ in done:
             live.remove(p)
-            if c != 0 and rc == 0:
-                rc, t_fail = (c if c > 0 else 1), time.time()
-                print(f'bench.py: rank {procs.index(p)} exited with {c}; stopping the other ranks', file=sys.stderr)
-                for q in live:
-                    q.terminate()
+        failed = [(procs.index(p), c) for p, c in done if c != 0]
+        if failed and rc == 0:  # every rank found failed in the same sweep is named (a peer may exit in the same 0.1 s)
+            rc, t_fail = (failed[0][1] if failed[0][1] > 0 else 1), time.time()
+            for r, c in failed:
+                print(f'bench.py: rank {r} exited with {c}; stopping the other ranks', file=sys.stderr)
+            for q in live:
+                q.terminate()
         if t_fail is not None and time.time() - t_fail > 30:
             for q in live:
                 q.kill()

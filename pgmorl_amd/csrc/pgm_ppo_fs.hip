@@ -42,9 +42,13 @@ PGM_STAMP_UNIT(fs)
 namespace pgm {
 
 // ---------------------------------------------------------------- geometry shared by host and device
-// gradient / parameter fragments of one tower: per wave w (feature block w) K1B dW1 blocks, 4 dW2 blocks, 1 head
-// block, 1 vector block (b1, b2 and, wave 0, head bias / logstd)
-constexpr int fs_bpw(int O) { return (O + 15) / 16 + 6; }
+// gradient / parameter fragments of one tower: per wave w (feature block w) K1M dW1 blocks, 4 dW2 blocks, 1 head
+// block, 1 vector block (b1, b2 and, wave 0, head bias / logstd). Compact form (obs_dim <= 20, <= 8 head columns):
+// the head block's free lanes (columns 8..15) carry the vector block and dW1 input rows 16..19, so a wave exchanges
+// 6 blocks instead of 7 / 8 (a quarter fewer bytes per hand-off at obs_dim 17)
+constexpr bool fs_compact(int O) { return O <= 20; }
+constexpr int fs_k1m(int O) { return fs_compact(O) ? 1 : (O + 15) / 16; }
+constexpr int fs_bpw(int O) { return fs_k1m(O) + (fs_compact(O) ? 5 : 6); }
 constexpr int fs_nb(int O) { return 4 * fs_bpw(O); }
 constexpr int fs_nown(int O, int NS) { return (fs_nb(O) + NS - 1) / NS; }  // blocks per owner (max)
 // parameter-slot positions a part writes: every wave publishes the same number of blocks (ceil(NOWN / 4)), past NOWN
@@ -81,19 +85,45 @@ size_t fs_workspace_extra(const pgm_dims* d) {
     return fs_payload_bytes(d->P, d->O, 16);
 }
 
+// compact head block, column c of feature block wb: entry v (= 4 g + r) at image index base + v for v < lim -- head
+// column c (c < 8), b1, b2, head bias, logstd (8..11), dW1 input 16 + (c - 12) (12..15)
+template <int O, int A, int K>
+__device__ __forceinline__ void cpt_column(int c, int wb, int m, int& base, int& lim) {
+    constexpr int Q = qmax<A, K>();
+    constexpr int oW2 = O * H, oWh = oW2 + H * SCR, oB1 = oWh + Q * H, oB2 = oB1 + H, oBh = oB2 + H, oLs = oBh + Q;
+    const int NQ = m == 0 ? K : A, in = 16 + c - 12;
+    base = c < 8 ? oWh + c * H + 16 * wb
+         : c == 8 ? oB1 + 16 * wb
+         : c == 9 ? oB2 + 16 * wb
+         : c == 10 ? oBh
+         : c == 11 ? oLs
+                   : in * H + 16 * wb;
+    lim = c < 8 ? (c < NQ ? 16 : 0)
+        : c < 10 ? 16
+        : c == 10 ? (wb == 0 ? NQ : 0)
+        : c == 11 ? (wb == 0 && m == 1 ? A : 0)
+                  : (in < O ? 16 : 0);
+}
+
 // fragment slot (block b, lane l, register r) -> tower image index (TowerImg), -1 for padding
 template <int O, int A, int K>
 __device__ __forceinline__ int frag_img(int b, int l, int r, int m) {
-    constexpr int Q = qmax<A, K>(), K1B = (O + 15) / 16, BPW = fs_bpw(O);
+    constexpr int Q = qmax<A, K>(), K1M = fs_k1m(O), BPW = fs_bpw(O);
     constexpr int oW2 = O * H, oWh = oW2 + H * SCR, oB1 = oWh + Q * H, oB2 = oB1 + H, oBh = oB2 + H, oLs = oBh + Q;
+    static_assert(!fs_compact(O) || Q <= 8, "compact fragments: head columns 0..7 only");
     const int wb = b / BPW, k = b - wb * BPW, g = l >> 4, c = l & 15;
     const int NQ = m == 0 ? K : A;
-    if (k < K1B) {
+    if (k < K1M) {
         const int in = 16 * k + 4 * g + r;
         return in < O ? in * H + 16 * wb + c : -1;
     }
-    if (k < K1B + 4) return oW2 + (16 * (k - K1B) + 4 * g + r) * SCR + 16 * wb + c;
-    if (k == K1B + 4) return c < NQ ? oWh + c * H + 16 * wb + 4 * g + r : -1;
+    if (k < K1M + 4) return oW2 + (16 * (k - K1M) + 4 * g + r) * SCR + 16 * wb + c;
+    if (k == K1M + 4) {
+        if (!fs_compact(O)) return c < NQ ? oWh + c * H + 16 * wb + 4 * g + r : -1;
+        int base, lim;
+        cpt_column<O, A, K>(c, wb, m, base, lim);
+        return 4 * g + r < lim ? base + 4 * g + r : -1;
+    }
     if (g != 0) return -1;
     if (r == 0) return oB1 + 16 * wb + c;
     if (r == 1) return oB2 + 16 * wb + c;
@@ -127,7 +157,8 @@ struct FsSmem {
     alignas(16) float Zs[ZA ? 1 : SB][SF];                     // dZ2
     alignas(16) float H1T[HT ? H : 1][STT];                    // H1 transposed (R <= 4)
     float dOs[SB][DQS];                                        // dL/d(head output), transposed for dH2
-    float HP[NHP][SB][DQS];                                    // R < 4: the waves' partial head outputs
+    alignas(16) float HP[NHP][SB][DQS];                        // R < 4: the waves' partial head outputs (after B3:
+                                                               // the waves' compact head-block staging, 128 floats each)
     float aiv[A];                                              // actor 1 / std^2
     float red[192];  // [0, 64) head-bias partials / poll results, [64, 128) logstd partials / norms, 128+ loss sums
 };
@@ -152,7 +183,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 3 ? 2 
     constexpr int KS1 = (O + 3) / 4, K1B = (O + 15) / 16;
     constexpr int IMG = img_floats<O, A, K>(), RS = Sm::RS, RSL = Sm::RSL, SB = Sm::SB, NDT = Sm::NDT;
     constexpr int CR = RS / 4;
-    constexpr int BPW = fs_bpw(O), NB = fs_nb(O), NOWN = fs_nown(O, NS);
+    constexpr int BPW = fs_bpw(O), NB = fs_nb(O), NOWN = fs_nown(O, NS), K1M = fs_k1m(O);
+    constexpr bool CPT = fs_compact(O);
+    constexpr int KV = K1M + (CPT ? 4 : 5);  // the block b1 lives in (compact: the head block)
+    static_assert(!CPT || Sm::NHP * Sm::SB * DQS >= 512, "compact head-block staging: 128 floats per wave");
     constexpr int OWV = (NOWN + 3) / 4;  // owned blocks per wave (block j of the part: wave j mod 4)
     constexpr int ISB = NB * 1024, PSB = fs_pslots(O, NS) * 1024;
     constexpr bool HSPLIT = R >= 4;      // heads: row tiles split over the waves (else units + samples split)
@@ -226,13 +260,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 3 ? 2 
     }
     if (t < A) S.aiv[t] = expf(-2.f * P[L.off[PGM_P_LOGSTD] + t]);
     // parameters + moments of this part's own blocks b = hs + NS j (block j of the part: wave j mod 4)
+    // (their image indices, fixed for the launch, stay in registers: the Adam writes and the write-back reuse them)
     f32x4 op[OWV], om[OWV], ov[OWV];
+    int oix[OWV][4];
 #pragma unroll
     for (int i = 0; i < OWV; ++i) {
         const int b = hs + NS * (w + 4 * i);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int ii = b < NB ? frag_img<O, A, K>(b, l, r, m) : -1;
+            int ii = b < NB ? frag_img<O, A, K>(b, l, r, m) : -1;
+            asm volatile("" : "+v"(ii));
+            oix[i][r] = ii;
             const int f = ii >= 0 ? img_to_flat<O, A, K>(ii, m, L) : -1;
             op[i][r] = f >= 0 ? P[f] : 0.f;
             om[i][r] = f >= 0 ? Mo[f] : 0.f;
@@ -262,12 +300,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 3 ? 2 
     // layer 1, W2 before layer 2, the head block before B2 (heads read every wave's); the own part's blocks are
     // written by their owners before the parameter hand-off
     u32x4 pv[BPW];
+    // compact head block of this wave: entry v = 4 g + r of the lane's column at kvb + v for v < kvl (frag_img)
+    int kvb = 0, kvl = 0;
+    if constexpr (CPT) {
+        cpt_column<O, A, K>(c, w, m, kvb, kvl);
+        asm volatile("" : "+v"(kvb), "+v"(kvl));
+    }
     auto put_block = [&](int k) {  // (the own part's blocks rewrite the values their owners already wrote)
-        const int b = BPW * w + k;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int ii = frag_img<O, A, K>(b, l, r, m);
-            if (ii >= 0) Pf[ii] = __uint_as_float(pv[k][r]);
+            const float v = __uint_as_float(pv[k][r]);
+            if (k < K1M) {  // dW1 rows 16 k + 4 g + r, this wave's features
+                const int in = 16 * k + 4 * g + r;
+                if (in < O) Pf[in * H + fb + c] = v;
+            } else if (k < K1M + 4) {  // dW2 rows 16 (k - K1M) + 4 g + r
+                Pf[oW2 + (16 * (k - K1M) + 4 * g + r) * SCR + fb + c] = v;
+            } else if (CPT) {  // the compact head block: launch-fixed column base / limit
+                if (4 * g + r < kvl) Pf[kvb + 4 * g + r] = v;
+            } else {
+                const int ii = frag_img<O, A, K>(BPW * w + k, l, r, m);
+                if (ii >= 0) Pf[ii] = v;
+            }
         }
     };
     auto pload = [&](int k, int par_) {
@@ -282,8 +335,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 3 ? 2 
         // ================================================================ tiles
         if (gp > 0) {
 #pragma unroll
-            for (int k = 0; k < K1B; ++k) put_block(k);
-            put_block(K1B + 5);
+            for (int k = 0; k < K1M; ++k) put_block(k);
+            put_block(KV);
             if (m == 1 && w == 0 && l < A) S.aiv[l] = expf(-2.f * Wt.logstd[l]);  // read in the heads, after B2
         }
         // ---- layer 1: Z1[s][fb + c] over the inputs (A = X rows, B = W1t, shared by the tiles)
@@ -320,7 +373,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 3 ? 2 
         PGM_STAMP(0);
         if (gp > 0) {
 #pragma unroll
-            for (int k = K1B; k < K1B + 5; ++k) put_block(k);
+            for (int k = K1M; k < K1M + (CPT ? 4 : 5); ++k) put_block(k);
         }
         PGM_STAMP(11);
         lds_sync_m();  // B1: H1 of every feature block (and every wave's head block)
@@ -526,8 +579,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 3 ? 2 
             __builtin_amdgcn_raw_buffer_store_b128(u, xr, islot(hs, par) + ((w * BPW + k) * 64 + l) * 16, 0, SC1);
         };
 #pragma unroll
-        for (int ib = 0; ib < 4; ++ib) pub(K1B + ib, gW2[ib]);
-        pub(K1B + 4, gWh);
+        for (int ib = 0; ib < 4; ++ib) pub(K1M + ib, gW2[ib]);
+        if (!CPT || c < 8) pub(K1M + 4, gWh);  // (compact: the head columns now, the rest of the block at the end)
         PGM_STAMP(3);
         lds_sync_m();  // B3: dZ2 of every feature block
         // ---- dH1 = dZ2 W2 for this wave's input block, dZ1, dW1^T[k][fb + c] += X^T dZ1
@@ -580,11 +633,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 3 ? 2 
                 // -entropy_coef * d(mean entropy)/d logstd enters once per tower (ppo.py:98): part 0
                 if (hs == 0) vls -= a.hp.entropy_coef;
             }
-            const f32x4 vec = g == 0 ? f32x4{gB1, gB2, c < NQ ? vb2 : 0.f, m == 1 && c < A ? vls : 0.f}
-                                     : f32x4{0.f, 0.f, 0.f, 0.f};
+            if constexpr (CPT) {
+                pub(0, gW1[0]);
+                // the head block's columns 8..15 through LDS (the head partials are dead after B3): lane v writes entry
+                // v of b1 / b2 / head bias / logstd and dW1 inputs 16..19 of feature v (register j of block 1) to
+                // column 8 + kind, row v; lane (g, c >= 8) reads rows 4 g .. 4 g + 3 of column c
+                float* hs_ = &S.HP[0][0][0] + 128 * w;
+                if (l < 16) {
+                    hs_[l] = gB1;
+                    hs_[16 + l] = gB2;
+                    hs_[32 + l] = c < NQ ? vb2 : 0.f;
+                    hs_[48 + l] = m == 1 && c < A ? vls : 0.f;
 #pragma unroll
-            for (int kb = 0; kb < K1B; ++kb) pub(kb, gW1[kb]);
-            pub(K1B + 5, vec);
+                    for (int j = 0; j < 4; ++j) hs_[64 + 16 * j + l] = K1B == 2 ? gW1[K1B - 1][j] : 0.f;
+                }
+                const float4 h4 = *reinterpret_cast<const float4*>(&hs_[16 * (c - 8 < 0 ? 0 : c - 8) + 4 * g]);
+                const f32x4 hv = f32x4{h4.x, h4.y, h4.z, h4.w};
+                if (c >= 8) pub(K1M + 4, hv);
+            } else {
+                const f32x4 vec = g == 0 ? f32x4{gB1, gB2, c < NQ ? vb2 : 0.f, m == 1 && c < A ? vls : 0.f}
+                                         : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int kb = 0; kb < K1B; ++kb) pub(kb, gW1[kb]);
+                pub(K1M + 5, vec);
+            }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
         lds_sync_m();
@@ -704,10 +776,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 3 ? 2 
                     op[i][r] = pp;
                 }
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int ii = frag_img<O, A, K>(b, l, r, m);
-                    if (ii >= 0) Pf[ii] = op[i][r];
-                }
+                for (int r = 0; r < 4; ++r)
+                    if (oix[i][r] >= 0) Pf[oix[i][r]] = op[i][r];
             }
             // the part's owned block w + 4 i (slot position always valid: blocks past NB publish unused values, so every
             // wave issues the same number of stores)
@@ -739,7 +809,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 3 ? 2 
         if (b < NB) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int ii = frag_img<O, A, K>(b, l, r, m);
+                const int ii = oix[i][r];
                 const int f = ii >= 0 ? img_to_flat<O, A, K>(ii, m, L) : -1;
                 if (f >= 0) {
                     P[f] = op[i][r];

@@ -119,7 +119,8 @@ def test_update_workspace_covers_every_split(env, P, N, T):
     from granule 16 P + 8 the feature-split update's [3 kinds][P][2 towers][<= 16 parts][2 parities]; 256-B padded),
     exchange slots [P][2 towers][4 parts][2 parities], and the packed sample table + the feature-split payload
     (obs_dim <= 32: [P][2][NS][2] image slots of NB KiB and parameter slots of 4 ceil(ceil(NB / NS) / 4) KiB, NS = 16,
-    the largest a launch with P' <= P tasks may pick, NB = 4 (ceil(O / 16) + 6)) or the parts' private parameter
+    the largest a launch with P' <= P tasks may pick, NB = 4 x 6 blocks for obs_dim <= 20 (compact fragments), else
+    4 (ceil(O / 16) + 6)) or the parts' private parameter
     rows (wide)."""
     from pgmorl_amd import envspec
     spec = envspec.make_spec(env)
@@ -134,7 +135,7 @@ def test_update_workspace_covers_every_split(env, P, N, T):
         n = O + A + 2 + 2 * K
         rs = 16 if n <= 16 else 32 if n <= 32 else 64 if n <= 64 else 128
         ns = 16
-        nb = 4 * (-(-O // 16) + 6)
+        nb = 4 * (6 if O <= 20 else -(-O // 16) + 6)
         fs = P * 2 * ns * 2 * (nb + 4 * -(-(-(-nb // ns)) // 4)) * 1024
         want = flags + P * 2 * 4 * 2 * xslot * 8 + P * T * N * rs * 4 + fs
     else:
@@ -153,7 +154,7 @@ def _fs_need(P, O):
     ns = 16
     while ns > 1 and 16 * ns * -(-P // 8) > 512:
         ns //= 2
-    nb = 4 * (-(-O // 16) + 6)
+    nb = 4 * (6 if O <= 20 else -(-O // 16) + 6)
     return P * 2 * ns * 2 * (nb + 4 * -(-(-(-nb // ns)) // 4)) * 1024 if ns >= 2 else 0
 
 

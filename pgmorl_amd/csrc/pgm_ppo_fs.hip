@@ -345,8 +345,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 3 ? 2 
         for (int ti = 0; ti < R; ++ti)
 #pragma unroll
             for (int q = 0; q < NC; ++q) z[ti][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+        // (compact: inputs 16.. -- at most 4, one mostly-padding k-step -- on the VALU, added below)
+        constexpr int KS1M = fs_compact(O) && O > 16 ? 4 : KS1, NT1 = KS1M < KS1 ? O - 16 : 0;
 #pragma unroll
-        for (int ks = 0; ks < KS1; ++ks) {
+        for (int ks = 0; ks < KS1M; ++ks) {
             const int k = 4 * ks + g;
             const bool kv = k < O;
             const float bw = kv ? Wt.W1t[kv ? k : 0][fb + c] : 0.f;
@@ -355,6 +357,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 3 ? 2 
                 const float av = kv ? rt(ti)[c * RSL + (kv ? k : 0)] : 0.f;
                 z[ti][ks % NC] = mfma16(av, bw, z[ti][ks % NC]);
             }
+        }
+        if constexpr (NT1 > 0) {  // z[sample 4 g + r][feature c] += X[sample][16 + j] W1t[16 + j][fb + c]
+            float w16[NT1 > 0 ? NT1 : 1];
+#pragma unroll
+            for (int j = 0; j < NT1; ++j) w16[j] = Wt.W1t[16 + j][fb + c];
+#pragma unroll
+            for (int ti = 0; ti < R; ++ti)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float* xr16 = rt(ti) + (4 * g + r) * RSL + 16;
+#pragma unroll
+                    for (int j = 0; j < NT1; ++j) z[ti][0][r] = fmaf(xr16[j], w16[j], z[ti][0][r]);
+                }
         }
         {
             const float bias = Wt.b1[fb + c];
@@ -526,12 +541,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 3 ? 2 
         PGM_STAMP(2);
         lds_sync_m();  // B2b: the dO tile of every wave's rows / samples (and, R = 8, H2 reads done before dZ2)
         // ---- head-weight gradient gWh^T[u][q] += H2^T dO, dH2 = dO . Wh -> dZ2 (this wave's units)
-        f32x4 gWh = f32x4{0.f, 0.f, 0.f, 0.f}, gW2[4], gW1[K1B];
+        // (compact: dW1 inputs 16.. (at most 4, mostly padding in a 16-row MFMA block) on the VALU: gT[j] = input 16 + j)
+        constexpr int K1G = CPT ? K1M : K1B, NT = CPT && O > 16 ? O - 16 : 0;
+        f32x4 gWh = f32x4{0.f, 0.f, 0.f, 0.f}, gW2[4], gW1[K1G];
+        float gT[NT > 0 ? NT : 1] = {};
         float gB1 = 0.f, gB2 = 0.f;
 #pragma unroll
         for (int ib = 0; ib < 4; ++ib) gW2[ib] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int kb = 0; kb < K1B; ++kb) gW1[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int kb = 0; kb < K1G; ++kb) gW1[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
         const float* dtl = &S.dOs[0][0];
         float (*Zt)[SF] = Sm::ZA ? S.H2s : S.Zs;
         f32x4 dZ2[R];
@@ -610,14 +628,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 3 ? 2 
             for (int r = 0; r < 4; ++r) {
                 gB1 += dZ1[r];
 #pragma unroll
-                for (int kb = 0; kb < K1B; ++kb) {
+                for (int kb = 0; kb < K1G; ++kb) {
                     const int k = 16 * kb + c;
                     const float ax = k < O ? rt(ti)[(4 * g + r) * RSL + (k < O ? k : 0)] : 0.f;
                     gW1[kb] = mfma16(ax, dZ1[r], gW1[kb]);
                 }
+                if constexpr (NT > 0) {  // this lane group's 4 samples; the groups are summed after the tiles
+                    const float* xr16 = rt(ti) + (4 * g + r) * RSL + 16;
+#pragma unroll
+                    for (int j = 0; j < NT; ++j) gT[j] = fmaf(xr16[j], dZ1[r], gT[j]);
+                }
             }
         }
         gB1 = group4_sum(gB1);
+#pragma unroll
+        for (int j = 0; j < NT; ++j) gT[j] = group4_sum(gT[j]);
         gB2 = group4_sum(gB2);
         PGM_STAMP(4);
 
@@ -636,7 +661,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 3 ? 2 
             if constexpr (CPT) {
                 pub(0, gW1[0]);
                 // the head block's columns 8..15 through LDS (the head partials are dead after B3): lane v writes entry
-                // v of b1 / b2 / head bias / logstd and dW1 inputs 16..19 of feature v (register j of block 1) to
+                // v of b1 / b2 / head bias / logstd and dW1 inputs 16..19 of feature v (gT) to
                 // column 8 + kind, row v; lane (g, c >= 8) reads rows 4 g .. 4 g + 3 of column c
                 float* hs_ = &S.HP[0][0][0] + 128 * w;
                 if (l < 16) {
@@ -645,7 +670,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 3 ? 2 
                     hs_[32 + l] = c < NQ ? vb2 : 0.f;
                     hs_[48 + l] = m == 1 && c < A ? vls : 0.f;
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) hs_[64 + 16 * j + l] = K1B == 2 ? gW1[K1B - 1][j] : 0.f;
+                    for (int j = 0; j < 4; ++j) hs_[64 + 16 * j + l] = j < NT ? gT[j < NT ? j : 0] : 0.f;
                 }
                 const float4 h4 = *reinterpret_cast<const float4*>(&hs_[16 * (c - 8 < 0 ? 0 : c - 8) + 4 * g]);
                 const f32x4 hv = f32x4{h4.x, h4.y, h4.z, h4.w};

@@ -409,6 +409,7 @@ class EPFileCache:
             blocks = layout.unflatten_batch(flats) if sdw.ok else None
             sds = None if blocks is not None else [layout.unflatten(f) for f in flats]
             envs = [smp.env_params for _, smp in new]
+            smps = [smp for _, smp in new]
             paths = [self._paths(uid) for uid, _ in new]
             for (uid, _), pp in zip(new, paths):
                 self.files[uid] = pp
@@ -422,6 +423,7 @@ class EPFileCache:
                         sdw.save(sds[i], pt)
                     with open(pkl, 'wb') as fp:
                         pickle.dump(envs[i], fp)
+                    smps[i]._env_line = _env_params_line(envs[i])  # env_params.txt's line, ahead too
             self.writer.submit(job)
         if gone:
             def drop():
@@ -447,6 +449,12 @@ class EPFileCache:
         import shutil
         shutil.rmtree(self.dir, ignore_errors=True)
         self.files.clear()
+
+
+def _env_params_line(env_params):
+    """One line of final/env_params.txt (morl/morl.py:236-239): numpy's own str() of obj_rms mean / var."""
+    r = env_params.get('obj_rms') if env_params else None
+    return None if r is None else 'obj_rms: mean: {} var: {}\n'.format(r.mean, r.var)
 
 
 def write_final(args, ep, cache=None):
@@ -500,4 +508,5 @@ def write_final(args, ep, cache=None):
     if args.obj_rms:
         with open(os.path.join(final, 'env_params.txt'), 'w') as fp:
             for s in ep.sample_batch:
-                fp.write('obj_rms: mean: {} var: {}\n'.format(s.env_params['obj_rms'].mean, s.env_params['obj_rms'].var))
+                line = getattr(s, '_env_line', None)  # (formatted on the writer thread by EPFileCache)
+                fp.write(line if line is not None else _env_params_line(s.env_params))

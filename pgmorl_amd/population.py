@@ -287,12 +287,12 @@ class Population2d(_PopulationBase):
         center = opt_graph.weights[node]
         ac = np.arctan2(center[1], center[0])
         lo, hi = ac - np.pi / 4., ac + np.pi / 4.
-        succ_w = [opt_graph.weights[s] / np.linalg.norm(opt_graph.weights[s]) for s in opt_graph.succ[node]]
+        succ_w = _rows([opt_graph.weights[s] / np.linalg.norm(opt_graph.weights[s]) for s in opt_graph.succ[node]], 2)
         out = []
         for i in range(num_weights):
             angle = lo + (hi - lo) / (num_weights - 1) * i
             w = np.array([np.cos(angle), np.sin(angle)])
-            if w[0] >= -1e-7 and w[1] >= -1e-7 and not any(np.linalg.norm(s - w) < 1e-3 for s in succ_w):
+            if w[0] >= -1e-7 and w[1] >= -1e-7 and not _taken(succ_w, w):
                 out.append(w)
         return out
 
@@ -345,9 +345,9 @@ class Population3d(_PopulationBase):
         num_weights = args.num_weight_candidates
         center = opt_graph.weights[node] / np.sum(opt_graph.weights[node])
         grid = weight_grid(args.obj_num, args.delta_weight / 2.0)
-        succ_w = [opt_graph.weights[s] / np.sum(opt_graph.weights[s]) for s in opt_graph.succ[node]]
+        succ_w = _rows([opt_graph.weights[s] / np.sum(opt_graph.weights[s]) for s in opt_graph.succ[node]], args.obj_num)
         out = []
-        if not any(np.linalg.norm(s - center) < 1e-3 for s in succ_w):
+        if not _taken(succ_w, center):
             out.append(center)
         idx = np.array([i for i in range(len(grid))])
         np.random.shuffle(idx)
@@ -359,9 +359,22 @@ class Population3d(_PopulationBase):
             if np.linalg.norm(w - center) < 1e-3:
                 continue
             angle = np.arccos(np.clip(np.dot(center, w) / cn / np.linalg.norm(w), -1.0, 1.0))
-            if angle < np.pi / 4.0 and not any(np.linalg.norm(s - w) < 1e-3 for s in succ_w):
+            if angle < np.pi / 4.0 and not _taken(succ_w, w):
                 out.append(w)
         return out
+
+
+def _rows(ws, k):
+    return np.array(ws, dtype=np.float64).reshape(-1, k)
+
+
+def _taken(succ_w, w):
+    """any(np.linalg.norm(s - w) < 1e-3 for s in succ_w) over the rows at once (population_2d.py:253-255,
+    population_3d.py:270-283): the direction w was already taken from this node."""
+    if not len(succ_w):
+        return False
+    d = succ_w - w
+    return bool(np.any(np.sqrt((d * d).sum(axis=1)) < 1e-3))
 
 
 def make_population(args):

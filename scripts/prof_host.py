@@ -17,7 +17,7 @@ import torch  # noqa: E402
 from pgmorl_amd.layout import ParamLayout  # noqa: E402
 from pgmorl_amd.morl import run as morl_run  # noqa: E402
 from pgmorl_amd.run import get_parser, merge_argv  # noqa: E402
-from pgmorl_amd.sample import DeviceSnapshot, RunningMeanStd, Sample  # noqa: E402
+from pgmorl_amd.sample import DeviceSnapshot, RowStore, RunningMeanStd, Sample  # noqa: E402
 
 
 class StandIn:
@@ -44,7 +44,7 @@ class StandIn:
         total = int(a.num_env_steps) // a.num_steps // a.num_processes
         I = len(range(iteration, min(iteration + num_updates, total)))
         P = len(task_batch)
-        arena = torch.zeros(I, 3, P, self.lay.total)
+        arena = RowStore(torch.zeros(I, 3, P, self.lay.total), 'arena')
         out = []
         for p, t in enumerate(task_batch):
             w = t.scalarization.weights.numpy()

@@ -402,12 +402,12 @@ class EPFileCache:
         gone = [self.files.pop(u) for u in [u for u in self.files if u not in live]]
         if new:
             layout = new[0][1].snapshot.layout
-            flats = torch.stack([smp.snapshot.params for _, smp in new])
+            # the new members' flat parameters in ONE device->host copy; the per-key fp64 / transposed blocks are
+            # made from it on the writer thread (numpy, the same values as the device conversion)
+            flats = torch.stack([smp.snapshot.params for _, smp in new]).cpu().numpy()
             if self.sdw is None:
                 self.sdw = _StateDictWriter(layout.unflatten(flats[0]))
             sdw = self.sdw  # (its template was verified when it was built: the path chosen here is final)
-            blocks = layout.unflatten_batch(flats) if sdw.ok else None
-            sds = None if blocks is not None else [layout.unflatten(f) for f in flats]
             envs = [smp.env_params for _, smp in new]
             smps = [smp for _, smp in new]
             paths = [self._paths(uid) for uid, _ in new]
@@ -416,6 +416,8 @@ class EPFileCache:
 
             def job():
                 os.makedirs(self.dir, exist_ok=True)
+                blocks = layout.unflatten_batch(flats) if sdw.ok else None
+                sds = None if blocks is not None else [layout.unflatten(f) for f in flats]
                 for i, (pt, pkl) in enumerate(paths):
                     if blocks is not None:
                         sdw.save_records([b[i] for b in blocks], pt)

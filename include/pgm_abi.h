@@ -206,6 +206,11 @@ int pgm_ppo_update_variant(const pgm_dims* d, const pgm_ppo_hparams* hp, char* b
  * and let that call skip its own reset (the caller orders this stream before the update's stream and after
  * every read of the previous update's timeout word).  Lets a caller take the reset off the update's stream. */
 int pgm_ppo_update_reset(const pgm_dims* d, void* workspace, pgm_stream_t stream);
+/* The feature-split update's fragment map (diagnostic, no reference counterpart): for tower m (0 critic, 1 actor)
+ * of dims (O, A, K), O <= 32, out[(b * 64 + l) * 4 + r] = the tower-image index the kernel keeps in register r of
+ * lane l of exchange block b (-1: padding), for every block b < NB; returns NB or a negative status (cap = out's
+ * length in entries, >= 256 NB).  Host-only, no device work. */
+int pgm_ppo_fs_fragment_map(int32_t O, int32_t A, int32_t K, int32_t m, int32_t* out, int32_t cap);
 
 /* evaluation(): eval_num deterministic episodes per task from s0_eval [eval_num][O], obs normalised
  * with the snapshot ob_mean/ob_var [P][O] (use_ob_rms), objs_out [P][K] fp64 (discounted by gamma

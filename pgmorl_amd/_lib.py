@@ -71,6 +71,7 @@ _SIGS = {
     'pgm_ppo_update_workspace_bytes': (C.c_size_t, [C.POINTER(Dims)]),
     'pgm_ppo_update_variant': (C.c_int, [C.POINTER(Dims), C.c_void_p, C.c_char_p, C.c_int]),
     'pgm_ppo_update_reset': (C.c_int, [C.POINTER(Dims), P_, P_]),
+    'pgm_ppo_fs_fragment_map': (C.c_int, [I32, I32, I32, I32, C.POINTER(I32), I32]),
     'pgm_eval': (C.c_int, [C.POINTER(Dims), P_, C.POINTER(EnvSpec), P_, P_, P_, I32, I32, I32, F64, P_, P_]),
     'pgm_randperm': (C.c_int, [I32, I32, C.c_uint64, P_, P_]),
     'pgm_normal_noise': (C.c_int, [C.c_int64, C.c_uint64, P_, P_]),

@@ -88,7 +88,7 @@ size_t fs_workspace_extra(const pgm_dims* d) {
 // compact head block, column c of feature block wb: entry v (= 4 g + r) at image index base + v for v < lim -- head
 // column c (c < 8), b1, b2, head bias, logstd (8..11), dW1 input 16 + (c - 12) (12..15)
 template <int O, int A, int K>
-__device__ __forceinline__ void cpt_column(int c, int wb, int m, int& base, int& lim) {
+__host__ __device__ __forceinline__ void cpt_column(int c, int wb, int m, int& base, int& lim) {
     constexpr int Q = qmax<A, K>();
     constexpr int oW2 = O * H, oWh = oW2 + H * SCR, oB1 = oWh + Q * H, oB2 = oB1 + H, oBh = oB2 + H, oLs = oBh + Q;
     const int NQ = m == 0 ? K : A, in = 16 + c - 12;
@@ -107,7 +107,7 @@ __device__ __forceinline__ void cpt_column(int c, int wb, int m, int& base, int&
 
 // fragment slot (block b, lane l, register r) -> tower image index (TowerImg), -1 for padding
 template <int O, int A, int K>
-__device__ __forceinline__ int frag_img(int b, int l, int r, int m) {
+__host__ __device__ __forceinline__ int frag_img(int b, int l, int r, int m) {
     constexpr int Q = qmax<A, K>(), K1M = fs_k1m(O), BPW = fs_bpw(O);
     constexpr int oW2 = O * H, oWh = oW2 + H * SCR, oB1 = oWh + Q * H, oB2 = oB1 + H, oBh = oB2 + H, oLs = oBh + Q;
     static_assert(!fs_compact(O) || Q <= 8, "compact fragments: head columns 0..7 only");
@@ -970,3 +970,26 @@ int ppo_update_fs_op(const pgm_dims* d, const MArgs& a, int ns, bool dual, int o
 }
 
 }  // namespace pgm
+
+// the fragment map as the kernels use it (frag_img on the host): what the CPU tests check for a bijection onto the
+// tower's parameters
+extern "C" int pgm_ppo_fs_fragment_map(int32_t O, int32_t A, int32_t K, int32_t m, int32_t* out, int32_t cap) {
+    using namespace pgm;
+    return dispatch_dims(O, A, K, "pgm_ppo_fs_fragment_map", [&](auto o, auto aa, auto k) -> int {
+        constexpr int O_ = decltype(o)::value, A_ = decltype(aa)::value, K_ = decltype(k)::value;
+        if constexpr (O_ > 32) {
+            set_error("pgm_ppo_fs_fragment_map: obs_dim %d > 32 has no feature-split update", O_);
+            return PGM_E_UNSUPPORTED;
+        } else {
+            constexpr int NB = fs_nb(O_);
+            if (!out || cap < NB * 256 || (m != 0 && m != 1)) {
+                set_error("pgm_ppo_fs_fragment_map: tower %d, buffer %d < %d entries", m, cap, NB * 256);
+                return PGM_E_INVALID_ARG;
+            }
+            for (int b = 0; b < NB; ++b)
+                for (int l = 0; l < 64; ++l)
+                    for (int r = 0; r < 4; ++r) out[(b * 64 + l) * 4 + r] = frag_img<O_, A_, K_>(b, l, r, m);
+            return NB;
+        }
+    });
+}

@@ -185,3 +185,41 @@ def test_update_workspace_is_monotone_in_tasks(env):
                 xslot = -(-(img + 1) // 32) * 32
                 need = flags + P * 2 * 4 * 2 * xslot * 8 + P * 2048 * 4 * rs * 4 + _fs_need(P, O)
                 assert need <= fixed, (cap, P, need, fixed)
+
+
+@pytest.mark.parametrize('env', ['MO-Walker2d-v2', 'MO-Hopper-v2', 'MO-Hopper-v3', 'MO-Ant-v2', 'MO-Swimmer-v2'])
+def test_fs_fragment_map_is_a_bijection_onto_the_tower(env):
+    """pgm_ppo_fs_fragment_map (the kernels' frag_img on the host): every parameter of a tower's image -- W1 [O][H],
+    W2 [H][H] of the [H][H+1] slab, the NQ head columns, b1, b2, the NQ head biases and (actor) logstd -- sits in
+    exactly one (block, lane, register) slot and nothing else does; obs_dim <= 20 takes the compact layout (6 blocks
+    per feature block: the head block's free columns carry the vector entries and dW1 inputs 16..19), above it
+    ceil(O / 16) + 6."""
+    import ctypes as C
+    from pgmorl_amd import envspec
+    spec = envspec.make_spec(env)
+    O, A, K, H = spec['obs_dim'], spec['act_dim'], spec['obj_num'], 64
+    Q = max(A, K)
+    bpw = 6 if O <= 20 else -(-O // 16) + 6
+    for m in (0, 1):
+        NQ = K if m == 0 else A
+        out = (C.c_int32 * (4 * bpw * 256))()
+        nb = _lib.lib().pgm_ppo_fs_fragment_map(O, A, K, m, out, len(out))
+        assert nb == 4 * bpw, (nb, bpw)
+        ix = np.frombuffer(out, dtype=np.int32)
+        valid = ix[ix >= 0]
+        assert len(np.unique(valid)) == len(valid), 'an image entry in two slots'
+        oW2 = O * H
+        oWh = oW2 + H * (H + 1)
+        oB1 = oWh + Q * H
+        oBh = oB1 + 2 * H
+        oLs = oBh + Q
+        want = set(range(O * H))
+        want |= {oW2 + i * (H + 1) + o for i in range(H) for o in range(H)}
+        want |= {oWh + q * H + u for q in range(NQ) for u in range(H)}
+        want |= set(range(oB1, oB1 + 2 * H)) | {oBh + q for q in range(NQ)}
+        if m == 1:
+            want |= {oLs + j for j in range(A)}
+        assert set(valid.tolist()) == want, (env, m, len(valid), len(want))
+    bad = (C.c_int32 * 16)()
+    assert _lib.lib().pgm_ppo_fs_fragment_map(O, A, K, 0, bad, 16) < 0
+    assert _lib.lib().pgm_ppo_fs_fragment_map(376, 17, 2, 0, bad, 16) < 0

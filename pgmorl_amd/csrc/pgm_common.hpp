@@ -172,6 +172,13 @@ __device__ __forceinline__ float row_sum16(float v) {
     v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x121, 0xf, 0xf, true));  // row_ror:1
     return v;
 }
+// sum over each 8-lane half of a 16-lane row (the result in every lane of the half): mirror, then two quad swaps
+__device__ __forceinline__ float row_sum8(float v) {
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xf, 0xf, true));  // row_half_mirror
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xb1, 0xf, 0xf, true));   // quad_perm 1,0,3,2
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4e, 0xf, 0xf, true));   // quad_perm 2,3,0,1
+    return v;
+}
 // rows (optional, 128 floats of LDS): the two reduced rows stored by every lane, so that another wave reads value i at
 // rows[(i / 4) * 64 + {0, 32, 16, 48}[i % 4]] without the readlanes
 // grow (optional, 8 floats of global memory): value i stored by one lane as an sc1 store at grow[(i / 4) * 4 + {0, 2, 1, 3}[i % 4]]

@@ -2,7 +2,8 @@
 // per-GPU populations (strong scaling: pop 40 over 8 GPUs = 5 tasks per GPU) and the alternative at every P.
 //
 // Work split.  Each tower of a task runs on NS workgroups (2 NS per task, all on one XCD under round-robin dispatch);
-// workgroup hs takes rows [hs mb / NS, (hs + 1) mb / NS) of every minibatch: R = mb / (16 NS) 16-row tiles.  Inside
+// workgroup hs takes its share of every minibatch's 16-row tiles: R = ceil(mb / (16 NS)) (NS = 6: 3 / 3 / 3 / 3 / 2 / 2
+// on a 256-row minibatch, a missing tile a zero-gradient dummy).  Inside
 // a workgroup the FOUR WAVES SPLIT THE 64 HIDDEN FEATURES (wave w: features 16w .. 16w + 15) instead of the rows, on
 // the v_mfma_f32_16x16x4_f32 layout
 //     C/D: lane l, register r <-> (row 4(l >> 4) + r, column l & 15); A: lane l holds A[l & 15][l >> 4];
@@ -13,7 +14,8 @@
 // shared LDS tiles, three workgroup barriers per minibatch step.
 //
 // Exchange (per Adam step, tags = step + 1, slots double-buffered by step parity):
-//   1. every wave publishes its gradient blocks (1 KiB "fragments" = the f32x4 C registers of 64 lanes) with
+//   1. every wave publishes its gradient blocks (1 KiB "fragments" = the f32x4 C registers of 64 lanes; obs_dim <= 20:
+//      6 per wave, the head block's free columns carrying b1 / b2 / head bias / logstd and dW1 inputs 16..19) with
 //      16-B sc1 stores, the workgroup drains and one lane stores the tagged image flag {step, loss sum};
 //   2. REDUCE-SCATTER: block b belongs to part b mod NS, which sums it over the NS parts in part order (sc1 loads) --
 //      a sum only its owner forms, so it is deterministic without being replicated;
@@ -28,7 +30,11 @@
 // (every wave gathers its own feature block).  Measured and dropped: a two-hop form (owners publish the reduced
 // gradient, every workgroup gathers all of it and runs Adam on the whole tower) -- one hop fewer, but Adam on ~32
 // elements per thread plus the wider gather cost more than the hop (P = 5: 28.1 K vs 24.7 K cycles per Adam step,
-// profiles/r04c_fs2_stamps_p5.txt, r04c_fs3_stamps_p5.txt).
+// profiles/r04c_fs2_stamps_p5.txt, r04c_fs3_stamps_p5.txt; again with compact fragments and feature-block Adam:
+// HalfCheetah P = 20 +5 %, Walker P = 40 equal, profiles/r05m_fs_twohop_ab.txt).
+//
+// Padding kept off the critical path: obs inputs 16..19 (one valid row of a 16-input MFMA block at obs_dim 17) are
+// VALU FMAs in layer 1 and dW1, and the actor's per-sample loss runs two tiles per pass (R = 2 / 3).
 //
 // Reference semantics (a2c_ppo_acktr/algo/ppo.py:58-115, storage.py:118-154, model.py:75-82, distributions.py:29-40)
 // as in pgm_ppo_mfma.hip, including torch.min/max/clamp tie gradients; entropy_coef enters once per tower.

@@ -1094,8 +1094,9 @@ int launch_critic_values(const pgm_dims* d, const RolloutArgs& a, hipStream_t s)
         const int R = (d->T + 1) * d->N;
         ValueArgs va{R, a.L, a.params, a.rb.obs, a.rb.values};
         if constexpr (O <= 32) {
-            // persistent workgroups: one per CU over the tasks (>= 1 per task), at most one per 4 tiles
-            const int wg = max(1, min(device_cu_count() / d->P, (R + 127) / 128));
+            // persistent workgroups: two per CU over the tasks (>= 1 per task; two waves per SIMD hide the dependent
+            // 32x32 MFMA chains of one tile), at most one per 4 tiles
+            const int wg = max(1, min(2 * device_cu_count() / d->P, (R + 127) / 128));
             return launch_k(value_mfma_kernel<O, K>, dim3(wg, d->P), dim3(256), sizeof(CriticMSmem<O, K>), s, va,
                             "pgm_rollout (critic values)");
         }

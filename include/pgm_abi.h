@@ -6,8 +6,9 @@
  * an int status (PGM_OK or a negative PGM_E_*).  pgm_last_error() returns a thread-local
  * message for the last failure.  No global mutable state besides that string, the pre-zeroed-workspace
  * marks of pgm_ppo_update_reset (mutex-guarded) and a per-device CU count (an immutable device property):
- * no cached launch decisions, no allocation inside the library.  Calls on distinct streams are
- * independent.  One host thread per device.
+ * no cached launch decisions, no allocation inside the library, and no environment variables read: every
+ * launch choice is an argument (pgm_launch_opts).  Calls on distinct streams are independent.  One host
+ * thread per device.
  *
  * Reference seams replaced (albo437/PGMORL; paths relative to the reference tree):
  *   pgm_act_forward       Policy.act / get_value            a2c_ppo_acktr/model.py:57-73
@@ -52,7 +53,7 @@
 extern "C" {
 #endif
 
-#define PGM_ABI_VERSION 3
+#define PGM_ABI_VERSION 4
 
 #define PGM_OK 0
 #define PGM_E_INVALID_ARG (-1)
@@ -124,6 +125,28 @@ typedef struct pgm_rollout_buf { /* device pointers */
     float* adv;
 } pgm_rollout_buf;
 
+/* Launch options (ABI 4; no reference counterpart): which kernel family pgm_rollout / pgm_eval / pgm_ppo_update may
+ * launch.  All zero, or a NULL pointer, = the automatic rule documented at each entry point.  The library reads no
+ * environment variables; pgmorl_amd/_lib.py maps PGM_UPDATE_KERNEL / PGM_UPDATE_SPLIT / PGM_FS_DUAL /
+ * PGM_ROLLOUT_KERNEL / PGM_EVAL_KERNEL onto this struct (A/B runs and tests). */
+#define PGM_UPDATE_AUTO 0     /* feature-split while it gets >= 4 parts per tower, else the row split */
+#define PGM_UPDATE_FS 1       /* the feature-split update wherever it fits */
+#define PGM_UPDATE_ROWSPLIT 2 /* the row-split MFMA kernels (t16, MODE 2 / 1 / 0) */
+#define PGM_UPDATE_VALU 3     /* the VALU reference update (obs_dim <= 64; A/B only) */
+#define PGM_SPLIT_AUTO 0      /* row split: as many workgroups per tower as fit the device */
+#define PGM_SPLIT_TASK 1      /* at most one workgroup per task (MODE 0; wide: one per tower) */
+#define PGM_SPLIT_TOWER 2     /* at most one workgroup per tower (MODE 1; wide NS 1) */
+#define PGM_SPLIT_HALVES 3    /* at most two per tower (MODE 2; wide NS 2) */
+#define PGM_SPLIT_QUARTERS 4  /* at most four per tower (t16; wide NS 4) */
+typedef struct pgm_launch_opts {
+    int32_t update_kernel;   /* PGM_UPDATE_*; obs_dim <= 32 with update_split != AUTO means ROWSPLIT */
+    int32_t update_split;    /* PGM_SPLIT_* (row-split and wide updates) */
+    int32_t fs_one_per_cu;   /* 1: the feature-split update never places two workgroups on one CU */
+    int32_t rollout_kernel;  /* 0 automatic (lane / wide kernels), 1 the workgroup-per-step kernel (A/B, tests) */
+    int32_t eval_kernel;     /* 0 automatic (wave / wide kernels), 1 the workgroup-per-step kernel (A/B, tests) */
+    int32_t _pad;
+} pgm_launch_opts;
+
 typedef struct pgm_ppo_hparams {
     float clip_param, value_loss_coef, entropy_coef, max_grad_norm;
     float adam_eps, beta1, beta2, _pad;
@@ -161,7 +184,7 @@ int pgm_env_step(const pgm_dims* d, const pgm_env_spec* spec, const pgm_env_stat
  * pgm_normal_noise keyed by seed (the iteration index). */
 int pgm_rollout(const pgm_dims* d, const float* params, const pgm_env_spec* spec, const pgm_env_state* st,
                 const pgm_norm_state* ns, const pgm_rollout_buf* rb, const float* noise, uint64_t seed,
-                int32_t carry, pgm_stream_t stream);
+                int32_t carry, const pgm_launch_opts* opts, pgm_stream_t stream);
 
 /* compute_returns(next_value already in values[T], use_gae, gamma, lam, use_proper_time_limits). */
 int pgm_gae(const pgm_dims* d, const pgm_rollout_buf* rb, float gamma, float lam, int32_t use_gae,
@@ -180,28 +203,30 @@ int pgm_adv_normalize(const pgm_dims* d, const pgm_rollout_buf* rb, const double
  * The critic and actor towers of a task run on separate CUs that exchange the squared gradient norm per
  * minibatch step.  obs_dim <= 32 and small per-GPU populations (>= 4 parts per tower fit: 16 NS ceil(P/8) <= CUs,
  * or <= 2 x CUs with two workgroups per CU when each part takes two 16-row tiles; minibatch rows a multiple of 16 NS):
- * each tower on NS = 16 / 8 / 4 workgroups that split the minibatch rows, the four waves of a workgroup split the
+ * each tower on NS = 16 / 8 / 6 / 4 workgroups that split the minibatch rows, the four waves of a workgroup split the
  * hidden features, and the gradient is reduce-scattered over the parts before Adam (the feature-split update;
- * PGM_FS_DUAL=0 keeps one workgroup per CU).  Otherwise each tower is split over four CUs (a quarter of the minibatch rows each, gradient
+ * opts->fs_one_per_cu keeps one workgroup per CU).  Otherwise each tower is split over four CUs (a quarter of the minibatch rows each, gradient
  * images added through the workspace) while 64 * ceil(P/8) <= CU count, else over two CUs while
  * 32 * ceil(P/8) <= CU count (obs_dim > 32: 32 * ceil(P/4) / 16 * ceil(P/4)).  obs_dim <= 32: tower
  * images LDS-resident (falls back to 2 CUs per task, then 1, as P grows); obs_dim > 32 (Humanoid): layer
  * 1 streamed from L2, needs 2P <= CU count (PGM_E_UNSUPPORTED otherwise: shard the tasks over more
- * GPUs).  PGM_UPDATE_SPLIT=0/1/2/4 caps the row split; PGM_UPDATE_KERNEL=fs forces the feature-split
- * update wherever it fits, =mfma the row-split kernels.
+ * GPUs).  opts->update_split caps the row split; opts->update_kernel = PGM_UPDATE_FS forces the feature-split
+ * update wherever it fits, PGM_UPDATE_ROWSPLIT the row-split kernels.
  * After the call, the 8-byte word at index 2P of the workspace is nonzero iff an exchange timed out
  * (the workgroups were not co-resident); the results of such a call are invalid. */
 int pgm_ppo_update(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params, float* adam_m,
                    float* adam_v, int32_t* adam_step, const float* lr, const int32_t* perms,
-                   const pgm_rollout_buf* rb, float* stats, void* workspace, pgm_stream_t stream);
+                   const pgm_rollout_buf* rb, float* stats, void* workspace, const pgm_launch_opts* opts,
+                   pgm_stream_t stream);
 /* Workspace bytes for dims d; monotone in d->P, so a workspace sized for P serves every call with P' <= P tasks
  * (the same other dims). */
 size_t pgm_ppo_update_workspace_bytes(const pgm_dims* d);
-/* The update kernel pgm_ppo_update would launch for these dims and hyper-parameters on the current device (same
- * selection rule, including the PGM_UPDATE_KERNEL / PGM_UPDATE_SPLIT overrides), as text into buf[n]
+/* The update kernel pgm_ppo_update would launch for these dims, hyper-parameters and opts on the current device
+ * (the same selection rule), as text into buf[n]
  * (e.g. "ppo_update_fs_kernel (NS=16, R=1)", "... (NS=8, R=2, 2 per CU)"): what benchmarks and profiles report.  No reference
  * counterpart (diagnostic). */
-int pgm_ppo_update_variant(const pgm_dims* d, const pgm_ppo_hparams* hp, char* buf, int n);
+int pgm_ppo_update_variant(const pgm_dims* d, const pgm_ppo_hparams* hp, const pgm_launch_opts* opts, char* buf,
+                           int n);
 /* Zero, on `stream`, the part of the workspace the next pgm_ppo_update for dims d would reset inside the call,
  * and let that call skip its own reset (the caller orders this stream before the update's stream and after
  * every read of the previous update's timeout word).  Lets a caller take the reset off the update's stream. */
@@ -217,7 +242,7 @@ int pgm_ppo_fs_fragment_map(int32_t O, int32_t A, int32_t K, int32_t m, int32_t*
  * unless raw). */
 int pgm_eval(const pgm_dims* d, const float* params, const pgm_env_spec* spec, const double* ob_mean,
              const double* ob_var, const double* s0_eval, int32_t eval_num, int32_t use_ob_rms, int32_t raw,
-             double gamma, double* objs_out, pgm_stream_t stream);
+             double gamma, double* objs_out, const pgm_launch_opts* opts, pgm_stream_t stream);
 
 /* count independent random permutations of [0, n) into out [count][n] (int32), keyed by seed. */
 int pgm_randperm(int32_t n, int32_t count, uint64_t seed, int32_t* out, pgm_stream_t stream);

@@ -46,8 +46,16 @@ def build_host(force=False, verbose=False):
     return HOST_LIB
 
 
-def build(force=False, verbose=False, stamps=False):
-    """stamps=True builds the diagnostic libpgm_stamps.so (-DPGM_STAMPS phase timers); never shipped."""
+TEST_LIB = os.path.join(HERE, 'libpgm_test.so')
+
+
+def build(force=False, verbose=False, stamps=False, test_hooks=False):
+    """stamps=True builds the diagnostic libpgm_stamps.so (-DPGM_STAMPS phase timers); never shipped.
+    test_hooks=True builds libpgm_test.so: the production objects with pgm_abi.cpp recompiled -DPGM_TEST_HOOKS (the
+    PGM_TEST_DELAY exchange stall and the PGM_TEST_RESIDENT_CUS co-residency override, read by the test build only;
+    tests/test_gpu_exchange.py loads it through _lib.test_build())."""
+    if test_hooks:
+        return _build_test(force=force, verbose=verbose)
     objdir = OBJDIR + ('_stamps' if stamps else '')
     lib = LIB.replace('libpgm.so', 'libpgm_stamps.so') if stamps else LIB
     flags = FLAGS + (['-DPGM_STAMPS'] if stamps else [])
@@ -83,5 +91,32 @@ def build(force=False, verbose=False, stamps=False):
     return lib
 
 
+def _build_test(force=False, verbose=False):
+    build(force=force, verbose=verbose)
+    hipcc = _hipcc()
+    objdir = OBJDIR + '_test'
+    os.makedirs(objdir, exist_ok=True)
+    src = os.path.join(CSRC, 'pgm_abi.cpp')
+    o = os.path.join(objdir, 'pgm_abi.cpp.o')
+    deps = [src] + [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(ROOT, 'include', 'pgm_abi.h')]
+    if force or not os.path.exists(o) or os.path.getmtime(o) < _newest(deps):
+        cmd = [hipcc, *FLAGS, '-DPGM_TEST_HOOKS', '-c', src, '-o', o]
+        if verbose:
+            print(' '.join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f'hipcc failed on pgm_abi.cpp (test hooks):\n{r.stdout}\n{r.stderr}')
+    objs = [o] + [os.path.join(OBJDIR, s + '.o') for s in SOURCES if s != 'pgm_abi.cpp']
+    if force or not os.path.exists(TEST_LIB) or os.path.getmtime(TEST_LIB) < _newest(objs):
+        cmd = [hipcc, f'--offload-arch={ARCH}', '-shared', '-fPIC', *objs, '-o', TEST_LIB]
+        if verbose:
+            print(' '.join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f'hipcc link failed (test build):\n{r.stdout}\n{r.stderr}')
+    return TEST_LIB
+
+
 if __name__ == '__main__':
-    print(build(force='--force' in sys.argv, verbose=True, stamps='--stamps' in sys.argv))
+    print(build(force='--force' in sys.argv, verbose=True, stamps='--stamps' in sys.argv,
+                test_hooks='--test' in sys.argv))

@@ -49,7 +49,9 @@ int check_coresident(const void* kern, int block, size_t smem, int grid, const c
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, block, smem);
     if (e != hipSuccess) return hip_fail(e, what);
     int cus = device_cu_count();
-    if (const char* o = getenv("PGM_TEST_RESIDENT_CUS")) cus = atoi(o);  // test-only: pretend a smaller device
+#ifdef PGM_TEST_HOOKS
+    if (const char* o = getenv("PGM_TEST_RESIDENT_CUS")) cus = atoi(o);  // test build only: pretend a smaller device
+#endif
     if (per_cu < 1 || (long long)grid > (long long)per_cu * cus) {
         set_error("%s: %d workgroups of %d threads (%zu B LDS) cannot all be co-resident: occupancy %d per CU x %d "
                   "CUs; shard the tasks over more GPUs", what, grid, block, smem, per_cu, cus);
@@ -58,15 +60,29 @@ int check_coresident(const void* kern, int block, size_t smem, int grid, const c
     return PGM_OK;
 }
 
-DbgDelay dbg_delay_from_env() {
+DbgDelay dbg_delay_hook() {
     DbgDelay d{0, 0, 0, 0u};
+#ifdef PGM_TEST_HOOKS
     const char* s = getenv("PGM_TEST_DELAY");
     if (s && *s) {
         int st = 0, bl = 0, wh = 0;
         unsigned cy = 0;
         if (sscanf(s, "%d:%d:%d:%u", &st, &bl, &wh, &cy) == 4) d = DbgDelay{st, bl, wh, cy};
     }
+#endif
     return d;
+}
+
+int read_opts(const pgm_launch_opts* o, pgm_launch_opts* out, const char* what) {
+    *out = o ? *o : pgm_launch_opts{};
+    if (out->update_kernel < PGM_UPDATE_AUTO || out->update_kernel > PGM_UPDATE_VALU ||
+        out->update_split < PGM_SPLIT_AUTO || out->update_split > PGM_SPLIT_QUARTERS ||
+        (unsigned)out->fs_one_per_cu > 1u || (unsigned)out->rollout_kernel > 1u || (unsigned)out->eval_kernel > 1u) {
+        set_error("%s: invalid pgm_launch_opts {%d, %d, %d, %d, %d}", what, out->update_kernel, out->update_split,
+                  out->fs_one_per_cu, out->rollout_kernel, out->eval_kernel);
+        return PGM_E_INVALID_ARG;
+    }
+    return PGM_OK;
 }
 
 static inline int32_t round_up(int32_t x, int32_t m) { return (x + m - 1) / m * m; }

@@ -78,15 +78,28 @@ int device_cu_count();  // CUs of the current device (cached)
 // block size and LDS must admit grid <= blocks-per-CU x CUs.  PGM_E_UNSUPPORTED (with the numbers) otherwise.
 int check_coresident(const void* kern, int block, size_t smem, int grid, const char* what);
 
-// Test-only exchange delay (PGM_TEST_DELAY="step:block:where:cycles", parsed by the launcher; cycles 0 = off):
-// workgroup `block` stalls `cycles` shader cycles at hand-off point `where` of Adam step `step` -- 0 before
-// publishing its gradient image, 1 between its image flag store and its partner poll, 2 between its tower-norm
-// granule store and its poll.  Provokes the delayed-poll orders the step-parity double buffering must survive.
+// Launch options with NULL = automatic, validated (pgm_abi.h pgm_launch_opts).
+int read_opts(const pgm_launch_opts* o, pgm_launch_opts* out, const char* what);
+// Row-split cap of opts->update_split: 4 (four per tower), 2, 1 (one per tower), 0 (one per task); 4 when automatic.
+inline int split_cap(const pgm_launch_opts& o) {
+    switch (o.update_split) {
+        case PGM_SPLIT_TASK: return 0;
+        case PGM_SPLIT_TOWER: return 1;
+        case PGM_SPLIT_HALVES: return 2;
+        default: return 4;
+    }
+}
+
+// Exchange delay of the TEST build only (libpgm_test.so, -DPGM_TEST_HOOKS; the production library returns an inert
+// delay and keeps no such hook): PGM_TEST_DELAY="step:block:where:cycles" -- workgroup `block` stalls `cycles` shader
+// cycles at hand-off point `where` of Adam step `step` -- 0 before publishing its gradient image, 1 between its image
+// flag store and its partner poll, 2 between its tower-norm granule store and its poll, 3 (feature-split) before its
+// Adam step.  Provokes the delayed-poll orders the step-parity double buffering must survive.
 struct DbgDelay {
     int step, block, where;
     unsigned cycles;
 };
-DbgDelay dbg_delay_from_env();
+DbgDelay dbg_delay_hook();
 __device__ __forceinline__ void dbg_delay(const DbgDelay& d, int nstep, int where) {
     if (d.cycles != 0u && nstep == d.step && (int)blockIdx.x == d.block && where == d.where) {
         const unsigned long long t0 = __builtin_amdgcn_s_memtime();

@@ -747,8 +747,10 @@ int pgm_env_step(const pgm_dims* d, const pgm_env_spec* spec, const pgm_env_stat
 
 int pgm_rollout(const pgm_dims* d, const float* params, const pgm_env_spec* spec, const pgm_env_state* st,
                 const pgm_norm_state* ns, const pgm_rollout_buf* rb, const float* noise, uint64_t seed,
-                int32_t carry, pgm_stream_t stream) {
+                int32_t carry, const pgm_launch_opts* opts, pgm_stream_t stream) {
     if (int rc = env_common(d, spec, st, ns, "pgm_rollout")) return rc;
+    pgm_launch_opts o;
+    if (int rc = read_opts(opts, &o, "pgm_rollout")) return rc;
     if (!params || !rb || !rb->obs || !rb->actions || !rb->logp || !rb->values || !rb->rewards || !rb->masks ||
         !rb->bad_masks) {
         set_error("pgm_rollout: null pointer");
@@ -760,9 +762,9 @@ int pgm_rollout(const pgm_dims* d, const float* params, const pgm_env_spec* spec
     }
     RolloutArgs a{d->P, d->N, d->T, make_layout(d->O, d->A, d->K, d->H), params, *spec, *st, *ns, *rb,
                   noise, seed, carry};
-    const char* sel = getenv("PGM_ROLLOUT_KERNEL");  // "block": the workgroup-per-step kernel (A/B, tests)
-    if (!(sel && sel[0] == 'b') && rollout_lanes_supported(d)) return launch_rollout_lanes(d, a, (hipStream_t)stream);
-    if (!(sel && sel[0] == 'b') && rollout_wide_supported(d)) return launch_rollout_wide(d, a, (hipStream_t)stream);
+    const bool block = o.rollout_kernel == 1;  // the workgroup-per-step kernel (A/B, tests)
+    if (!block && rollout_lanes_supported(d)) return launch_rollout_lanes(d, a, (hipStream_t)stream);
+    if (!block && rollout_wide_supported(d)) return launch_rollout_wide(d, a, (hipStream_t)stream);
     return dispatch_dims(d->O, d->A, d->K, "pgm_rollout", [&](auto o, auto aa, auto k) {
         constexpr int O = decltype(o)::value, A = decltype(aa)::value, K = decltype(k)::value;
         return launch_smem(rollout_kernel<O, A, K>, d->P, sizeof(StepSmem<O, A, K>), (hipStream_t)stream, a,
@@ -772,17 +774,19 @@ int pgm_rollout(const pgm_dims* d, const float* params, const pgm_env_spec* spec
 
 int pgm_eval(const pgm_dims* d, const float* params, const pgm_env_spec* spec, const double* ob_mean,
              const double* ob_var, const double* s0_eval, int32_t eval_num, int32_t use_ob_rms, int32_t raw,
-             double gamma, double* objs_out, pgm_stream_t stream) {
+             double gamma, double* objs_out, const pgm_launch_opts* opts, pgm_stream_t stream) {
     if (int rc = check_dims(d, "pgm_eval")) return rc;
+    pgm_launch_opts o;
+    if (int rc = read_opts(opts, &o, "pgm_eval")) return rc;
     if (!params || !spec_ok(spec) || !s0_eval || !objs_out || eval_num <= 0 || (use_ob_rms && (!ob_mean || !ob_var))) {
         set_error("pgm_eval: bad arguments");
         return PGM_E_INVALID_ARG;
     }
     EvalArgs a{d->P, make_layout(d->O, d->A, d->K, d->H), params, *spec, ob_mean, ob_var, s0_eval,
                eval_num, use_ob_rms, raw, gamma, objs_out};
-    const char* sel = getenv("PGM_EVAL_KERNEL");  // "block": the workgroup-per-step kernel (A/B, tests)
-    if (!(sel && sel[0] == 'b') && eval_waves_supported(d, eval_num)) return launch_eval_waves(d, a, (hipStream_t)stream);
-    if (!(sel && sel[0] == 'b') && eval_wide_supported(d, eval_num)) return launch_eval_wide(d, a, (hipStream_t)stream);
+    const bool block = o.eval_kernel == 1;  // the workgroup-per-step kernel (A/B, tests)
+    if (!block && eval_waves_supported(d, eval_num)) return launch_eval_waves(d, a, (hipStream_t)stream);
+    if (!block && eval_wide_supported(d, eval_num)) return launch_eval_wide(d, a, (hipStream_t)stream);
     return dispatch_dims(d->O, d->A, d->K, "pgm_eval", [&](auto o, auto aa, auto k) {
         constexpr int O = decltype(o)::value, A = decltype(aa)::value, K = decltype(k)::value;
         return launch_smem(eval_kernel<O, A, K>, d->P, sizeof(StepSmem<O, A, K>), (hipStream_t)stream, a,

@@ -933,14 +933,13 @@ int ppo_update_fs_op(const pgm_dims* d, const MArgs& a, int ns, bool dual, int o
 // 8 per part; 0 = the feature-split update does not apply.  *dual = 1: the grid (16 NS ceil(P/8) workgroups) exceeds
 // the CU count and runs two workgroups per CU, taken for R = 2 where both fit one CU (<= 80 KiB LDS, <= 256
 // registers): a step's three hand-offs then overlap the other workgroup's tiles (HalfCheetah P = 20: NS 4, R 4
-// 4.45 ms -> NS 8, R 2 4.01 ms; profiles/r04r_fs_dual_ab.json).  PGM_FS_DUAL=0: one per CU only.  The occupancy of
-// the exact kernel is queried at every call (no cached answer: the library keeps no mutable state, pgm_abi.h).
-int fs_choose_ns(const pgm_dims* d, int mb, int* dual) {
+// 4.45 ms -> NS 8, R 2 4.01 ms; profiles/r04r_fs_dual_ab.json).  dual_ok = false (pgm_launch_opts.fs_one_per_cu): one
+// per CU only.  The occupancy of the exact kernel is queried at every call (no cached answer: the library keeps no
+// mutable state, pgm_abi.h).
+int fs_choose_ns(const pgm_dims* d, int mb, bool dual_ok, int* dual) {
     *dual = 0;
     if (d->O > 32) return 0;
     const int cus = device_cu_count();
-    const char* dsel = getenv("PGM_FS_DUAL");
-    const bool dual_ok = !(dsel && dsel[0] == '0');
     if (mb % 16 != 0) return 0;
     for (const int ns : FS_NS_LIST) {
         // (6 parts: the row tiles dealt raggedly, at most 3 per part; other counts: an exact split)

@@ -1804,32 +1804,29 @@ int launch_mode(const pgm_dims* d, const MArgs& a, hipStream_t stream) {
     return launch_mode_k<O, A, K, MODE, false>(d, a, stream);
 }
 
-int fs_choose_ns(const pgm_dims* d, int mb, int* dual);
+int fs_choose_ns(const pgm_dims* d, int mb, bool dual_ok, int* dual);
 int ppo_update_fs(const pgm_dims* d, const MArgs& a, int ns, bool dual, hipStream_t stream);
 
 // Which obs_dim <= 32 update runs (one rule for the launcher and pgm_ppo_update_variant):
 //   * feature-split with the reduce-scattered Adam (pgm_ppo_fs.hip) while it gets >= FS_AUTO_NS parts per tower
-//     (small per-GPU populations: the latency form), or always with PGM_UPDATE_KERNEL=fs;
-//   * else the row-split kernels, PGM_UPDATE_SPLIT capping them: 4 (default) = 16-row tiles on 4 workgroups per
-//     tower (8 CUs per task, while t16_grid(P, 4) <= CUs), 2 = 32-row tiles on 2 workgroups per tower (MODE 2, while
-//     mode2_grid(P) <= CUs), 1 = one workgroup per tower (2P <= CUs), 0 = one per task; each falls back to the next
-//     one down.  (16-row tiles on 2 workgroups of 8 waves measured slower than MODE 2 everywhere: 7.37 vs 6.55 ms.)
-// PGM_UPDATE_KERNEL other than fs / auto (e.g. "mfma", the tests' row-split A/B) or any PGM_UPDATE_SPLIT keeps the
-// row-split kernels.
+//     (small per-GPU populations: the latency form), or always with opts.update_kernel = PGM_UPDATE_FS;
+//   * else the row-split kernels, opts.update_split capping them: four workgroups per tower (default) = 16-row tiles
+//     (8 CUs per task, while t16_grid(P, 4) <= CUs), two = 32-row tiles (MODE 2, while mode2_grid(P) <= CUs), one per
+//     tower (2P <= CUs), one per task; each falls back to the next one down.  (16-row tiles on 2 workgroups of 8
+//     waves measured slower than MODE 2 everywhere: 7.37 vs 6.55 ms.)
+// opts.update_kernel = PGM_UPDATE_ROWSPLIT (the tests' row-split A/B) or any update_split keeps the row-split kernels.
 constexpr int FS_AUTO_NS = 4;
 struct UpdateChoice {
     int kind;  // 0 = MODE (mode), 1 = t16 (ns, w), 2 = feature-split (ns, dual: two workgroups per CU)
     int ns, w, mode, dual;
 };
-static UpdateChoice choose_update(const pgm_dims* d, int mb) {
-    const char* ksel = getenv("PGM_UPDATE_KERNEL");
-    const char* sel = getenv("PGM_UPDATE_SPLIT");
-    const bool force_fs = ksel && ksel[0] == 'f' && ksel[1] == 's';
-    const bool auto_k = !sel && (!ksel || !ksel[0] || (ksel[0] == 'a' && ksel[1] == 'u'));
+static UpdateChoice choose_update(const pgm_dims* d, int mb, const pgm_launch_opts& o) {
+    const bool force_fs = o.update_kernel == PGM_UPDATE_FS;
+    const bool auto_k = o.update_split == PGM_SPLIT_AUTO && o.update_kernel == PGM_UPDATE_AUTO;
     int fs_dual = 0;
-    const int fs_ns = fs_choose_ns(d, mb, &fs_dual);
+    const int fs_ns = fs_choose_ns(d, mb, o.fs_one_per_cu == 0, &fs_dual);
     if (fs_ns > 0 && (force_fs || (auto_k && fs_ns >= FS_AUTO_NS))) return {2, fs_ns, 4, 0, fs_dual};
-    const int cap = sel && sel[0] >= '0' && sel[0] <= '4' ? sel[0] - '0' : 4;
+    const int cap = split_cap(o);
     const int cus = device_cu_count();
     if (cap >= 4 && t16_grid(d->P, 4) <= cus) return {1, 4, 4, 0, 0};
     if (cap >= 2 && mode2_grid(d->P) <= cus) return {0, 2, 4, 2, 0};
@@ -1837,9 +1834,9 @@ static UpdateChoice choose_update(const pgm_dims* d, int mb) {
     return {0, 1, 4, 0, 0};
 }
 
-int describe_update_mfma(const pgm_dims* d, const pgm_ppo_hparams* hp, char* buf, int n) {
+int describe_update_mfma(const pgm_dims* d, const pgm_ppo_hparams* hp, const pgm_launch_opts& o, char* buf, int n) {
     const int mb = d->T * d->N / hp->num_mini_batch;
-    const UpdateChoice c = choose_update(d, mb);
+    const UpdateChoice c = choose_update(d, mb, o);
     if (c.kind == 2)
         return snprintf(buf, n, "ppo_update_fs_kernel (NS=%d, R=%d%s)", c.ns, (mb / 16 + c.ns - 1) / c.ns,
                         c.dual ? ", 2 per CU" : "");
@@ -1848,7 +1845,8 @@ int describe_update_mfma(const pgm_dims* d, const pgm_ppo_hparams* hp, char* buf
 }
 
 template <int O, int A, int K>
-int launch_ppo_update_mfma(const pgm_dims* d, const MArgs& a, const pgm_rollout_buf* rb, hipStream_t stream) {
+int launch_ppo_update_mfma(const pgm_dims* d, const MArgs& a, const pgm_rollout_buf* rb, const pgm_launch_opts& o,
+                           hipStream_t stream) {
     // packed sample table, then the update
     constexpr int RS = row_stride<O, A, K>();
     static_assert(img_floats<O, A, K>() == ppo_img_floats(O, A, K), "host exchange-slot size out of sync");
@@ -1861,7 +1859,7 @@ int launch_ppo_update_mfma(const pgm_dims* d, const MArgs& a, const pgm_rollout_
     // every workgroup of a split launch must be resident at once: one per CU (LDS > 80 KiB, 512 registers
     // per lane), so the grid must fit the CU count (choose_update)
     static_assert(sizeof(MSmem<O, A, K, true>) > 80 * 1024, "split residency argument needs > 80 KiB LDS");
-    const UpdateChoice c = choose_update(d, d->T * d->N / a.hp.num_mini_batch);
+    const UpdateChoice c = choose_update(d, d->T * d->N / a.hp.num_mini_batch, o);
     if (c.kind == 2) return ppo_update_fs(d, a, c.ns, c.dual != 0, stream);
     if (c.kind == 1) return launch_t16<O, A, K, 4, 4>(d, a, stream);
     if (c.mode == 2) return launch_mode<O, A, K, 2>(d, a, stream);
@@ -1871,7 +1869,7 @@ int launch_ppo_update_mfma(const pgm_dims* d, const MArgs& a, const pgm_rollout_
 
 int ppo_update_mfma(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params, float* adam_m, float* adam_v,
                     int32_t* adam_step, const float* lr, const int32_t* perms, const pgm_rollout_buf* rb, float* stats,
-                    void* workspace, hipStream_t stream) {
+                    void* workspace, const pgm_launch_opts& opts, hipStream_t stream) {
     if (!workspace) {
         set_error("pgm_ppo_update: the MFMA update needs the workspace (pgm_ppo_update_workspace_bytes)");
         return PGM_E_INVALID_ARG;
@@ -1880,7 +1878,7 @@ int ppo_update_mfma(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params,
     MArgs a{d->N, d->T, make_layout(d->O, d->A, d->K, d->H), *hp, params, adam_m, adam_v, adam_step, lr, perms,
             (const float*)(ws + ppo_flag_bytes(d->P) + ppo_xbuf_bytes(d)), stats, (unsigned long long*)ws,
             (unsigned long long*)(ws + ppo_flag_bytes(d->P)), ppo_xslot(d->O, d->A, d->K), (int)ppo_xbuf_bytes(d),
-            d->P, dbg_delay_from_env(),
+            d->P, dbg_delay_hook(),
             ws + ppo_flag_bytes(d->P) + ppo_xbuf_bytes(d) + (size_t)d->P * d->T * d->N * ppo_row_stride(d->O, d->A, d->K) * sizeof(float)};
     return dispatch_dims(d->O, d->A, d->K, "pgm_ppo_update", [&](auto o, auto aa, auto k) -> int {
         constexpr int O = decltype(o)::value, A = decltype(aa)::value, K = decltype(k)::value;
@@ -1888,7 +1886,7 @@ int ppo_update_mfma(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params,
             set_error("pgm_ppo_update: obs_dim %d > 32 not supported by the MFMA update kernel", O);
             return PGM_E_UNSUPPORTED;
         } else {
-            return launch_ppo_update_mfma<O, A, K>(d, a, rb, stream);
+            return launch_ppo_update_mfma<O, A, K>(d, a, rb, opts, stream);
         }
     });
 }

@@ -513,10 +513,10 @@ __global__ __launch_bounds__(UT) void ppo_update_kernel(UpdArgs a) {
 namespace pgm {
 int ppo_update_mfma(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params, float* adam_m, float* adam_v,
                     int32_t* adam_step, const float* lr, const int32_t* perms, const pgm_rollout_buf* rb, float* stats,
-                    void* workspace, hipStream_t stream);
+                    void* workspace, const pgm_launch_opts& o, hipStream_t stream);
 int ppo_update_wide(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params, float* adam_m, float* adam_v,
                     int32_t* adam_step, const float* lr, const int32_t* perms, const pgm_rollout_buf* rb, float* stats,
-                    void* workspace, hipStream_t stream);
+                    void* workspace, const pgm_launch_opts& o, hipStream_t stream);
 }
 
 using namespace pgm;
@@ -524,19 +524,22 @@ using namespace pgm;
 extern "C" size_t pgm_ppo_update_workspace_bytes(const pgm_dims* d) { return d ? ppo_workspace_bytes(d) : 0; }
 
 namespace pgm {
-int describe_update_mfma(const pgm_dims* d, const pgm_ppo_hparams* hp, char* buf, int n);
-int describe_update_wide(const pgm_dims* d, char* buf, int n);
+int describe_update_mfma(const pgm_dims* d, const pgm_ppo_hparams* hp, const pgm_launch_opts& o, char* buf, int n);
+int describe_update_wide(const pgm_dims* d, const pgm_launch_opts& o, char* buf, int n);
 }
-extern "C" int pgm_ppo_update_variant(const pgm_dims* d, const pgm_ppo_hparams* hp, char* buf, int n) {
+extern "C" int pgm_ppo_update_variant(const pgm_dims* d, const pgm_ppo_hparams* hp, const pgm_launch_opts* opts,
+                                      char* buf, int n) {
     if (int rc = check_dims(d, "pgm_ppo_update_variant")) return rc;
     if (!hp || !buf || n <= 0 || hp->num_mini_batch <= 0) {
         set_error("pgm_ppo_update_variant: null pointer or empty buffer");
         return PGM_E_INVALID_ARG;
     }
-    const char* sel = getenv("PGM_UPDATE_KERNEL");
-    if (sel && sel[0] == 'v') return snprintf(buf, n, "ppo_update_kernel (VALU, A/B)") > 0 ? PGM_OK : PGM_E_INVALID_ARG;
-    if (d->O <= 32) return describe_update_mfma(d, hp, buf, n) > 0 ? PGM_OK : PGM_E_INVALID_ARG;
-    return describe_update_wide(d, buf, n) > 0 ? PGM_OK : PGM_E_INVALID_ARG;
+    pgm_launch_opts o;
+    if (int rc = read_opts(opts, &o, "pgm_ppo_update_variant")) return rc;
+    if (o.update_kernel == PGM_UPDATE_VALU)
+        return snprintf(buf, n, "ppo_update_kernel (VALU, A/B)") > 0 ? PGM_OK : PGM_E_INVALID_ARG;
+    if (d->O <= 32) return describe_update_mfma(d, hp, o, buf, n) > 0 ? PGM_OK : PGM_E_INVALID_ARG;
+    return describe_update_wide(d, o, buf, n) > 0 ? PGM_OK : PGM_E_INVALID_ARG;
 }
 
 // workspaces zeroed ahead of their next launch by pgm_ppo_update_reset: pointer -> zeroed bytes
@@ -568,8 +571,11 @@ extern "C" int pgm_ppo_update_reset(const pgm_dims* d, void* workspace, pgm_stre
 
 extern "C" int pgm_ppo_update(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params, float* adam_m,
                               float* adam_v, int32_t* adam_step, const float* lr, const int32_t* perms,
-                              const pgm_rollout_buf* rb, float* stats, void* workspace, pgm_stream_t stream) {
+                              const pgm_rollout_buf* rb, float* stats, void* workspace, const pgm_launch_opts* opts,
+                              pgm_stream_t stream) {
     if (int rc = check_dims(d, "pgm_ppo_update")) return rc;
+    pgm_launch_opts o;
+    if (int rc = read_opts(opts, &o, "pgm_ppo_update")) return rc;
     if (!hp || !params || !adam_m || !adam_v || !adam_step || !lr || !perms || !rb || !rb->obs || !rb->actions ||
         !rb->logp || !rb->values || !rb->returns || !rb->adv || !stats) {
         set_error("pgm_ppo_update: null pointer");
@@ -582,14 +588,13 @@ extern "C" int pgm_ppo_update(const pgm_dims* d, const pgm_ppo_hparams* hp, floa
     }
     // f32-MFMA kernels: obs_dim <= 32 (Walker, Cheetah, Hopper, Ant, Swimmer) with LDS-resident towers, wider
     // observations (Humanoid) with layer 1 in L2; the VALU kernel is kept for A/B measurements
-    // (PGM_UPDATE_KERNEL=valu) and covers obs_dim <= 64
-    const char* sel = getenv("PGM_UPDATE_KERNEL");
-    const bool valu = sel && sel[0] == 'v';
+    // (opts.update_kernel = PGM_UPDATE_VALU) and covers obs_dim <= 64
+    const bool valu = o.update_kernel == PGM_UPDATE_VALU;
     if (!valu && d->O <= 32)
-        return ppo_update_mfma(d, hp, params, adam_m, adam_v, adam_step, lr, perms, rb, stats, workspace,
+        return ppo_update_mfma(d, hp, params, adam_m, adam_v, adam_step, lr, perms, rb, stats, workspace, o,
                                (hipStream_t)stream);
     if (!valu && d->O > 64)
-        return ppo_update_wide(d, hp, params, adam_m, adam_v, adam_step, lr, perms, rb, stats, workspace,
+        return ppo_update_wide(d, hp, params, adam_m, adam_v, adam_step, lr, perms, rb, stats, workspace, o,
                                (hipStream_t)stream);
     if (d->O > 64) {
         set_error("pgm_ppo_update: obs_dim %d > 64 not supported by the update kernels", d->O);

@@ -888,28 +888,27 @@ PGM_UNROLL_W(PGM_UW_L2)
 
 }  // namespace
 
-static int wide_choose_ns(const pgm_dims* d) {
-    const char* sel = getenv("PGM_UPDATE_SPLIT");
-    const int cap = sel && sel[0] >= '0' && sel[0] <= '4' ? sel[0] - '0' : 4;
+static int wide_choose_ns(const pgm_dims* d, const pgm_launch_opts& o) {
+    const int cap = split_cap(o);
     const int cus = device_cu_count();
     return cap >= 4 && wide_grid(d->P, 4) <= cus ? 4 : cap >= 2 && wide_grid(d->P, 2) <= cus ? 2 : 1;
 }
 
-int describe_update_wide(const pgm_dims* d, char* buf, int n) {
-    return snprintf(buf, n, "ppo_update_wide_kernel (NS=%d)", wide_choose_ns(d));
+int describe_update_wide(const pgm_dims* d, const pgm_launch_opts& o, char* buf, int n) {
+    return snprintf(buf, n, "ppo_update_wide_kernel (NS=%d)", wide_choose_ns(d, o));
 }
 
 int ppo_update_wide(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params, float* adam_m, float* adam_v,
                     int32_t* adam_step, const float* lr, const int32_t* perms, const pgm_rollout_buf* rb, float* stats,
-                    void* workspace, hipStream_t stream) {
+                    void* workspace, const pgm_launch_opts& o, hipStream_t stream) {
     if (!workspace) {
         set_error("pgm_ppo_update: the wide update needs the workspace (pgm_ppo_update_workspace_bytes)");
         return PGM_E_INVALID_ARG;
     }
     // NS = 4 (each tower on four CUs) while the 32-block groups fit the CU count, else NS = 2 while the
-    // 16-block groups do, else 1; PGM_UPDATE_SPLIT caps it (0/1: one workgroup per tower, 2: at most two)
+    // 16-block groups do, else 1; opts.update_split caps it (TASK / TOWER: one workgroup per tower, HALVES: two)
     const int cus = device_cu_count();
-    const int ns = wide_choose_ns(d);
+    const int ns = wide_choose_ns(d, o);
     if (ns == 1 && 2 * d->P > cus) {
         set_error("pgm_ppo_update: the wide update needs 2P <= CUs (P=%d); shard the tasks over more GPUs", d->P);
         return PGM_E_UNSUPPORTED;

@@ -17,7 +17,7 @@ import numpy as np
 import torch
 
 from . import envspec
-from ._lib import (Dims, EnvSpec, EnvState, NormState, PGMError, PPOHParams, RolloutBuf, check, lib)
+from ._lib import (Dims, EnvSpec, EnvState, NormState, PGMError, PPOHParams, RolloutBuf, check, launch_opts, lib)
 from .layout import ParamLayout
 
 F32, F64, I32 = torch.float32, torch.float64, torch.int32
@@ -241,7 +241,7 @@ class TaskBatch:
             nz = self.noise
         check(lib().pgm_rollout(C.byref(self.dims), _ptr(self.params), C.byref(self.c_spec), C.byref(self.c_state),
                                 C.byref(self.c_norm), C.byref(self.c_rb), _ptr(nz), C.c_uint64(seed),
-                                int(carry), _stream()), 'pgm_rollout')
+                                int(carry), C.byref(launch_opts()), _stream()), 'pgm_rollout')
 
     def gae(self):
         check(lib().pgm_gae(C.byref(self.dims), C.byref(self.c_rb), self.gamma, self.gae_lambda, int(self.use_gae),
@@ -276,13 +276,14 @@ class TaskBatch:
         """pgm_ppo_update alone (packed rows + the update kernel) on the current stream."""
         check(lib().pgm_ppo_update(C.byref(self.dims), C.byref(self.hp), _ptr(self.params), _ptr(self.adam_m),
                                    _ptr(self.adam_v), _ptr(self.adam_step), _ptr(self.lr), _ptr(self.perms),
-                                   C.byref(self.c_rb), _ptr(self.stats), _ptr(self.update_ws), _stream()),
-              'pgm_ppo_update')
+                                   C.byref(self.c_rb), _ptr(self.stats), _ptr(self.update_ws),
+                                   C.byref(launch_opts()), _stream()), 'pgm_ppo_update')
 
     def update_variant(self):
         """The update kernel pgm_ppo_update launches for this batch (pgm_ppo_update_variant: the launcher's own rule)."""
         buf = C.create_string_buffer(128)
-        check(lib().pgm_ppo_update_variant(C.byref(self.dims), C.byref(self.hp), buf, 128), 'pgm_ppo_update_variant')
+        check(lib().pgm_ppo_update_variant(C.byref(self.dims), C.byref(self.hp), C.byref(launch_opts()), buf, 128),
+              'pgm_ppo_update_variant')
         return buf.value.decode()
 
     def take_update_failed(self):
@@ -309,7 +310,7 @@ class TaskBatch:
         out = self.objs if out is None else out
         check(lib().pgm_eval(C.byref(self.dims), _ptr(self.params), C.byref(self.c_spec), _ptr(mean), _ptr(var),
                              _ptr(self.s0_eval), self.eval_num, int(self.use_ob_rms), int(self.raw), self.gamma,
-                             _ptr(out), _stream()), 'pgm_eval')
+                             _ptr(out), C.byref(launch_opts()), _stream()), 'pgm_eval')
         return out
 
     @property

@@ -44,6 +44,8 @@ CONFIGS = {  # pop and the reference's per-env flags (scripts/*.py), iterations 
     # scripts/hopper-v3.py: 3 objectives, delta 0.25 (15 warm-up tasks), pbuffer-num 20, sparsity 1e6
     'MO-Hopper-v3': dict(delta='0.25', tasks=15, N=4, warmup=4, update=3, gens=3,
                          extra=['--pbuffer-num', '20', '--sparsity', '1000000.0']),
+    # scripts/halfcheetah-v2.py:37-51: delta 0.2 (6 warm-up tasks), num-tasks 6, eval-num 1; iterations scaled like Walker's
+    'MO-HalfCheetah-v2': dict(delta='0.2', tasks=6, N=4, warmup=4, update=3, gens=3, extra=[]),
     # config 4 reduced (scripts/humanoid-v2.py: N = 8, gamma 0.99, eval_num 6, warm-up 200 / update 40 iterations at
     # delta 0.2): 5 tasks (delta 0.25), warm-up 40 + 2 generations x 10 = 60 iterations, past the iteration (~34)
     # where the archive of non-negative points first fills (profiles/r04_humanoid_hv.json)

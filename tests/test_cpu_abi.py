@@ -42,8 +42,8 @@ def test_struct_sizes_match_header():
 #include <stdio.h>
 #include "pgm_abi.h"
 int main(void) {
-  printf("%zu %zu %zu %zu %zu %zu\n", sizeof(pgm_dims), sizeof(pgm_env_spec), sizeof(pgm_env_state),
-         sizeof(pgm_norm_state), sizeof(pgm_rollout_buf), sizeof(pgm_ppo_hparams));
+  printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(pgm_dims), sizeof(pgm_env_spec), sizeof(pgm_env_state),
+         sizeof(pgm_norm_state), sizeof(pgm_rollout_buf), sizeof(pgm_ppo_hparams), sizeof(pgm_launch_opts));
   return 0; }
 '''
     with tempfile.TemporaryDirectory() as d:
@@ -52,8 +52,61 @@ int main(void) {
         subprocess.run(['gcc', '-I', os.path.join(ROOT, 'include'), c, '-o', exe], check=True)
         sizes = [int(x) for x in subprocess.run([exe], capture_output=True, text=True).stdout.split()]
     want = [C.sizeof(s) for s in (_lib.Dims, _lib.EnvSpec, _lib.EnvState, _lib.NormState, _lib.RolloutBuf,
-                                   _lib.PPOHParams)]
+                                   _lib.PPOHParams, _lib.LaunchOpts)]
     assert sizes == want
+
+
+def test_production_library_reads_no_environment():
+    """ABI 4: every launch choice is a pgm_launch_opts argument.  The production libpgm.so imports no getenv (the
+    test hooks live only in libpgm_test.so, built -DPGM_TEST_HOOKS), and no source under csrc/ calls getenv outside
+    a PGM_TEST_HOOKS block."""
+    und = subprocess.run(['nm', '-D', '--undefined-only', _lib.LIB_PATH], capture_output=True, text=True).stdout
+    assert 'getenv' not in und
+    if os.path.exists(_lib.TEST_LIB_PATH):
+        und_t = subprocess.run(['nm', '-D', '--undefined-only', _lib.TEST_LIB_PATH], capture_output=True,
+                               text=True).stdout
+        assert 'getenv' in und_t  # the hooks are really in the test build
+    csrc = os.path.join(ROOT, 'pgmorl_amd', 'csrc')
+    for f in sorted(os.listdir(csrc)):
+        depth, hooked = 0, []
+        for i, line in enumerate(open(os.path.join(csrc, f)), 1):
+            t = line.strip()
+            if t.startswith('#if'):
+                hooked.append('PGM_TEST_HOOKS' in t)
+            elif t.startswith('#endif') and hooked:
+                hooked.pop()
+            if 'getenv' in line.split('//')[0]:
+                assert any(hooked), f'{f}:{i} calls getenv outside #ifdef PGM_TEST_HOOKS'
+
+
+def test_launch_opts_from_environment():
+    o = _lib.launch_opts({})
+    assert (o.update_kernel, o.update_split, o.fs_one_per_cu, o.rollout_kernel, o.eval_kernel) == (0, 0, 0, 0, 0)
+    o = _lib.launch_opts({'PGM_UPDATE_KERNEL': 'fs', 'PGM_FS_DUAL': '0', 'PGM_ROLLOUT_KERNEL': 'block'})
+    assert (o.update_kernel, o.fs_one_per_cu, o.rollout_kernel, o.eval_kernel) == (1, 1, 1, 0)
+    for sp, want in (('0', 1), ('1', 2), ('2', 3), ('4', 4)):
+        assert _lib.launch_opts({'PGM_UPDATE_SPLIT': sp, 'PGM_UPDATE_KERNEL': 'mfma'}).update_split == want
+    assert _lib.launch_opts({'PGM_UPDATE_KERNEL': 'valu', 'PGM_EVAL_KERNEL': 'block'}).eval_kernel == 1
+    with pytest.raises(_lib.PGMError):
+        _lib.launch_opts({'PGM_UPDATE_KERNEL': 'bogus'})
+    with pytest.raises(_lib.PGMError):
+        _lib.launch_opts({'PGM_UPDATE_SPLIT': '7'})
+
+
+def test_invalid_launch_opts_are_rejected_before_any_launch():
+    import ctypes as C
+    L = _lib.lib()
+    d = _lib.Dims(2, 4, 64, 17, 6, 2, 64)
+    hp = _lib.PPOHParams(0.2, 0.5, 0.0, 0.5, 1e-5, 0.9, 0.999, 0.0, 1, 2, 1, 0)
+    buf = C.create_string_buffer(128)
+    for bad in (_lib.LaunchOpts(update_kernel=9), _lib.LaunchOpts(update_split=-1), _lib.LaunchOpts(fs_one_per_cu=2),
+                _lib.LaunchOpts(rollout_kernel=3), _lib.LaunchOpts(eval_kernel=-1)):
+        assert L.pgm_ppo_update_variant(C.byref(d), C.byref(hp), C.byref(bad), buf, 128) == _lib.PGM_E_INVALID_ARG
+        assert b'pgm_launch_opts' in L.pgm_last_error()
+    # the VALU A/B choice is decided before any device query
+    valu = _lib.LaunchOpts(update_kernel=3)
+    assert L.pgm_ppo_update_variant(C.byref(d), C.byref(hp), C.byref(valu), buf, 128) == _lib.PGM_OK
+    assert buf.value == b'ppo_update_kernel (VALU, A/B)'
 
 
 def test_error_reporting_without_gpu():

@@ -2,7 +2,8 @@
 
 Every row-split update (MODE 2: each tower on two workgroups; t16: on four) hands gradient images over through
 16-B sc1 publishes + tagged flag granules, and the two towers hand their squared norms over through tagged 8-B
-granules, all double-buffered by Adam-step parity (pgm_common.hpp ppo_norm_granule).  PGM_TEST_DELAY stalls ONE
+granules, all double-buffered by Adam-step parity (pgm_common.hpp ppo_norm_granule).  PGM_TEST_DELAY (read only by
+the test build libpgm_test.so, -DPGM_TEST_HOOKS, which these tests run through _lib.test_build()) stalls ONE
 workgroup for a fixed number of cycles at one hand-off point of one step:
   where 0 -- before it publishes its gradient image (its partners spin on its flag),
   where 1 -- between its image flag store and its own partner poll (the partners run ahead to the next step),
@@ -17,6 +18,7 @@ import pytest
 import torch
 
 from oracle import ppo as oppo
+from pgmorl_amd import _lib
 from pgmorl_amd._lib import PGMError
 
 from .test_gpu_kernels import _close, _update_setup
@@ -37,7 +39,8 @@ def _run_update(env, P, T, N, E, M, split, delay, monkeypatch):
     obs, actions, logp, values, returns, adv = data
     lr = 3e-4
     tb.lr.fill_(lr)
-    tb.ppo_update(torch.stack(perms).numpy())
+    with _lib.test_build():
+        tb.ppo_update(torch.stack(perms).numpy())
     tb.check_update()  # PGMError if any spin-wait gave up
     for p in range(P):
         agent = oppo.PPO(pols[p], args.clip_param, E, M, args.value_loss_coef, args.entropy_coef, lr=lr, eps=1e-5,
@@ -134,8 +137,13 @@ def test_coresidency_check_refuses_an_oversized_grid(gpu, monkeypatch):
     # MODE 2 grid for 2 tasks: one group of 8 tasks' blocks (32 workgroups, 8 of them live; padding exits at once)
     monkeypatch.setenv('PGM_TEST_RESIDENT_CUS', '16')
     args, spec, tb, pols, data, perms = _update_setup('MO-Walker2d-v2', 2, 64, 4, 1, 1, seed=3)
-    with pytest.raises(PGMError, match='co-resident'):
+    with _lib.test_build():
+        with pytest.raises(PGMError, match='co-resident'):
+            tb.ppo_update(torch.stack(perms).numpy())
+        monkeypatch.setenv('PGM_TEST_RESIDENT_CUS', '32')  # exactly fits: runs
         tb.ppo_update(torch.stack(perms).numpy())
-    monkeypatch.setenv('PGM_TEST_RESIDENT_CUS', '32')  # exactly fits: runs
+    tb.check_update()
+    # the production library has no such hook: the same override changes nothing there
+    monkeypatch.setenv('PGM_TEST_RESIDENT_CUS', '16')
     tb.ppo_update(torch.stack(perms).numpy())
     tb.check_update()

@@ -85,8 +85,11 @@ def bytes_per_env_step(O, A, K, E):
     return 4 * ((O + A + 2 * K + 3) + (3 * K + 2) + (2 * K + 3) + E * (O + A + 2 * K + 2))
 
 
-def _cpu_task(args, spec, task, barrier, q):
-    """One reference-style task process (morl/morl.py:84-88): 1 thread (morl/morl.py:34), fp64 oracle."""
+def _cpu_task(args, spec, task, barrier, q, cpu=None):
+    """One reference-style task process (morl/morl.py:84-88): 1 thread (morl/morl.py:34), fp64 oracle, pinned to
+    logical CPU ``cpu`` (one per physical core, _pick_cores) when given."""
+    if cpu is not None:
+        os.sched_setaffinity(0, {cpu})
     torch.set_num_threads(1)
     from oracle.mopg import initial_sample, mopg_worker
     from pgmorl_amd import envspec
@@ -117,6 +120,52 @@ def _lscpu():
         return f'lscpu unavailable ({e!r})'
 
 
+def _cpu_busy(cpus, window=1.0):
+    """Busy fraction of each logical CPU over ``window`` seconds (/proc/stat), {} if unreadable."""
+    def snap():
+        out = {}
+        with open('/proc/stat') as f:
+            for line in f:
+                if line.startswith('cpu') and line[3].isdigit():
+                    v = line.split()
+                    c, t = int(v[0][3:]), [int(x) for x in v[1:]]
+                    out[c] = (sum(t), t[3] + (t[4] if len(t) > 4 else 0))
+        return out
+    try:
+        a = snap()
+        time.sleep(window)
+        b = snap()
+    except OSError:
+        return {}
+    return {c: 1.0 - (b[c][1] - a[c][1]) / max(1, b[c][0] - a[c][0]) for c in cpus if c in a and c in b}
+
+
+def _pick_cores(n):
+    """n logical CPUs of the affinity mask on n distinct PHYSICAL cores (no SMT siblings: the topology from
+    /sys/devices/system/cpu/cpu*/topology), the idlest cores first (busy fraction of both siblings over 1 s), so the
+    baseline's processes neither share a core with each other nor land on a neighbour's busy core.  Returns
+    (cpus, info); cpus None when the topology is unreadable."""
+    avail = sorted(os.sched_getaffinity(0))
+    cores = {}
+    try:
+        for c in avail:
+            t = f'/sys/devices/system/cpu/cpu{c}/topology/'
+            key = (int(open(t + 'physical_package_id').read()), int(open(t + 'core_id').read()))
+            cores.setdefault(key, []).append(c)
+    except (OSError, ValueError) as e:
+        return None, {'pinning': f'none (topology unreadable: {e!r})'}
+    busy = _cpu_busy(avail)
+    own = os.sched_getaffinity(0)
+    ranked = sorted(cores.items(), key=lambda kv: (max(busy.get(c, 0.0) for c in kv[1]), kv[0]))
+    if len(ranked) < n:
+        return None, {'pinning': f'none ({len(ranked)} physical cores < {n} processes)'}
+    pick = [sibs[0] for _, sibs in ranked[:n]]
+    return pick, {'pinning': 'one process per physical core, no SMT siblings, idlest cores first',
+                  'cpus': pick, 'physical_cores_available': len(cores), 'own_mask_size': len(own),
+                  'picked_busy_max': max(busy.get(c, 0.0) for _, sibs in ranked[:n] for c in sibs) if busy else None,
+                  'all_cpus_busy_mean': float(np.mean(list(busy.values()))) if busy else None}
+
+
 def cpu_baseline(args, spec, tasks):
     """The reference's CPU path, whole-node: one single-thread fp64 oracle process per task
     (morl/morl.py:34,84-88), as many concurrent processes as this GPU's host-core share (16 on the box,
@@ -126,9 +175,12 @@ def cpu_baseline(args, spec, tasks):
     import multiprocessing as mp
     ncpu = len(os.sched_getaffinity(0))
     procs = max(1, min(args.cpu_procs, 15, ncpu, tasks))
+    cpus, pin = _pick_cores(procs)
+    load0 = os.getloadavg()
     ctx = mp.get_context('spawn')
     barrier, q = ctx.Barrier(procs), ctx.Queue()
-    ps = [ctx.Process(target=_cpu_task, args=(args, spec, i, barrier, q)) for i in range(procs)]
+    ps = [ctx.Process(target=_cpu_task, args=(args, spec, i, barrier, q, cpus[i] if cpus else None))
+          for i in range(procs)]
     hide = {k: os.environ.get(k) for k in ('HIP_VISIBLE_DEVICES', 'ROCR_VISIBLE_DEVICES')}
     os.environ['HIP_VISIBLE_DEVICES'] = os.environ['ROCR_VISIBLE_DEVICES'] = ''  # CPU-only children
     try:
@@ -149,6 +201,7 @@ def cpu_baseline(args, spec, tasks):
                 raise RuntimeError(f'cpu_baseline worker died: {[p.exitcode for p in ps]}')
     for p in ps:
         p.join(60)
+    load1 = os.getloadavg()
     t0, t1 = min(r[1] for r in res), max(r[2] for r in res)
     steps = sum(r[3] for r in res)
     value = steps / (t1 - t0)
@@ -159,7 +212,9 @@ def cpu_baseline(args, spec, tasks):
             'per_process': {'min': float(rates.min()), 'median': float(np.median(rates)), 'max': float(rates.max()),
                             'rel_sd': float(rates.std(ddof=1) / rates.mean()) if len(rates) > 1 else 0.0},
             'extrapolation': f'per-core value x 96 vCPUs (reference hardware, README.md:92-94)',
-            'host': {'affinity_cpus': ncpu, 'os_cpu_count': os.cpu_count(), 'lscpu': _lscpu()},
+            'host': {'affinity_cpus': ncpu, 'os_cpu_count': os.cpu_count(), 'lscpu': _lscpu(),
+                     'loadavg_before': list(load0), 'loadavg_after': list(load1)},
+            'pinning': pin,
             'sample': f'{procs} concurrent single-thread processes x {args.cpu_iters} MOPG iterations each '
                       f'({steps} train env-steps, T={args.num_steps}, N={args.num_processes}, E={args.ppo_epoch}, '
                       f'M={args.num_mini_batch}, + eval) of the fp64 torch/numpy oracle, {t1 - t0:.1f} s wall'}
@@ -169,7 +224,7 @@ def hv_comparison(env_name):
     """The newest committed full-algorithm device-vs-oracle HV comparison at an equal budget for this env
     (scripts/hv_full.py: warm-up + prediction-guided generations on both sides, per seed), summarised."""
     key = {'MO-Walker2d-v2': 'walker', 'MO-Hopper-v2': 'hopper', 'MO-Hopper-v3': 'hopper3',
-           'MO-Humanoid-v2': 'humanoid'}.get(env_name)
+           'MO-Humanoid-v2': 'humanoid', 'MO-HalfCheetah-v2': 'cheetah'}.get(env_name)
     if key is None:
         return None
     import re
@@ -188,20 +243,32 @@ def hv_comparison(env_name):
             continue
         hd_, ho_ = np.array(pairs).T
         # per-seed relative difference; when an oracle seed ends with an empty archive (HV 0: no point with every
-        # objective >= 0 at this budget, Humanoid), every difference is taken relative to the oracle's mean HV
-        scale = ho_ if (ho_ > 0).all() else np.full_like(ho_, ho_.mean())
-        rel = (hd_ - ho_) / scale
-        half = None
-        if len(rel) > 1:  # Student-t 95% interval of the mean per-seed difference
-            from scipy import stats
-            half = float(stats.t.ppf(0.975, len(rel) - 1) * rel.std(ddof=1) / np.sqrt(len(rel)))
+        # objective >= 0 at this budget, Humanoid), every difference is taken relative to the oracle's mean HV, and
+        # the verdict key changes with it (within_1pct_of_mean_at_95: not the per-seed statement); all oracle seeds
+        # empty: no relative difference at all
+        per_seed = bool((ho_ > 0).all())
+        if not per_seed and ho_.mean() <= 0:
+            rel, half = None, None
+        else:
+            scale = ho_ if per_seed else np.full_like(ho_, ho_.mean())
+            rel = (hd_ - ho_) / scale
+            half = None
+            if len(rel) > 1:  # Student-t 95% interval of the mean per-seed difference
+                from scipy import stats
+                half = float(stats.t.ppf(0.975, len(rel) - 1) * rel.std(ddof=1) / np.sqrt(len(rel)))
+        within = None if rel is None or half is None else bool(abs(rel.mean()) + half < 0.01)
+        rec = d.get('device_sources_hash')
         return {'source': [os.path.relpath(dev, ROOT), os.path.relpath(orc, ROOT)], 'config': d.get('config'),
-                'seeds': len(rel), 'hv_rel_diff_per_seed': [float(x) for x in rel],
-                'hv_rel_diff_mean': float(rel.mean()), 'ci95_half_width': half,
-                'within_1pct_at_95': None if half is None else bool(abs(rel.mean()) + half < 0.01),
+                'seeds': len(pairs), 'hv_rel_diff_per_seed': None if rel is None else [float(x) for x in rel],
+                'hv_rel_diff_mean': None if rel is None else float(rel.mean()), 'ci95_half_width': half,
+                'within_1pct_at_95': within if per_seed else None,
+                'within_1pct_of_mean_at_95': None if per_seed else within,
                 'hv_mean': {'device': float(hd_.mean()), 'oracle': float(ho_.mean())},
                 'empty_archive_seeds': {'device': int((hd_ == 0).sum()), 'oracle': int((ho_ == 0).sum())},
-                'normalised_by': 'per-seed oracle HV' if (ho_ > 0).all() else 'mean oracle HV'}
+                'normalised_by': 'per-seed oracle HV' if per_seed else 'mean oracle HV',
+                # the device side's kernel sources (scripts/hv_full.py records them): null = not recorded (older run)
+                'device_sources_hash': rec,
+                'device_at_head': None if rec is None else rec == device_sources_hash()}
     return None
 
 
@@ -284,6 +351,21 @@ KERNEL_SOURCES = {
     'ppo_update_fs_kernel': ['pgm_ppo_fs.hip'], 'ppo_update_wide_kernel': ['pgm_ppo_wide.hip'],
 }
 KERNEL_HEADERS = ['pgm_common.hpp', 'pgm_mfma.hpp', 'pgm_ppo_shared.hpp', 'pgm_dispatch.hpp']
+
+
+def device_sources_hash():
+    """sha256 (16 hex digits) of every device-path source (csrc/ except the host-only pgm_host.cpp) and the C ABI
+    header: what a device-side result (e.g. scripts/hv_full.py's HV runs) was produced with."""
+    import hashlib
+    h = hashlib.sha256()
+    d = os.path.join(ROOT, 'pgmorl_amd', 'csrc')
+    for f in sorted(os.listdir(d)):
+        if f.endswith(('.hip', '.hpp', '.cpp')) and f != 'pgm_host.cpp':
+            with open(os.path.join(d, f), 'rb') as fp:
+                h.update(f.encode() + b'\0' + fp.read())
+    with open(os.path.join(ROOT, 'include', 'pgm_abi.h'), 'rb') as fp:
+        h.update(fp.read())
+    return h.hexdigest()[:16]
 
 
 def kernel_source_hash(variant):

@@ -350,6 +350,9 @@ class _StateDictWriter:
         buf = bytearray(self.tmpl)
         for (off, size, lcrc, ccrc), arr in zip(self.rec, arrays):
             data = memoryview(np.ascontiguousarray(arr)).cast('B')
+            if data.nbytes != size:  # a slice assignment of another length would resize the zip silently
+                raise ValueError(f'EP template record of {size} bytes given {data.nbytes} bytes '
+                                 f'({getattr(arr, "dtype", "?")} {getattr(arr, "shape", "?")})')
             buf[off:off + size] = data
             if self.crc:
                 crc = zlib.crc32(data).to_bytes(4, 'little')

@@ -229,6 +229,9 @@ def main():
         env, seeds = a.env, a.seeds
     runs = [run_side(a.side, env, s, a.procs) for s in seeds]
     out = {'side': a.side, 'env': env, 'config': CONFIGS[env], 'runs': runs}
+    if a.side == 'device':  # the kernel sources these runs used (bench.hv_comparison flags a stale comparison)
+        from bench import device_sources_hash
+        out['device_sources_hash'] = device_sources_hash()
     if a.ref:
         cmp = []
         for r, o in zip(runs, ref['runs']):

@@ -63,7 +63,9 @@ def _check_update(env, P, N, E, M, mb, seed, entropy_coef=0.0, capacity=None, va
                                              ('MO-HalfCheetah-v2', 35, 4, 256, '1'),  # the same, a partial group
                                              ('MO-Hopper-v3', 27, 4, 256, '1'),      # NS 8, R 2, 2 per CU, 3 objectives
                                              ('MO-Hopper-v2', 5, 1, 64, '1'),        # NS 4, R 1 (config 0)
-                                             ('MO-Ant-v2', 3, 2, 128, '1')])         # NS 8, R 1, O = 27 (two dW1 blocks)
+                                             ('MO-Ant-v2', 3, 2, 128, '1'),          # NS 8, R 1, O = 27 (two dW1 blocks)
+                                             ('MO-Ant-v2', 20, 4, 256, '1'),         # R 2: packed actor loss, A = 8
+                                             ('MO-Ant-v2', 40, 4, 256, '1')])        # NS 6, R 3 where it fits
 def test_fs_update_all_tasks(gpu, monkeypatch, env, P, N, mb, dual):
     monkeypatch.setenv('PGM_UPDATE_KERNEL', 'fs')
     monkeypatch.setenv('PGM_FS_DUAL', dual)

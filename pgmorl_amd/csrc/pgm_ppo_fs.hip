@@ -899,10 +899,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 3 ? 2 
     }
 }
 
-// op 0: launch (dual: two workgroups per CU); op 1: 1 if two workgroups of this kernel fit one CU (LDS and registers), else 0
+// op 0: launch (dual: two workgroups per CU); op 1: 1 if two workgroups of this kernel fit one CU (LDS and registers),
+// else 0; op 2: 1 if one workgroup's LDS fits a CU (160 KiB), else 0
 template <int O, int A, int K, int NS, int R>
 static int launch_fs_k(const pgm_dims* d, const MArgs& a, bool dual, int op, hipStream_t stream) {
     const size_t smem = fs_smem_bytes<O, A, K, R>(dual || op == 1);
+    if (op == 2) return smem <= 160 * 1024 ? 1 : 0;
     if (smem > 160 * 1024) {
         set_error("pgm_ppo_update (fs): LDS %zu bytes exceeds 160 KiB", smem);
         return op == 1 ? 0 : PGM_E_UNSUPPORTED;
@@ -948,11 +950,12 @@ int fs_choose_ns(const pgm_dims* d, int mb, bool dual_ok, int* dual) {
         if (!fs_built(ns, R)) continue;
         const int grid = fs_grid(d->P, ns);
         if (grid > 2 * cus) continue;
-        if (grid <= cus) return ns;
+        MArgs q{};
+        q.hp.num_mini_batch = d->T * d->N / mb;
+        // (O = 27: 8 tiles per part overflow the LDS; the next NS down is taken instead)
+        if (grid <= cus && ppo_update_fs_op(d, q, ns, false, 2, nullptr) == 1) return ns;
         // two workgroups per CU for R = 2 / 3 (R 4 -> 2 pays; R 2 -> 1 does not: Walker P = 10 3.18 -> 3.70 ms)
-        if (dual_ok && (R == 2 || R == 3)) {
-            MArgs q{};
-            q.hp.num_mini_batch = d->T * d->N / mb;
+        if (grid > cus && dual_ok && (R == 2 || R == 3)) {
             if (ppo_update_fs_op(d, q, ns, true, 1, nullptr) == 1) {
                 *dual = 1;
                 return ns;
@@ -997,7 +1000,7 @@ int ppo_update_fs_op(const pgm_dims* d, const MArgs& a, int ns, bool dual, int o
         constexpr bool skip = false;
 #endif
         if constexpr (O > 32 || skip) {
-            return op == 1 ? 0 : PGM_E_UNSUPPORTED;
+            return op != 0 ? 0 : PGM_E_UNSUPPORTED;
         } else {
             switch (ns) {
                 case 2: return launch_fs_ns<O, A, K, 2>(d, a, R, dual, op, stream);

@@ -91,8 +91,7 @@ def test_block_of_inverts_the_kernel_maps():
 CASES = [('2', 0, 0, 0, 0), ('2', 0, 1, 1, 0), ('2', 0, 0, 1, 1), ('2', 0, 1, 0, 1), ('2', 0, 0, 0, 2), ('2', 0, 1, 1, 2),
          ('4', 0, 0, 0, 0), ('4', 0, 1, 3, 0), ('4', 0, 1, 2, 1), ('4', 0, 0, 0, 2), ('4', 0, 1, 0, 2), ('4', 0, 0, 3, 2),
          ('fs', 0, 0, 0, 0), ('fs', 1, 1, 15, 0), ('fs', 0, 1, 7, 1), ('fs', 1, 0, 3, 2), ('fs', 0, 1, 0, 2),
-         ('fs', 1, 1, 9, 3), ('fs', 0, 0, 15, 3),
-         ('fst', 0, 1, 4, 3), ('fst', 1, 0, 15, 3), ('fst', 0, 0, 0, 0), ('fst', 1, 1, 8, 2)]
+         ('fs', 1, 1, 9, 3), ('fs', 0, 0, 15, 3)]
 
 
 @pytest.mark.parametrize('split,task,tower,part,where', CASES)

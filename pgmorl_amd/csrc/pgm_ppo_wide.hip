@@ -264,7 +264,11 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
                     }
                     // ---- layer 1: Z1[s][u] = sum_k X[s][k] W1t[k][u]; X row of sample c, features h*KH + ks;
                     // groups of KG k-steps, three groups in flight ahead of the MFMAs
+#ifdef PGM_DIAG_XFIXED  // timing-only A/B (wrong results): every lane of a half streams ONE row (one line per load)
+                    const float4* xr = reinterpret_cast<const float4*>(obs + (size_t)S.rowid[w][0] * O + h * KH);
+#else
                     const float4* xr = reinterpret_cast<const float4*>(obs + (size_t)row * O + h * KH);
+#endif
                     f32x16 z[2] = {f32x16{0}, f32x16{0}};
                     // four register groups in rotation, each loaded three groups (24 MFMAs) ahead of its MFMAs;
                     // branch-free trips (the group count padded to a multiple of 4, padding groups read clamped
@@ -278,8 +282,13 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
                         if (g >= NG) x = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
                         for (int q = 0; q < KG; ++q) {
+#ifdef PGM_DIAG_WFIXED  // timing-only A/B (wrong results): W1 rows of the first group only (L1-resident)
+                            wv[q][0] = w1(h * KH + q, c);
+                            wv[q][1] = w1(h * KH + q, TS + c);
+#else
                             wv[q][0] = w1(h * KH + gg * KG + q, c);
                             wv[q][1] = w1(h * KH + gg * KG + q, TS + c);
+#endif
                         }
                     };
                     auto mfma_group = [&](const float4& x, const float (&wv)[KG][2]) {
@@ -476,7 +485,11 @@ PGM_UNROLL_W(PGM_UW_L2)
                         const bool live = u < nu && kf < O;
 #pragma unroll
                         for (int r = 0; r < 16; ++r) {
+#ifdef PGM_DIAG_DXFIXED  // timing-only A/B (wrong results): the dW1 gather reads one row per tile
+                            const int rr = S.rowid[u][0];
+#else
                             const int rr = S.rowid[u][rowof(r, h)];
+#endif
                             xv[r] = live ? obs[(size_t)rr * O + kf] : 0.f;
                         }
                     };

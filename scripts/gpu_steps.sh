@@ -39,7 +39,7 @@ for step in "$@"; do
       python -c "import json;d=json.load(open('$OUT/sq_${TAG}_$name.json'));pw=d.get('per_wave',{});sh=d.get('share_of_wave_cycles',{});print('$name', d['kernel'][:60], 'ns', round(d['kernel_ns_profiled']), 'mfma_busy', round(d.get('mfma_busy_share',0),3), 'valu/mfma', round(pw.get('VALU',0)/max(pw.get('MFMA',1),1),2), 'lds_conf', round(d.get('lds_bank_conflict_per_active_lds',0),3), 'wait_any', round(sh.get('SQ_WAIT_ANY',0),3))" ;;
     pmc) bash scripts/pmc.sh ${TAG}_$name $args > /dev/null || { echo PMC $name FAILED; exit 1; }
       python -c "import json;d=json.load(open('$OUT/pmc_${TAG}_$name.json'));print('$name', d['variant'], d['source_hash'], round(d['hbm_bytes_per_launch']/1e9,3),'GB')" ;;
-    stamps) timeout -k 10 300 env $args PGM_LIB=pgmorl_amd/libpgm_stamps.so python -u scripts/stamps.py > $OUT/stamps_${TAG}_$name.txt 2>&1 || { echo STAMPS $name FAILED; tail -5 $OUT/stamps_${TAG}_$name.txt; exit 1; }
+    stamps) timeout -k 10 300 env PGM_LIB=pgmorl_amd/libpgm_stamps.so $args python -u scripts/stamps.py > $OUT/stamps_${TAG}_$name.txt 2>&1 || { echo STAMPS $name FAILED; tail -5 $OUT/stamps_${TAG}_$name.txt; exit 1; }
       tail -4 $OUT/stamps_${TAG}_$name.txt ;;
     hv) timeout -k 10 1100 python -u scripts/hv_full.py device --ref $args --out $OUT/${TAG}_hvfull_$name.json > $OUT/${TAG}_hv_$name.log 2>&1 || { echo HV $name FAILED; tail -20 $OUT/${TAG}_hv_$name.log; exit 1; }
       tail -c 400 $OUT/${TAG}_hv_$name.log ;;

@@ -9,7 +9,8 @@
 #   check                   scripts/round_check.sh TAG --no-tests (bench line + whole run + cpu_baseline + kernel stats)
 #   configs                 scripts/configs_check.sh TAG (every BASELINE config's per-GPU line + strong-scaling loads)
 #   bench=NAME:ARGS         one bench line (no cpu baseline / whole run) -> bench_TAG_NAME.json
-#   sq=NAME:ARGS            SQ counters of the update kernel (scripts/sq_counters.sh)
+#   sq=NAME[@KERNEL]:ARGS   SQ counters of the update kernel, or of the kernel whose name contains KERNEL
+#                           (scripts/sq_counters.sh)
 #   pmc=NAME:ARGS           FETCH/WRITE_SIZE of the update kernel (scripts/pmc.sh)
 #   stamps=NAME:VARS        phase stamps (libpgm_stamps.so prebuilt with `python -m pgmorl_amd.build --stamps`,
 #                           scripts/stamps.py; VARS = its environment, e.g. ENV=MO-Humanoid-v2,P=20)
@@ -35,7 +36,8 @@ for step in "$@"; do
     bench)
       timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-whole-run $args > $OUT/bench_${TAG}_$name.json 2> $OUT/bench_${TAG}_$name.err || { echo BENCH $name FAILED; tail -5 $OUT/bench_${TAG}_$name.err; exit 1; }
       python -c "import json;d=json.load(open('$OUT/bench_${TAG}_$name.json'));r=d['roofline'];print('$name', round(d['value']/1e6,3),'M/s', round(d['ms_per_step'],3),'ms/step', r['kernel'], round(r['avg_launch_ms'],3),'ms frac', round(r['frac'],4))" ;;
-    sq) bash scripts/sq_counters.sh ${TAG}_$name $args > /dev/null || { echo SQ $name FAILED; exit 1; }
+    sq) kern=ppo_update; if [ "${name#*@}" != "$name" ]; then kern=${name#*@}; name=${name%@*}; fi
+      SQ_KERNEL=$kern bash scripts/sq_counters.sh ${TAG}_$name $args > /dev/null || { echo SQ $name FAILED; exit 1; }
       python -c "import json;d=json.load(open('$OUT/sq_${TAG}_$name.json'));pw=d.get('per_wave',{});sh=d.get('share_of_wave_cycles',{});print('$name', d['kernel'][:60], 'ns', round(d['kernel_ns_profiled']), 'mfma_busy', round(d.get('mfma_busy_share',0),3), 'valu/mfma', round(pw.get('VALU',0)/max(pw.get('MFMA',1),1),2), 'lds_conf', round(d.get('lds_bank_conflict_per_active_lds',0),3), 'wait_any', round(sh.get('SQ_WAIT_ANY',0),3))" ;;
     pmc) bash scripts/pmc.sh ${TAG}_$name $args > /dev/null || { echo PMC $name FAILED; exit 1; }
       python -c "import json;d=json.load(open('$OUT/pmc_${TAG}_$name.json'));print('$name', d['variant'], d['source_hash'], round(d['hbm_bytes_per_launch']/1e9,3),'GB')" ;;

@@ -7,10 +7,14 @@ XCDs, so the effective clock is GRBM_GUI_ACTIVE / 8 / kernel time.  WAIT_ANY + W
 Usage: sq_summary.py DIR [bench args]; prints one JSON object.  Measurement tool, not product code.
 """
 import csv
+import os
 import glob
 import json
 import sys
 from collections import defaultdict
+
+
+KFILTER = os.environ.get('SQ_KERNEL', 'ppo_update')  # kernel-name substring (e.g. rollout_lane for the rollout)
 
 
 def load(d):
@@ -19,7 +23,7 @@ def load(d):
     for f in sorted(glob.glob(f'{d}/g*/**/*counter_collection.csv', recursive=True)):
         gp = f[len(d):].split('/')[1]
         for row in csv.DictReader(open(f)):
-            if 'ppo_update' not in row['Kernel_Name']:
+            if KFILTER not in row['Kernel_Name']:
                 continue
             key = (gp, row['Dispatch_Id'])
             per[key][row['Counter_Name']] += float(row['Counter_Value'])
@@ -27,7 +31,7 @@ def load(d):
                          int(row.get('VGPR_Count') or 0), int(row.get('Accum_VGPR_Count') or 0),
                          int(row.get('LDS_Block_Size') or 0), int(row['End_Timestamp']) - int(row['Start_Timestamp']))
     if not per:
-        raise SystemExit(f'no ppo_update dispatches under {d}')
+        raise SystemExit(f'no {KFILTER} dispatches under {d}')
     # average every counter over the dispatches of its pass
     sums, counts, dur = defaultdict(float), defaultdict(int), []
     for key, cs in per.items():
@@ -53,7 +57,7 @@ def main():
            'kernel': name, 'grid_threads': grid, 'workgroup': wg, 'vgpr': vgpr, 'agpr': agpr, 'lds_bytes': lds,
            'kernel_ns_profiled': ns, 'counters_per_launch': c,
            'method': 'rocprofv3 --pmc, 2 passes (8 SQ + GRBM / 8 SQ), --kernel-trace only; per-dispatch sums '
-                     'averaged over the ppo_update dispatches of each pass'}
+                     f'averaged over the {KFILTER} dispatches of each pass'}
     if waves:
         out['waves'] = waves
         out['wave_lifetime_cycles'] = wave_cyc / waves

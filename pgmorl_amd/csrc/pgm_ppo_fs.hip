@@ -138,8 +138,6 @@ __host__ __device__ __forceinline__ int frag_img(int b, int l, int r, int m) {
 }
 
 constexpr int SF = 72;  // fs activation-tile row stride (floats)
-// swizzled column of feature f in row s of the H1 tile (FsSmem::H1s): f ^ 4 (s & 15), float4 groups stay whole
-__device__ __forceinline__ int h1x(int s, int f) { return f ^ ((s & 15) << 2); }
 
 template <int O, int A, int K, int R>
 struct FsSmem {
@@ -160,11 +158,7 @@ struct FsSmem {
     static constexpr bool HT = R <= 4 && R != 3;               // H1 also [feature][sample] (the dW2 A operand;
                                                                // R = 3: not, to fit two workgroups per CU)
     static constexpr int STT = HT ? 72 : 4;                    // its row stride (16 R <= 64 samples, = 8 mod 64)
-    // H1 of all tiles, all 64 features, XOR-swizzled (h1x): element (s, f) at column f ^ 4 (s & 15) of row s.  Its three
-    // access patterns -- the layer-1 stores (sample 4 g + r, feature c), the layer-2 ds_read_b128 (sample c, features
-    // 4 g .. 4 g + 3) and the dW2 A-operand ds_read_b32 (sample 4 g + r, feature c) -- are then all conflict-free
-    // (a 72-float stride left the last one 2-way: lanes g and g + 1 on one bank)
-    alignas(16) float H1s[SB][H];
+    alignas(16) float H1s[SB][SF];                             // H1 of all tiles, all 64 features
     alignas(16) float H2s[SB][SF];                             // H2 (R >= 8: then dZ2)
     alignas(16) float Zs[ZA ? 1 : SB][SF];                     // dZ2
     alignas(16) float H1T[HT ? H : 1][STT];                    // H1 transposed (R <= 4)
@@ -391,7 +385,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 3 ? 2 
                 if constexpr (NC == 2) zz += z[ti][1];
                 tanh_bias_pk<4>(zz, bias, H1[ti]);
 #pragma unroll
-                for (int r = 0; r < 4; ++r) S.H1s[16 * ti + 4 * g + r][h1x(4 * g + r, fb + c)] = H1[ti][r];
+                for (int r = 0; r < 4; ++r) S.H1s[16 * ti + 4 * g + r][fb + c] = H1[ti][r];
                 if constexpr (Sm::HT)
                     *reinterpret_cast<float4*>(&S.H1T[fb + c][16 * ti + 4 * g]) =
                         make_float4(H1[ti][0], H1[ti][1], H1[ti][2], H1[ti][3]);
@@ -420,7 +414,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 3 ? 2 
             for (int i = 0; i < 4; ++i) bw[i] = Wt.W2t[16 * j + 4 * g + i][fb + c];
 #pragma unroll
             for (int ti = 0; ti < R; ++ti) {
-                const float4 a4 = *reinterpret_cast<const float4*>(&S.H1s[16 * ti + c][h1x(c, 16 * j + 4 * g)]);
+                const float4 a4 = *reinterpret_cast<const float4*>(&S.H1s[16 * ti + c][16 * j + 4 * g]);
                 const float av[4] = {a4.x, a4.y, a4.z, a4.w};
 #pragma unroll
                 for (int i = 0; i < 4; ++i) z[ti][(4 * j + i) % NC] = mfma16(av[i], bw[i], z[ti][(4 * j + i) % NC]);
@@ -638,7 +632,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 3 ? 2 
                 for (int r = 0; r < 4; ++r)
 #pragma unroll
                     for (int ib = 0; ib < 4; ++ib)
-                        gW2[ib] = mfma16(S.H1s[16 * ti + 4 * g + r][h1x(4 * g + r, 16 * ib + c)], dZ2[ti][r], gW2[ib]);
+                        gW2[ib] = mfma16(S.H1s[16 * ti + 4 * g + r][16 * ib + c], dZ2[ti][r], gW2[ib]);
             }
         }
         // this wave's dW2 / head-weight blocks are final: out now (write-through under the dH1 / dW1 pass)

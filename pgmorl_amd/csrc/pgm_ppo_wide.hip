@@ -480,9 +480,6 @@ PGM_UNROLL_W(PGM_UW_L2)
                 {
                     const int nu = min(4, (mbs - ps * 4 * TS + TS - 1) / TS);  // tiles of this pass
                     constexpr int NR = NKW * 4;                                // rounds (j, u)
-                    // (a branch-free form of these rounds -- conditions compile-time true for ONE, clamped gather rows,
-                    // dZ1 operands read four samples ahead -- ran out of registers: the gather serialised behind
-                    // vmcnt(0) on one reused register and the spills doubled, 304 -> 608 B)
                     auto gather = [&](int rd, float (&xv)[16]) {
                         const int j = rd >> 2, u = rd & 3, kf = (w + 4 * j) * TS + c;
                         const bool live = u < nu && kf < O;
@@ -598,25 +595,6 @@ PGM_UNROLL_W(PGM_UW_L2)
             const int kb = opaque(w * TS + 4 * h);           // lane's first layer-1 row (feature)
             const int fb = opaque(offW1 + kb * H + c);       // ... its flat parameter index
             auto krow = [&](int j, int r) { return 4 * j * TS + (r & 3) + 8 * (r >> 2); };  // row - kb of value r
-            auto live = [&](int j, int r) { return w + 4 * j < NKT && kb + krow(j, r) < O; };
-            // Adam operands of this part's layer-1 slice (moments + parameters; nothing writes them before this step's
-            // Adam): with every block in one batch (NS = 4: 24 values per lane) they are loaded at the start of the
-            // partner gather, so their HBM round trip hides under it instead of opening the Adam phase
-            constexpr int CB = RS >= 16 ? 1 : RS >= 8 ? 3 : NB;  // blocks per batch of Adam loads
-            constexpr bool PREF = CB == NB;
-            float pfm[PREF ? NB : 1][RS], pfv[PREF ? NB : 1][RS], pfp[PREF ? NB : 1][RS];
-            auto adam_loads = [&](int b0, float (*bm)[RS], float (*bv)[RS], float (*bp)[RS]) {
-#pragma unroll
-                for (int bb = 0; bb < CB; ++bb)
-#pragma unroll
-                    for (int ri = 0; ri < RS; ++ri) {
-                        const int b = b0 + bb, j = b >> 1, ib = b & 1, r = rbase + ri;
-                        const int f = b < NB && live(j, r) ? fb + krow(j, r) * H + ib * TS : offW1;
-                        bm[bb][ri] = Mo[f];
-                        bv[bb][ri] = Vo[f];
-                        bp[bb][ri] = P[f];
-                    }
-            };
             const unsigned tag = (unsigned)(nstep + 1);
             const int par = nstep & 1;
             auto slot_of = [&](int hh) { return ((p * 2 + m) * NS + hh) * 2 + par; };
@@ -699,7 +677,6 @@ PGM_UNROLL_W(PGM_UW_L2)
                     for (int hh = 0; hh < NS; ++hh) ls = hh == 0 ? S.red[24] : ls + S.red[24 + hh];  // part order
                     S.red[12] = ls;
                 }
-                if constexpr (PREF) adam_loads(0, pfm, pfv, pfp);
                 {  // this part's dW1 slice from every other part: all loads in flight, then the part-order sums
                     float ov[NS > 1 ? NS - 1 : 1][NB][RS];
 #pragma unroll
@@ -815,23 +792,23 @@ PGM_UNROLL_W(PGM_UW_L2)
                 const float den = __builtin_amdgcn_sqrtf(vv) * inv_bc2s + eps;
                 pp -= step_size * mm * __builtin_amdgcn_rcpf(den);
             };
+            auto live = [&](int j, int r) { return w + 4 * j < NKT && kb + krow(j, r) < O; };
             {
-                // loads of CB blocks in flight at a time (all of them at NS = 4: prefetched under the partner gather)
+                // loads of CB blocks in flight at a time (all of them at NS = 4)
+                constexpr int CB = RS >= 16 ? 1 : RS >= 8 ? 3 : NB;
 #pragma unroll
                 for (int b0 = 0; b0 < NB; b0 += CB) {
                     float bm[CB][RS], bv[CB][RS], bp[CB][RS];
-                    if constexpr (PREF && NS > 1) {
 #pragma unroll
-                        for (int bb = 0; bb < CB; ++bb)
+                    for (int bb = 0; bb < CB; ++bb)
 #pragma unroll
-                            for (int ri = 0; ri < RS; ++ri) {
-                                bm[bb][ri] = pfm[bb][ri];
-                                bv[bb][ri] = pfv[bb][ri];
-                                bp[bb][ri] = pfp[bb][ri];
-                            }
-                    } else {
-                        adam_loads(b0, bm, bv, bp);
-                    }
+                        for (int ri = 0; ri < RS; ++ri) {
+                            const int b = b0 + bb, j = b >> 1, ib = b & 1, r = rbase + ri;
+                            const int f = b < NB && live(j, r) ? fb + krow(j, r) * H + ib * TS : offW1;
+                            bm[bb][ri] = Mo[f];
+                            bv[bb][ri] = Vo[f];
+                            bp[bb][ri] = P[f];
+                        }
 #pragma unroll
                     for (int bb = 0; bb < CB; ++bb)
 #pragma unroll

@@ -409,6 +409,34 @@ def pmc_traffic(args, workload, kernel):
     return ent['hbm_bytes_per_launch'], ent['source']
 
 
+def sq_evidence(workload, kernel):
+    """The committed SQ-counter summary (scripts/sq_summary.py) of THIS workload's update launch from
+    profiles/sq_head.json, under the same rule as pmc_traffic (same pgm_ppo_update_variant string, same kernel
+    sources); (entry, None) or (None, reason)."""
+    try:
+        ent = json.load(open(os.path.join(ROOT, 'profiles', 'sq_head.json')))['entries'].get(workload)
+    except Exception as e:
+        return None, f'profiles/sq_head.json: {e!r}'
+    if not ent:
+        return None, f'no SQ summary for {workload}'
+    if not kernel or ent.get('variant') != kernel:
+        return None, f"SQ summary {ent.get('source')} is for {ent.get('variant')!r}, not {kernel!r}"
+    if ent.get('source_hash') != kernel_source_hash(kernel):
+        return None, f"SQ summary {ent.get('source')} measured other kernel sources (stale)"
+    return ent, None
+
+
+def limiter_of(sq):
+    """What bounds the priced kernel by its own counters: the f32 MFMA pipe when it is busy at least half the wave
+    lifetime, else latency (the dependent MFMA chains and the cross-CU hand-offs the waves wait on)."""
+    if sq is None:
+        return None
+    busy = sq.get('mfma_busy_share')
+    if busy is None:
+        return None
+    return 'mfma' if busy >= 0.5 else 'latency (hand-offs + dependent chains)'
+
+
 def launch_ranks(n):
     """``python bench.py --gpus N`` with no launcher around it: start N rank processes of this script, one per GPU,
     with the environment torch.distributed.run would give them (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR =
@@ -645,6 +673,7 @@ def main():
     achieved = upd_flop / (upd_ms * 1e-3) / 1e12 if upd_ms > 0 else 0.0
     kernel = main_leg['kernel']
     traffic, traffic_src = pmc_traffic(args, f'{args.env_name}/P{P}/N{N}/T{T}/E{E}/M{M}', kernel)
+    sq, sq_why = sq_evidence(f'{args.env_name}/P{P}/N{N}/T{T}/E{E}/M{M}', kernel)
     alg_bytes = P * T * N * E * 4 * (spec['obs_dim'] + spec['act_dim'] + 2 * spec['obj_num'] + 2)
     out = {
         'metric': METRIC, 'value': value, 'unit': 'env steps/sec', 'n_gpus': n_gpus, 'steps': args.steps,
@@ -658,7 +687,13 @@ def main():
                      'peak': PEAK_FP32_TFLOPS, 'unit': 'TFLOP/s', 'frac': achieved / PEAK_FP32_TFLOPS,
                      'traffic': traffic, 'traffic_source': traffic_src,
                      'traffic_vs_algorithmic': traffic / alg_bytes if traffic else None,
-                     'avg_launch_ms': upd_ms, 'flop_per_launch': upd_flop, 'algorithmic_bytes_per_launch': alg_bytes},
+                     'avg_launch_ms': upd_ms, 'flop_per_launch': upd_flop, 'algorithmic_bytes_per_launch': alg_bytes,
+                     # 'bound' names the roofline priced against (the dense f32 MFMA peak); 'limiter' what the kernel's
+                     # own SQ counters say holds it below that (profiles/sq_head.json, same variant and sources)
+                     'limiter': limiter_of(sq),
+                     'mfma_busy': sq.get('mfma_busy_share') if sq else None,
+                     'wait_any_share': sq.get('wait_any_share') if sq else None,
+                     'sq_source': sq.get('source') if sq else sq_why},
         # whole-iteration view: env-steps/s x algorithmic FLOP (or bytes) per env-step vs peak
         'path_roofline': {'flop_per_env_step': 2 * mf * (1 + 3 * E),
                           'compute_frac': value * 2 * mf * (1 + 3 * E) / (n_gpus * PEAK_FP32_TFLOPS * 1e12),

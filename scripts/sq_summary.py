@@ -53,7 +53,19 @@ def main():
     c, name, grid, wg, vgpr, agpr, lds, ns = load(d)
     waves = c.get('SQ_WAVES', 0.0)
     wave_cyc = 4.0 * c.get('SQ_WAVE_CYCLES', 0.0)
-    out = {'workload': f"{opt('--env-name', 'MO-Walker2d-v2')}/P{opt('--tasks', '40')}",
+    env, P, N = opt('--env-name', 'MO-Walker2d-v2'), opt('--tasks', '40'), opt('--num-processes', '4')
+    T, E, M = opt('--num-steps', '2048'), opt('--ppo-epoch', '10'), opt('--num-mini-batch', '32')
+    variant = None  # the launcher's own name of the profiled update (the bench line of pass 1)
+    try:
+        for line in open(os.path.join(d, 'g1.log')):
+            if line.startswith('{'):
+                variant = json.loads(line)['roofline']['kernel']
+    except (OSError, ValueError, KeyError):
+        pass
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import kernel_source_hash
+    out = {'workload': f'{env}/P{P}/N{N}/T{T}/E{E}/M{M}', 'variant': variant,
+           'source_hash': kernel_source_hash(variant) if KFILTER == 'ppo_update' else None,
            'kernel': name, 'grid_threads': grid, 'workgroup': wg, 'vgpr': vgpr, 'agpr': agpr, 'lds_bytes': lds,
            'kernel_ns_profiled': ns, 'counters_per_launch': c,
            'method': 'rocprofv3 --pmc, 2 passes (8 SQ + GRBM / 8 SQ), --kernel-trace only; per-dispatch sums '
@@ -72,6 +84,7 @@ def main():
             if k in c:
                 shares[k] = 4.0 * c[k] / wave_cyc
         out['share_of_wave_cycles'] = shares
+        out['wait_any_share'] = shares.get('SQ_WAIT_ANY')
         if 'SQ_VALU_MFMA_BUSY_CYCLES' in c:
             # one wave per SIMD in these kernels (256-thread WGs, one WG per CU): the MFMA pipe's busy share of
             # the SIMD's wave lifetime

@@ -705,20 +705,37 @@ PGM_UNROLL_W(PGM_UW_L2)
                             gs[b][ri] = acc;
                         }
                 }
-                for (int i = t; i < NV4; i += MT) {
-                    u32x4 pv[NS];
+                {  // the small images: every part's slot (this part's own too: the same bits it published), all
+                   // NS loads of the next trip in flight while this trip sums -- straight-line and branch-free (a
+                   // per-partner `hh != hs` test had made every trip a chain of branches, each value behind its
+                   // own vmcnt(0): ~6 serial round trips, 29 K cycles per Adam step with the dW1 slice loads)
+                    constexpr int NIT = (NV4 + MT - 1) / MT;
+                    u32x4 pa_[NS], pb_[NS];
+                    auto ld = [&](int it, u32x4 (&v)[NS]) {
+                        const int i = min(t + it * MT, NV4 - 1);  // (the tail trip re-reads a valid entry, unused)
 #pragma unroll
-                    for (int hh = 0; hh < NS; ++hh)
-                        if (hh != hs) pv[hh] = __builtin_amdgcn_raw_buffer_load_b128(xr, slot_of(hh) * a.xslot * 8 + 16 * i, 0, WSPLIT);
+                        for (int hh = 0; hh < NS; ++hh)
+                            v[hh] = __builtin_amdgcn_raw_buffer_load_b128(xr, slot_of(hh) * a.xslot * 8 + 16 * i, 0, WSPLIT);
+                    };
+                    ld(0, pa_);
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        float acc = 0.f;
+                    for (int it = 0; it < NIT; ++it) {
+                        u32x4(&cur)[NS] = (it & 1) ? pb_ : pa_;
+                        u32x4(&nxt)[NS] = (it & 1) ? pa_ : pb_;
+                        if (it + 1 < NIT) ld(it + 1, nxt);
+                        const int i = t + it * MT;
+                        if (i < NV4) {
 #pragma unroll
-                        for (int hh = 0; hh < NS; ++hh) {
-                            const float v = hh == hs ? G0[4 * i + q] : __uint_as_float(pv[hh][q]);
-                            acc = hh == 0 ? v : acc + v;
+                            for (int q = 0; q < 4; ++q) {
+                                float acc = 0.f;
+#pragma unroll
+                                for (int hh = 0; hh < NS; ++hh) {
+                                    const float v = __uint_as_float(cur[hh][q]);
+                                    acc = hh == 0 ? v : acc + v;
+                                }
+                                G0[4 * i + q] = acc;
+                            }
                         }
-                        G0[4 * i + q] = acc;
                     }
                 }
                 if (t < TAIL) {

@@ -677,33 +677,33 @@ PGM_UNROLL_W(PGM_UW_L2)
                     for (int hh = 0; hh < NS; ++hh) ls = hh == 0 ? S.red[24] : ls + S.red[24 + hh];  // part order
                     S.red[12] = ls;
                 }
-                {  // this part's dW1 slice from every other part: all loads in flight, then the part-order sums
-                    float ov[NS > 1 ? NS - 1 : 1][NB][RS];
-#pragma unroll
-                    for (int q = 0; q < NS - 1; ++q) {
-                        const int hh = q < hs ? q : q + 1;
+                {  // this part's dW1 slice: its own partial plus the other parts' in the fixed order hs + 1, hs + 2, ...
+                   // (each element has one owner, so any fixed order is deterministic), the next partner's loads in
+                   // flight while one is added.  (All three partners loaded at once beside the own partials -- 96 live
+                   // values -- went through scratch, each group of four loads behind a vmcnt(0).)
+                    float pb[2][NB][RS];
+                    auto ldp = [&](int q, float (&v)[NB][RS]) {
+                        int hh = hs + 1 + q;
+                        hh = hh >= NS ? hh - NS : hh;
 #pragma unroll
                         for (int j = 0; j < NKW; ++j)
 #pragma unroll
                             for (int ib = 0; ib < 2; ++ib)
 #pragma unroll
                                 for (int ri = 0; ri < RS; ++ri)
-                                    ov[q][j * 2 + ib][ri] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                                    v[j * 2 + ib][ri] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
                                         xr, dwb, slot_of(hh) * a.xslot * 8 + DW + 4 * (krow(j, rbase + ri) * H + ib * TS),
                                         WSPLIT));
+                    };
+                    ldp(0, pb[0]);
+#pragma unroll
+                    for (int q = 0; q < NS - 1; ++q) {
+                        if (q + 1 < NS - 1) ldp(q + 1, pb[(q + 1) & 1]);
+#pragma unroll
+                        for (int b = 0; b < NB; ++b)
+#pragma unroll
+                            for (int ri = 0; ri < RS; ++ri) gs[b][ri] += pb[q & 1][b][ri];
                     }
-#pragma unroll
-                    for (int b = 0; b < NB; ++b)
-#pragma unroll
-                        for (int ri = 0; ri < RS; ++ri) {
-                            float acc = 0.f;
-#pragma unroll
-                            for (int hh = 0; hh < NS; ++hh) {
-                                const float v = hh == hs ? gs[b][ri] : ov[hh < hs ? hh : hh - 1][b][ri];
-                                acc = hh == 0 ? v : acc + v;
-                            }
-                            gs[b][ri] = acc;
-                        }
                 }
                 {  // the small images: every part's slot (this part's own too: the same bits it published), all
                    // NS loads of the next trip in flight while this trip sums -- straight-line and branch-free (a
@@ -850,8 +850,9 @@ PGM_UNROLL_W(PGM_UW_L2)
                         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(gs[b][ri]), xr,
                                                               slot_of(hs) * a.xslot * 8 + DS + 4 * ((b * RS + ri) * MT + t), 0,
                                                               WSPLIT);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
+            // (the slice stores drain under the small image's Adam, an LDS-only loop: the wave's vmcnt(0) is taken
+            // after it, before the barrier that releases the flag store -- R1 order unchanged)
             for (int i = t; i < IMG; i += MT) {
                 float mm = S.MV[i], vv = S.MV[IMG + i], pp = Pf[i];
                 adam(G0[i], mm, vv, pp);
@@ -861,29 +862,36 @@ PGM_UNROLL_W(PGM_UW_L2)
                 if (m == 1 && i >= oLs && i < oLs + A) S.aiv[i - oLs] = expf(-2.f * pp);
             }
             if constexpr (NS > 1) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 lds_sync_m();  // every wave's slice stores drained
                 if (t == 0)
                     __hip_atomic_store(a.xb + (size_t)slot_of(hs) * a.xslot + a.xslot - 2, (unsigned long long)tag << 32,
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (t < NS && t != hs) spin(a.xb + (size_t)slot_of(t) * a.xslot + a.xslot - 2, tag);  // concurrent polls
                 lds_sync_m();
-                // the other parts' new slices -> this part's layer-1 copy
-#pragma unroll
-                for (int q = 0; q < NS - 1; ++q) {
+                // the other parts' new slices -> this part's layer-1 copy, the next part's loads in flight while one
+                // part's values are stored
+                float nvb[2][NB][RS];
+                auto ldn = [&](int q, float (&nv)[NB][RS]) {
                     const int hh = q < hs ? q : q + 1;
-                    float nv[NB][RS];
 #pragma unroll
                     for (int b = 0; b < NB; ++b)
 #pragma unroll
                         for (int ri = 0; ri < RS; ++ri)
                             nv[b][ri] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
                                 xr, slot_of(hh) * a.xslot * 8 + DS + 4 * ((b * RS + ri) * MT + t), 0, WSPLIT));
+                };
+                ldn(0, nvb[0]);
+#pragma unroll
+                for (int q = 0; q < NS - 1; ++q) {
+                    const int hh = q < hs ? q : q + 1;
+                    if (q + 1 < NS - 1) ldn(q + 1, nvb[(q + 1) & 1]);
 #pragma unroll
                     for (int b = 0; b < NB; ++b)
 #pragma unroll
                         for (int ri = 0; ri < RS; ++ri) {
                             const int j = b >> 1, ib = b & 1, r = RS * hh + ri;
-                            if (live(j, r)) P[fb + krow(j, r) * H + ib * TS] = nv[b][ri];
+                            if (live(j, r)) P[fb + krow(j, r) * H + ib * TS] = nvb[q & 1][b][ri];
                         }
                 }
             }

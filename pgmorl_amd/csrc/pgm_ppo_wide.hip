@@ -135,8 +135,8 @@ int wide_xslot_words(int O, int A, int K) {
     const int img = H * (H + 1) + Q * H + 2 * H + Q + A;
     const int nkt = (O + 31) / 32;
     const int nkw = (nkt + 3) / 4;
-    // small image | dW1 image | new-W1 slice [2 nkw 16/NS][256 threads] (NS >= 2) | 2 flag granules
-    return ((img + nkt * 32 * H + nkw * 16 * 256 + 1) / 2 + 2 + 31) / 32 * 32;  // 8-byte words, 256-B aligned
+    // small image (+ padding to 16 B) | dW1 block | new-W1 slices [2 nkw][16/NS][256 threads] (NS >= 2) | 2 flag granules
+    return ((img + 4 + nkt * 32 * H + nkw * 16 * 256 + 1) / 2 + 2 + 31) / 32 * 32;  // 8-byte words, 256-B aligned
 }
 
 namespace {
@@ -599,8 +599,13 @@ PGM_UNROLL_W(PGM_UW_L2)
             const int par = nstep & 1;
             auto slot_of = [&](int hh) { return ((p * 2 + m) * NS + hh) * 2 + par; };
             const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(a.xb, 0, a.xbytes, 0x00020000);
-            constexpr int DW = IMG * 4;                        // byte offset of the dW1 block inside a slot
+            // slot = small image | dW1 block [block b][quad q][thread][4] (lane t's values r = 4q .. 4q + 3 of register
+            // block b as one 16-B piece, so publish and gather are 16-B accesses, one contiguous KiB per wave and
+            // instruction) | new-W1 slices [b][quad][thread][4] | 2 flag granules
+            constexpr int DW = (IMG * 4 + 15) / 16 * 16;       // byte offset of the dW1 block inside a slot
             constexpr int DS = DW + NKT * TS * H * 4;          // byte offset of the new-W1-slice block
+            static_assert(NB * 16 * MT == NKT * TS * H, "dW1 exchange block: 16 values per lane and register block");
+            static_assert(RS % 4 == 0, "a part's slice is whole 16-B quads");
             auto spin = [&](const unsigned long long* fl, unsigned want) {  // one lane; bounded
                 unsigned long long x = 0;
                 for (unsigned spins = 0;; ++spins) {
@@ -650,15 +655,18 @@ PGM_UNROLL_W(PGM_UW_L2)
                     G0[4 * NV4 + t] = g;
                     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(g), xr, off_mine + 16 * NV4 + 4 * t, 0, WSPLIT);
                 }
-                const int dwb = opaque(4 * ((w * TS + 4 * h) * H + c));  // lane base of its dW1 elements
+                const int dwq = opaque(16 * t);  // this lane's 16-B piece of every (block, quad) row
 #pragma unroll
                 for (int j = 0; j < NKW; ++j)
 #pragma unroll
                     for (int ib = 0; ib < 2; ++ib)
 #pragma unroll
-                        for (int r = 0; r < 16; ++r)
-                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dW1[j][ib][r]), xr, dwb,
-                                                                  off_mine + DW + 4 * (krow(j, r) * H + ib * TS), WSPLIT);
+                        for (int q = 0; q < 4; ++q) {
+                            const u32x4 v = {__float_as_uint(dW1[j][ib][4 * q]), __float_as_uint(dW1[j][ib][4 * q + 1]),
+                                             __float_as_uint(dW1[j][ib][4 * q + 2]), __float_as_uint(dW1[j][ib][4 * q + 3])};
+                            __builtin_amdgcn_raw_buffer_store_b128(v, xr, dwq,
+                                                                   off_mine + DW + ((j * 2 + ib) * 4 + q) * MT * 16, WSPLIT);
+                        }
                 __builtin_amdgcn_sched_barrier(0);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 lds_sync_m();
@@ -686,14 +694,14 @@ PGM_UNROLL_W(PGM_UW_L2)
                         int hh = hs + 1 + q;
                         hh = hh >= NS ? hh - NS : hh;
 #pragma unroll
-                        for (int j = 0; j < NKW; ++j)
+                        for (int b = 0; b < NB; ++b)
 #pragma unroll
-                            for (int ib = 0; ib < 2; ++ib)
+                            for (int qq = 0; qq < RS / 4; ++qq) {
+                                const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(
+                                    xr, dwq, slot_of(hh) * a.xslot * 8 + DW + (b * 4 + (rbase >> 2) + qq) * MT * 16, WSPLIT);
 #pragma unroll
-                                for (int ri = 0; ri < RS; ++ri)
-                                    v[j * 2 + ib][ri] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-                                        xr, dwb, slot_of(hh) * a.xslot * 8 + DW + 4 * (krow(j, rbase + ri) * H + ib * TS),
-                                        WSPLIT));
+                                for (int e = 0; e < 4; ++e) v[b][4 * qq + e] = __uint_as_float(x[e]);
+                            }
                     };
                     ldp(0, pb[0]);
 #pragma unroll
@@ -842,14 +850,17 @@ PGM_UNROLL_W(PGM_UW_L2)
                         }
                 }
             }
-            if constexpr (NS > 1) {  // publish the new slice (4-B sc1 stores, [value][thread]), drain, flag
+            if constexpr (NS > 1) {  // publish the new slice (16-B sc1 stores, [block][quad][thread][4]), drain, flag
 #pragma unroll
                 for (int b = 0; b < NB; ++b)
 #pragma unroll
-                    for (int ri = 0; ri < RS; ++ri)
-                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(gs[b][ri]), xr,
-                                                              slot_of(hs) * a.xslot * 8 + DS + 4 * ((b * RS + ri) * MT + t), 0,
-                                                              WSPLIT);
+                    for (int qq = 0; qq < RS / 4; ++qq) {
+                        const u32x4 v = {__float_as_uint(gs[b][4 * qq]), __float_as_uint(gs[b][4 * qq + 1]),
+                                         __float_as_uint(gs[b][4 * qq + 2]), __float_as_uint(gs[b][4 * qq + 3])};
+                        __builtin_amdgcn_raw_buffer_store_b128(v, xr, 16 * t,
+                                                               slot_of(hs) * a.xslot * 8 + DS + (b * (RS / 4) + qq) * MT * 16,
+                                                               WSPLIT);
+                    }
             }
             // (the slice stores drain under the small image's Adam, an LDS-only loop: the wave's vmcnt(0) is taken
             // after it, before the barrier that releases the flag store -- R1 order unchanged)
@@ -877,9 +888,12 @@ PGM_UNROLL_W(PGM_UW_L2)
 #pragma unroll
                     for (int b = 0; b < NB; ++b)
 #pragma unroll
-                        for (int ri = 0; ri < RS; ++ri)
-                            nv[b][ri] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-                                xr, slot_of(hh) * a.xslot * 8 + DS + 4 * ((b * RS + ri) * MT + t), 0, WSPLIT));
+                        for (int qq = 0; qq < RS / 4; ++qq) {
+                            const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(
+                                xr, 16 * t, slot_of(hh) * a.xslot * 8 + DS + (b * (RS / 4) + qq) * MT * 16, WSPLIT);
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) nv[b][4 * qq + e] = __uint_as_float(x[e]);
+                        }
                 };
                 ldn(0, nvb[0]);
 #pragma unroll

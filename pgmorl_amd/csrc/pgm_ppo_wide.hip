@@ -909,9 +909,10 @@ PGM_UNROLL_W(PGM_UW_L2)
                         }
                 }
             }
-            // layer-1 stores land in L2, then this CU's L1 is invalidated: the next step's W1 stream (plain
-            // loads) must not hit lines cached before this update
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            // every layer-1 store of the step drained before any wave's next W1 stream.  No L1 invalidate: every
+            // byte of this workgroup's layer-1 copy is written by this workgroup (its own slice by the Adam above,
+            // the partners' slices from their sc1-loaded values), and one CU's own stores keep its L1 coherent
+            // (workgroup scope); the partners' bytes themselves only ever arrive through sc1 loads
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             lds_sync_m();
             PGM_STAMP(11);

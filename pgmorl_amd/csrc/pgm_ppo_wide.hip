@@ -9,10 +9,11 @@
 //     0..NS-1, so the NS Adam steps stay bitwise identical; the two towers exchange the squared gradient
 //     norm through one tagged granule per (step, row part) (the narrow kernel's protocol);
 //   * layer 1 (O x 64 = 96 KB) does not fit LDS next to the rest: the forward streams W1 through L1 (the
-//     four waves read the same rows; the L1 is invalidated after each layer-1 Adam step) and the observation
-//     rows straight from the rollout buffer (float4 per lane), both three 4-k-step groups ahead of the MFMAs.  Layer-1 k-steps pair features (h*KH + ks) of the two lane halves: any
-//     bijection between the MFMA's two k-slots and the features works as long as the A (X) and B (W1)
-//     operands use the same one;
+//     four waves read the same rows) and the observation rows straight from the rollout buffer (float4 per
+//     lane), both three 4-k-step groups ahead of the MFMAs; the rows were touched into L2 one Adam step
+//     earlier, under the previous step's exchange.  Layer-1 k-steps pair features (h*KH + ks) of the two
+//     lane halves: any bijection between the MFMA's two k-slots and the features works as long as the A (X)
+//     and B (W1) operands use the same one;
 //   * dW1 stays in REGISTERS: wave w owns the 32-feature tiles kt = w, w + 4, w + 8 of dW1 (96 accumulator
 //     registers) for the whole minibatch; every wave's dZ1 tile is shared through its LDS transpose tile, so
 //     each wave contracts its feature tiles over ALL samples of a pass, the observation values gathered from
@@ -94,6 +95,7 @@ struct WSmem {
     float red[32];  // [0,4) wave sums of squares, 4 norm total, [8,12) wave loss sums, 12 loss total,
                     // [16, 16 + 2 NS) norm parts, [24, 24 + NS) loss parts (one polling lane each)
     int32_t rowid[4][TS];  // rollout rows of every wave's tile of the current pass
+    int32_t nrowid[4][TS];  // ... of the next minibatch's first pass (prefetched into L2 under the exchange)
     float act2[4][TS][SCR];  // per-wave tile B: H2, then dZ2
     union Big {            // per-wave transpose tiles (dZ1 shared at the pass end), gradient images after
         float scr[4][TS][SCR];
@@ -197,6 +199,13 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
     auto w1 = [&](int k, int col) {  // W1^T[k][col]: through L1 (the 4 waves stream the same rows)
         return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(prs, (offW1 + k * H + col) * 4, 0, 0));
     };
+    // the task's observation rows as a buffer: a padding or dead element is a load at byte offset XOOB, past the
+    // range, which the hardware returns as 0.  (A select `ok ? load : 0` on the loaded value -- or a load under an
+    // exec mask -- made the compiler wait for the load right after issuing it: the layer-1 stream's X loads and the
+    // dW1 gather each lost their lookahead.)
+    constexpr int XOOB = (int)0x80000000u;
+    const __amdgpu_buffer_rsrc_t ors =
+        __builtin_amdgcn_make_buffer_rsrc((void*)obs, 0, (T + 1) * N * O * (int)sizeof(float), 0x00020000);
 
     // ---- small image + its Adam moments
     float* Pf = &S.Pm.W2t[0][0];
@@ -226,6 +235,9 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
     for (int e = 0; e < E; ++e) {
         for (int bb = 0; bb < nb; ++bb) {
             const int32_t* perm = a.perms + (size_t)e * B + bb * mb + r0;
+            // the next minibatch (the last step re-touches its own rows)
+            const bool has_next = bb + 1 < nb || e + 1 < E;
+            const int32_t* nperm = !has_next ? perm : bb + 1 < nb ? perm + mb : a.perms + (size_t)(e + 1) * B + r0;
             f32x16 gW2[2][2], gWh[2], dW1[NKW][2];
             float gB1[2], gB2[2];
             float gsm = 0.f;  // lanes q < Q: head-bias gradient q; lanes 32 + q (actor): logstd gradient q
@@ -246,6 +258,10 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
                 const bool ok = si < mbs;
                 const int row = perm[min(si, mbs - 1)];
                 if (h == 0) S.rowid[w][c] = row;
+                if (ps == 0) {
+                    const int nrow = nperm[min(si, mbs - 1)];
+                    if (h == 0) S.nrowid[w][c] = nrow;
+                }
                 if (ONE || i0 < mbs) {  // wave-uniform
                     // per-sample loss operands of this lane's sample, gathered now (random rows: an HBM round trip
                     // that the layer-1 stream hides) -- critic: old values, returns; actor: action, old logp, adv
@@ -265,21 +281,23 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
                     // ---- layer 1: Z1[s][u] = sum_k X[s][k] W1t[k][u]; X row of sample c, features h*KH + ks;
                     // groups of KG k-steps, three groups in flight ahead of the MFMAs
 #ifdef PGM_DIAG_XFIXED  // timing-only A/B (wrong results): every lane of a half streams ONE row (one line per load)
-                    const float4* xr = reinterpret_cast<const float4*>(obs + (size_t)S.rowid[w][0] * O + h * KH);
+                    const int xo = (S.rowid[w][0] * O + h * KH) * (int)sizeof(float);
 #else
-                    const float4* xr = reinterpret_cast<const float4*>(obs + (size_t)row * O + h * KH);
+                    const int xo = (row * O + h * KH) * (int)sizeof(float);  // byte offset of the lane's half row
 #endif
                     f32x16 z[2] = {f32x16{0}, f32x16{0}};
                     // four register groups in rotation, each loaded three groups (24 MFMAs) ahead of its MFMAs;
-                    // branch-free trips (the group count padded to a multiple of 4, padding groups read clamped
-                    // addresses and contribute X = 0) keep the loads outstanding across trips
-                    float4 xq[4];
-                    float wq[4][KG][2];
-                    constexpr int NGP = (NG + 3) / 4 * 4;
+                    // branch-free trips (the group count padded to a multiple of 4, padding groups read X = 0 past the
+                    // buffer's range and W1 at clamped addresses) keep the loads outstanding across trips
+                    constexpr int RING = 4;  // (6 or 7 groups in rotation: layer 1 slower, 54.6 -> 60.5 / 61.7 K cycles)
+                    float4 xq[RING];
+                    float wq[RING][KG][2];
+                    constexpr int NGP = (NG + RING - 1) / RING * RING;
                     auto load_group = [&](int g, float4& x, float (&wv)[KG][2]) {
                         const int gg = min(g, NG - 1);
-                        x = xr[gg];
-                        if (g >= NG) x = make_float4(0.f, 0.f, 0.f, 0.f);
+                        const u32x4 xv = __builtin_amdgcn_raw_buffer_load_b128(ors, g < NG ? xo + 16 * g : XOOB, 0, 0);
+                        x = make_float4(__uint_as_float(xv[0]), __uint_as_float(xv[1]), __uint_as_float(xv[2]),
+                                        __uint_as_float(xv[3]));
 #pragma unroll
                         for (int q = 0; q < KG; ++q) {
 #ifdef PGM_DIAG_WFIXED  // timing-only A/B (wrong results): W1 rows of the first group only (L1-resident)
@@ -300,13 +318,13 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
                         }
                     };
 #pragma unroll
-                    for (int b = 0; b < 4; ++b) load_group(b, xq[b], wq[b]);
+                    for (int b = 0; b < RING; ++b) load_group(b, xq[b], wq[b]);
 #pragma unroll 1
-                    for (int g = 0; g < NGP; g += 4) {
+                    for (int g = 0; g < NGP; g += RING) {
 #pragma unroll
-                        for (int b = 0; b < 4; ++b) {
+                        for (int b = 0; b < RING; ++b) {
                             mfma_group(xq[b], wq[b]);
-                            load_group(min(g + b + 4, NGP - 1), xq[b], wq[b]);
+                            load_group(min(g + b + RING, NGP - 1), xq[b], wq[b]);
                         }
                     }
                     // activations live in two per-wave LDS tiles, not registers (the 230 accumulator registers
@@ -482,7 +500,8 @@ PGM_UNROLL_W(PGM_UW_L2)
                     constexpr int NR = NKW * 4;                                // rounds (j, u)
                     auto gather = [&](int rd, float (&xv)[16]) {
                         const int j = rd >> 2, u = rd & 3, kf = (w + 4 * j) * TS + c;
-                        const bool live = u < nu && kf < O;
+                        // dead elements (features past O, tiles past the pass) at + XOOB: an integer add, not a select
+                        const int dead = u < nu && kf < O ? 0 : XOOB;
 #pragma unroll
                         for (int r = 0; r < 16; ++r) {
 #ifdef PGM_DIAG_DXFIXED  // timing-only A/B (wrong results): the dW1 gather reads one row per tile
@@ -490,7 +509,8 @@ PGM_UNROLL_W(PGM_UW_L2)
 #else
                             const int rr = S.rowid[u][rowof(r, h)];
 #endif
-                            xv[r] = live ? obs[(size_t)rr * O + kf] : 0.f;
+                            xv[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                                ors, (rr * O + kf) * (int)sizeof(float) + dead, 0, 0));
                         }
                     };
                     float xa[16], xb[16];
@@ -500,8 +520,12 @@ PGM_UNROLL_W(PGM_UW_L2)
                         float(&cur)[16] = (rd & 1) ? xb : xa;
                         float(&nxt)[16] = (rd & 1) ? xa : xb;
                         if (rd + 1 < NR) gather(rd + 1, nxt);
+                        // the next round's loads stay ahead of this round's MFMAs (no sinking / interleaving), and at
+                        // ONE with whole 4-tile groups the round is unconditional (a branch here let the compiler sink
+                        // the first gather into the round and wait for each load before its MFMA)
+                        __builtin_amdgcn_sched_barrier(0);
                         const int j = rd >> 2, u = rd & 3;
-                        if (u < nu && w + 4 * j < NKT) {
+                        if ((ONE || u < nu) && (NKT % 4 == 0 || w + 4 * j < NKT)) {
                             const float* dz = &S.big.scr[u][0][0];
 #pragma unroll
                             for (int r = 0; r < 16; ++r) {
@@ -516,6 +540,24 @@ PGM_UNROLL_W(PGM_UW_L2)
                 lds_sync_m();  // transpose tiles / row ids reused by the next pass
                 PGM_STAMP(6);
             }  // passes
+
+            // ---- the next minibatch's observation rows (this wave's tile of its first pass) into L2 while this step
+            // reduces, exchanges and updates: one 4-B touch per 128-B line of the lane's half row (and its last float),
+            // held in registers until the step's final vmcnt(0).  The layer-1 stream then meets L2 hits instead of
+            // HBM misses: layer 1 54.6 -> 39.6 K cycles per Adam step (the touches' issue costs the reduction ~2.7 K).
+            // (An LDS-DMA discard would hold no registers but puts a vmcnt(0) before the reduction's first LDS write:
+            // the compiler cannot tell the DMA's LDS target from the reduction's.  64-B touches, the two towers of a
+            // row part taking alternate lines, or the touches after the publish drain: no faster, or slower.)
+            constexpr int PF_NSEG = (KH * 4 + 127) / 128;
+            constexpr int NTOUCH = PF_NSEG + 1;
+            float pft[NTOUCH];
+            {
+                const int xo = (S.nrowid[w][c] * O + h * KH) * (int)sizeof(float);
+#pragma unroll
+                for (int i = 0; i < NTOUCH; ++i)
+                    pft[i] = __uint_as_float(
+                        __builtin_amdgcn_raw_buffer_load_b32(ors, xo + (i < PF_NSEG ? 128 * i : 4 * (KH - 1)), 0, 0));
+            }
 
             // ---- lane halves of the per-column partial sums; 64-lane sums of the per-sample ones
 #pragma unroll
@@ -595,6 +637,7 @@ PGM_UNROLL_W(PGM_UW_L2)
             const int kb = opaque(w * TS + 4 * h);           // lane's first layer-1 row (feature)
             const int fb = opaque(offW1 + kb * H + c);       // ... its flat parameter index
             auto krow = [&](int j, int r) { return 4 * j * TS + (r & 3) + 8 * (r >> 2); };  // row - kb of value r
+            auto live = [&](int j, int r) { return w + 4 * j < NKT && kb + krow(j, r) < O; };
             const unsigned tag = (unsigned)(nstep + 1);
             const int par = nstep & 1;
             auto slot_of = [&](int hh) { return ((p * 2 + m) * NS + hh) * 2 + par; };
@@ -817,7 +860,6 @@ PGM_UNROLL_W(PGM_UW_L2)
                 const float den = __builtin_amdgcn_sqrtf(vv) * inv_bc2s + eps;
                 pp -= step_size * mm * __builtin_amdgcn_rcpf(den);
             };
-            auto live = [&](int j, int r) { return w + 4 * j < NKT && kb + krow(j, r) < O; };
             {
                 // loads of CB blocks in flight at a time (all of them at NS = 4)
                 constexpr int CB = RS >= 16 ? 1 : RS >= 8 ? 3 : NB;
@@ -850,6 +892,7 @@ PGM_UNROLL_W(PGM_UW_L2)
                         }
                 }
             }
+            PGM_STAMP(12);
             if constexpr (NS > 1) {  // publish the new slice (16-B sc1 stores, [block][quad][thread][4]), drain, flag
 #pragma unroll
                 for (int b = 0; b < NB; ++b)
@@ -872,14 +915,17 @@ PGM_UNROLL_W(PGM_UW_L2)
                 Pf[i] = pp;
                 if (m == 1 && i >= oLs && i < oLs + A) S.aiv[i - oLs] = expf(-2.f * pp);
             }
+            PGM_STAMP(13);
             if constexpr (NS > 1) {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 lds_sync_m();  // every wave's slice stores drained
+                PGM_STAMP(14);
                 if (t == 0)
                     __hip_atomic_store(a.xb + (size_t)slot_of(hs) * a.xslot + a.xslot - 2, (unsigned long long)tag << 32,
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (t < NS && t != hs) spin(a.xb + (size_t)slot_of(t) * a.xslot + a.xslot - 2, tag);  // concurrent polls
                 lds_sync_m();
+                PGM_STAMP(15);
                 // the other parts' new slices -> this part's layer-1 copy, the next part's loads in flight while one
                 // part's values are stored
                 float nvb[2][NB][RS];
@@ -914,6 +960,8 @@ PGM_UNROLL_W(PGM_UW_L2)
             // the partners' slices from their sc1-loaded values), and one CU's own stores keep its L1 coherent
             // (workgroup scope); the partners' bytes themselves only ever arrive through sc1 loads
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int i = 0; i < NTOUCH; ++i) asm volatile("" ::"v"(pft[i]));  // the prefetch's values retire here
             lds_sync_m();
             PGM_STAMP(11);
         }  // minibatches
@@ -964,6 +1012,11 @@ int ppo_update_wide(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params,
     const int ns = wide_choose_ns(d, o);
     if (ns == 1 && 2 * d->P > cus) {
         set_error("pgm_ppo_update: the wide update needs 2P <= CUs (P=%d); shard the tasks over more GPUs", d->P);
+        return PGM_E_UNSUPPORTED;
+    }
+    if ((long long)(d->T + 1) * d->N * d->O * (long long)sizeof(float) >= (1ll << 31)) {
+        set_error("pgm_ppo_update: the wide update addresses a task's observations with 31-bit byte offsets "
+                  "((T+1) N O = %lld floats)", (long long)(d->T + 1) * d->N * d->O);
         return PGM_E_UNSUPPORTED;
     }
     const Layout L = make_layout(d->O, d->A, d->K, d->H);

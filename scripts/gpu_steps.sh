@@ -5,10 +5,11 @@
 #   bash scripts/gpu_steps.sh TAG STEP [STEP ...]
 # STEP:
 #   tests[=PYTEST_ARGS]     the -m gpu suite (default: all of it) -> gpu_tests_TAG.log
+#   testlib=LIB:PYTEST_ARGS the same against an A/B library (PGM_LIB=LIB) -> gpu_tests_TAG_ab.log
 #   smoke                   __graft_entry__.smoke()
 #   check                   scripts/round_check.sh TAG --no-tests (bench line + whole run + cpu_baseline + kernel stats)
 #   configs                 scripts/configs_check.sh TAG (every BASELINE config's per-GPU line + strong-scaling loads)
-#   bench=NAME:ARGS         one bench line (no cpu baseline / whole run) -> bench_TAG_NAME.json
+#   bench=NAME[@LIB]:ARGS   one bench line (no cpu baseline / whole run) -> bench_TAG_NAME.json; LIB: an A/B library
 #   sq=NAME[@KERNEL]:ARGS   SQ counters of the update kernel, or of the kernel whose name contains KERNEL
 #                           (scripts/sq_counters.sh)
 #   pmc=NAME:ARGS           FETCH/WRITE_SIZE of the update kernel (scripts/pmc.sh)
@@ -28,13 +29,17 @@ for step in "$@"; do
       timeout -k 10 1200 python -u -m pytest tests -m gpu -v --timeout 600 --timeout-method thread -p no:cacheprovider ${val//,/ } \
           > $OUT/gpu_tests_$TAG.log 2>&1 || { echo TESTS FAILED; grep -E "(FAILED|ERROR)" $OUT/gpu_tests_$TAG.log | head -20; tail -30 $OUT/gpu_tests_$TAG.log; exit 1; }
       tail -1 $OUT/gpu_tests_$TAG.log ;;
+    testlib)
+      timeout -k 10 1200 env PGM_LIB=$name python -u -m pytest tests -m gpu -v --timeout 600 --timeout-method thread -p no:cacheprovider $args \
+          > $OUT/gpu_tests_${TAG}_ab.log 2>&1 || { echo TESTS FAILED; grep -E "(FAILED|ERROR)" $OUT/gpu_tests_${TAG}_ab.log | head -20; tail -30 $OUT/gpu_tests_${TAG}_ab.log; exit 1; }
+      tail -1 $OUT/gpu_tests_${TAG}_ab.log ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke_$TAG.log 2>&1 || { echo SMOKE FAILED; tail -20 $OUT/smoke_$TAG.log; exit 1; }
       tail -1 $OUT/smoke_$TAG.log ;;
     check) bash scripts/round_check.sh $TAG --no-tests || exit 1 ;;
     configs) bash scripts/configs_check.sh $TAG || exit 1 ;;
-    bench)
-      timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-whole-run $args > $OUT/bench_${TAG}_$name.json 2> $OUT/bench_${TAG}_$name.err || { echo BENCH $name FAILED; tail -5 $OUT/bench_${TAG}_$name.err; exit 1; }
+    bench) lib=; if [ "${name#*@}" != "$name" ]; then lib=${name#*@}; name=${name%@*}; fi
+      timeout -k 10 300 env ${lib:+PGM_LIB=$lib} python -u bench.py --no-cpu-baseline --no-whole-run $args > $OUT/bench_${TAG}_$name.json 2> $OUT/bench_${TAG}_$name.err || { echo BENCH $name FAILED; tail -5 $OUT/bench_${TAG}_$name.err; exit 1; }
       python -c "import json;d=json.load(open('$OUT/bench_${TAG}_$name.json'));r=d['roofline'];print('$name', round(d['value']/1e6,3),'M/s', round(d['ms_per_step'],3),'ms/step', r['kernel'], round(r['avg_launch_ms'],3),'ms frac', round(r['frac'],4))" ;;
     sq) kern=ppo_update; if [ "${name#*@}" != "$name" ]; then kern=${name#*@}; name=${name%@*}; fi
       SQ_KERNEL=$kern bash scripts/sq_counters.sh ${TAG}_$name $args > /dev/null || { echo SQ $name FAILED; exit 1; }

@@ -41,7 +41,9 @@ wnames = {0: 'noise + layer-1 slices', 1: 'barrier A', 2: 'L1 sum, L2, head, dra
           4: 'dynamics', 5: 'objective wave sums', 6: 'reset + ob_rms + emit', 7: 'stats wave + barrier D'}
 unames = {0: 'layer 1 (L2 stream)', 1: 'layer 2 + tanh', 2: 'heads + loss', 3: 'gWh, dH2, gW2, dH1',
           4: 'pass barrier 1', 5: 'dW1 contraction', 6: 'pass barrier 2', 7: 'small-image reduction',
-          8: 'publish + flag wait', 9: 'gather partner', 10: 'sumsq + norm hand-off', 11: 'Adam (LDS + W1 HBM)'}
+          8: 'publish + flag wait', 9: 'gather partner', 10: 'sumsq + norm hand-off',
+          12: 'Adam: layer-1 slice (HBM)', 13: 'Adam: slice publish + image (LDS)', 14: 'Adam: slice drain',
+          15: 'Adam: slice flag wait', 11: 'Adam: partner slices -> copy'}
 fnames = {0: 'put W1/vec + L1', 11: 'put W2/Wh', 12: 'B1 wait', 1: 'L2 + H2 write', 13: 'B2 wait',
           14: 'Wh reads + head MFMAs', 15: 'loss VALU', 2: 'group sums', 3: 'B2b + gWh, dH2, gW2',
           4: 'B3 + dH1, gW1', 5: 'publish + drain + barrier', 6: 'image flag poll (+ row DMA)',

@@ -52,11 +52,13 @@ namespace pgm {
 
 namespace {
 
+constexpr int WHS = H + 4;  // head-weight row stride: 16-B rows (the VALU heads read them as b128) whose starts
+                            // fall on 8 bank quads (the reduction's column writes, lane = output q: 3-way, not 17-way)
 template <int A, int K>
 struct SmallImg {
     static constexpr int Q = qmax<A, K>();
     float W2t[H][SCR];
-    float Wh[Q][H];
+    float Wh[Q][WHS];
     float b1[H], b2[H], bh[Q], logstd[A];
 };
 template <int A, int K>
@@ -66,15 +68,15 @@ constexpr int simg_floats() { return (int)(sizeof(SmallImg<A, K>) / sizeof(float
 template <int A, int K>
 __device__ __forceinline__ int simg_to_flat(int i, int m, const Layout& L) {
     constexpr int Q = qmax<A, K>();
-    constexpr int s2 = H * SCR, s3 = s2 + Q * H, s4 = s3 + H, s5 = s4 + H, s6 = s5 + Q, s7 = s6 + A;
+    constexpr int s2 = H * SCR, s3 = s2 + Q * WHS, s4 = s3 + H, s5 = s4 + H, s6 = s5 + Q, s7 = s6 + A;
     const int NQ = m == 0 ? K : A;
     if (i < s2) {
         const int in = i / SCR, o = i - in * SCR;
         return o < H ? L.off[m ? PGM_P_ACTOR_W2 : PGM_P_CRITIC_W2] + in * H + o : -1;
     }
-    if (i < s3) {  // reference head weight [NQ][H] stored transposed [H][NQ]
-        const int j = i - s2, q = j / H, u = j - q * H;
-        return q < NQ ? L.off[m ? PGM_P_MEAN_W : PGM_P_VALUE_W] + u * NQ + q : -1;
+    if (i < s3) {  // reference head weight [NQ][H] stored transposed [H][NQ] (rows padded to WHS)
+        const int j = i - s2, q = j / WHS, u = j - q * WHS;
+        return q < NQ && u < H ? L.off[m ? PGM_P_MEAN_W : PGM_P_VALUE_W] + u * NQ + q : -1;
     }
     if (i < s4) return L.off[m ? PGM_P_ACTOR_B1 : PGM_P_CRITIC_B1] + (i - s3);
     if (i < s5) return L.off[m ? PGM_P_ACTOR_B2 : PGM_P_CRITIC_B2] + (i - s4);
@@ -134,7 +136,7 @@ struct WArgs {
 // exchange-slot geometry shared with the host-side workspace size (pgm_common.hpp declares it)
 int wide_xslot_words(int O, int A, int K) {
     const int Q = A > K ? A : K;
-    const int img = H * (H + 1) + Q * H + 2 * H + Q + A;
+    const int img = H * (H + 1) + Q * WHS + 2 * H + Q + A;
     const int nkt = (O + 31) / 32;
     const int nkw = (nkt + 3) / 4;
     // small image (+ padding to 16 B) | dW1 block | new-W1 slices [2 nkw][16/NS][256 threads] (NS >= 2) | 2 flag granules
@@ -159,7 +161,7 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
     static_assert(NG * KG == KH, "KH multiple of 4");
     constexpr int NKT = (O + TS - 1) / TS;  // 32-feature tiles of dW1
     constexpr int NKW = (NKT + 3) / 4;      // tiles owned per wave: kt = w + 4j
-    constexpr int oWh = H * SCR, oB1 = oWh + Q * H, oB2 = oB1 + H, oBh = oB2 + H, oLs = oBh + Q;
+    constexpr int oWh = H * SCR, oB1 = oWh + Q * WHS, oB2 = oB1 + H, oBh = oB2 + H, oLs = oBh + Q;
     const int t = threadIdx.x, w = t >> 6, l = t & 63, h = l >> 5, c = l & 31;
     // block map (NS > 1), groups of 8 NS blocks for 4 tasks; blocks b, b + 8, ... share an XCD under round-robin
     // dispatch (speed only: every hand-off is correct under any placement)
@@ -599,7 +601,7 @@ PGM_UNROLL_W(PGM_UW_L2)
                         for (int ob = 0; ob < 2; ++ob)
                             acc16([&](int r) { return (ib * TS + rowof(r, h)) * SCR + ob * TS + c; }, gW2[ib][ob]);
                         // head weights: gWh[ob] row rowof(r,h) = unit ob*32 + rowof, column c = output q (c < Q)
-                        if (c < Q) acc16([&](int r) { return oWh + c * H + ib * TS + rowof(r, h); }, gWh[ib]);
+                        if (c < Q) acc16([&](int r) { return oWh + c * WHS + ib * TS + rowof(r, h); }, gWh[ib]);
                         if (h == 0) {
                             acc(oB1 + ib * TS + c, gB1[ib]);
                             acc(oB2 + ib * TS + c, gB2[ib]);
@@ -613,6 +615,7 @@ PGM_UNROLL_W(PGM_UW_L2)
                         }
                         if (!add) {  // padding slots of a freshly written image
                             Gt[l * SCR + H] = 0.f;
+                            for (int i = l; i < Q * (WHS - H); i += 64) Gt[oWh + (i / (WHS - H)) * WHS + H + i % (WHS - H)] = 0.f;
                             if (l >= NQ && l < Q) Gt[oBh + l] = 0.f;
                             if (m == 0 && l < A) Gt[oLs + l] = 0.f;
                         }
@@ -676,8 +679,8 @@ PGM_UNROLL_W(PGM_UW_L2)
                         gs[j * 2 + ib][ri] = v;
                     }
             if constexpr (NS > 1) {
-                // ---- the parts' gradients: 16-B sc1 stores of the small image G0 + G1 and 4-B sc1 stores of the
-                // dW1 registers, every wave drains, barrier, one lane stores the tagged flag granule {step, loss
+                // ---- the parts' gradients: 16-B sc1 stores of the small image G0 + G1 and of the dW1 registers
+                // (all but this part's own slice, which no partner reads), every wave drains, barrier, one lane stores the tagged flag granule {step, loss
                 // sum} and polls the other parts' flags, barrier, sc1 loads of the other parts' small images and
                 // of THIS part's dW1 slice.  Sums in part order 0..NS-1 (the small-image Adam steps of the parts
                 // stay bitwise identical).  Slots are double-buffered by step parity.
@@ -705,6 +708,7 @@ PGM_UNROLL_W(PGM_UW_L2)
                     for (int ib = 0; ib < 2; ++ib)
 #pragma unroll
                         for (int q = 0; q < 4; ++q) {
+                            if (4 * q / RS == hs) continue;  // own slice: kept in registers, never read by a partner
                             const u32x4 v = {__float_as_uint(dW1[j][ib][4 * q]), __float_as_uint(dW1[j][ib][4 * q + 1]),
                                              __float_as_uint(dW1[j][ib][4 * q + 2]), __float_as_uint(dW1[j][ib][4 * q + 3])};
                             __builtin_amdgcn_raw_buffer_store_b128(v, xr, dwq,

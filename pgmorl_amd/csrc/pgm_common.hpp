@@ -62,12 +62,12 @@ inline size_t ppo_reset_bytes(const pgm_dims* d) {
 bool ws_take_zeroed(const void* ws, size_t need);
 // feature-split update (pgm_ppo_fs.hip): its exchange payload after the sample table (0 when it cannot run)
 size_t fs_workspace_extra(const pgm_dims* d);
-// obs_dim > 32 (wide kernel): flags, exchange slots [P][2 towers][NS parts][2 parities], parts 1..NS-1's
-// private [P][NS-1][L] parameter copies (sized for PGM_NS_MAX parts)
+// obs_dim > 32 (wide kernel): flags, exchange slots [P][2 towers][NS parts][2 parities], every workgroup's
+// layer-1 copy in k-quad layout [P][2 towers][NS parts][O H] (sized for PGM_NS_MAX parts)
 inline size_t ppo_workspace_bytes(const pgm_dims* d) {
     if (d->O > 32)
         return ppo_flag_bytes(d->P) + wide_xbuf_bytes(d) +
-               (size_t)d->P * (PGM_NS_MAX - 1) * make_layout(d->O, d->A, d->K, d->H).total * sizeof(float);
+               (size_t)d->P * 2 * PGM_NS_MAX * d->O * d->H * sizeof(float);
     return ppo_flag_bytes(d->P) + ppo_xbuf_bytes(d) +
            (size_t)d->P * d->T * d->N * ppo_row_stride(d->O, d->A, d->K) * sizeof(float) + fs_workspace_extra(d);
 }

@@ -23,8 +23,10 @@
 //     is an MFMA with the per-sample head gradients transposed through LDS.
 // Layer 1 (the bulk of the parameters) is sharded over the NS parts for the clip / Adam step: every part
 // sums, clips and updates only its slice of dW1 and hands the new weights to the others, which write them
-// into their own parameter copy (parts 1..NS-1 keep private parameter rows in the workspace, so no part
-// reads layer-1 weights another is rewriting; part 0 works on the caller's row).
+// into their own layer-1 copy.  Every workgroup streams W1 from a private copy in the workspace in k-quad
+// layout ([O/4][H][4]: a lane's four consecutive k-rows of one column are one 16-B load, a quarter of the
+// 4-B loads of the caller's row layout; the Adam slice and the partners' slices are 16-B accesses too), so no
+// part reads weights another is rewriting; part 0 writes layer 1 back to the caller's row at the end.
 #include <stdio.h>
 #include <stdlib.h>
 
@@ -119,7 +121,7 @@ struct WArgs {
     Layout L;
     pgm_ppo_hparams hp;
     float *params, *m, *v;  // caller's arrays (half 0)
-    float* copies;          // NS > 1: parts 1..NS-1's private parameter rows [P][NS-1][L]
+    float* copies;          // every workgroup's layer-1 copy, k-quad layout [P][2 towers][NS parts][O H]
     int32_t* step;
     const float* lr;
     const int32_t* perms;
@@ -185,8 +187,12 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
     const Layout& L = a.L;
     // parameters: part 0 the caller's row, parts 1..NS-1 private copies; Adam moments: the caller's rows for
     // every part (layer-1 elements are owned by one part each; the small image is written back by part 0 only)
-    float* __restrict__ P = hs == 0 ? a.params + (size_t)p * L.total
-                                    : a.copies + ((size_t)p * (NS - 1) + (hs - 1)) * L.total;
+    // parameters: the caller's row (the small image is read from it by every part, written back by part 0); layer 1
+    // lives in a private copy per workgroup in k-quad layout [O / 4][H][4] (W1^T[k][u] at (k / 4 H + u) 4 + k % 4),
+    // so a lane's four consecutive k-rows of one column are one 16-B load; part 0 writes it back at the end
+    float* __restrict__ P = a.params + (size_t)p * L.total;
+    float* __restrict__ Wq = a.copies + (((size_t)p * 2 + m) * NS + hs) * (size_t)(O * H);
+    auto qidx = [](int k, int u) { return ((k >> 2) * H + u) * 4 + (k & 3); };
     float* __restrict__ Mo = a.m + (size_t)p * L.total;
     float* __restrict__ Vo = a.v + (size_t)p * L.total;
     const int offW1 = L.off[m ? PGM_P_ACTOR_W1 : PGM_P_CRITIC_W1];
@@ -197,9 +203,9 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
     const float* vals = a.values + (size_t)p * (T + 1) * N * K;
     const float* rets = a.returns + (size_t)p * (T + 1) * N * K;
     // this workgroup's parameters as a buffer: layer-1 weights are re-read every tile with sc1 (L2) loads
-    const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(P, 0, L.total * 4, 0x00020000);
-    auto w1 = [&](int k, int col) {  // W1^T[k][col]: through L1 (the 4 waves stream the same rows)
-        return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(prs, (offW1 + k * H + col) * 4, 0, 0));
+    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(Wq, 0, O * H * 4, 0x00020000);
+    auto w1q = [&](int kq, int col) {  // W1^T[4 kq .. 4 kq + 3][col]: through L1 (the 4 waves stream the same rows)
+        return __builtin_amdgcn_raw_buffer_load_b128(wrs, (kq * H + col) * 16, 0, 0);
     };
     // the task's observation rows as a buffer: a padding or dead element is a load at byte offset XOOB, past the
     // range, which the hardware returns as 0.  (A select `ok ? load : 0` on the loaded value -- or a load under an
@@ -209,6 +215,11 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
     const __amdgpu_buffer_rsrc_t ors =
         __builtin_amdgcn_make_buffer_rsrc((void*)obs, 0, (T + 1) * N * O * (int)sizeof(float), 0x00020000);
 
+    // ---- this workgroup's layer-1 copy (k-quad layout) from the caller's W1; visible to every wave after the barrier
+    for (int i = t; i < O * H; i += MT) {
+        const int kq = i / (4 * H), rem = i - kq * 4 * H, u = rem >> 2, k = 4 * kq + (rem & 3);
+        Wq[i] = P[offW1 + k * H + u];
+    }
     // ---- small image + its Adam moments
     float* Pf = &S.Pm.W2t[0][0];
     if (t < A) S.aiv[t] = expf(-2.f * P[L.off[PGM_P_LOGSTD] + t]);
@@ -300,15 +311,12 @@ __global__ __launch_bounds__(MT) void ppo_update_wide_kernel(WArgs a) {
                         const u32x4 xv = __builtin_amdgcn_raw_buffer_load_b128(ors, g < NG ? xo + 16 * g : XOOB, 0, 0);
                         x = make_float4(__uint_as_float(xv[0]), __uint_as_float(xv[1]), __uint_as_float(xv[2]),
                                         __uint_as_float(xv[3]));
+                        static_assert(KG == 4 && KH % 4 == 0, "a group's k-rows are one k-quad");
+                        const u32x4 wa = w1q(h * (KH / 4) + gg, c), wb = w1q(h * (KH / 4) + gg, TS + c);
 #pragma unroll
                         for (int q = 0; q < KG; ++q) {
-#ifdef PGM_DIAG_WFIXED  // timing-only A/B (wrong results): W1 rows of the first group only (L1-resident)
-                            wv[q][0] = w1(h * KH + q, c);
-                            wv[q][1] = w1(h * KH + q, TS + c);
-#else
-                            wv[q][0] = w1(h * KH + gg * KG + q, c);
-                            wv[q][1] = w1(h * KH + gg * KG + q, TS + c);
-#endif
+                            wv[q][0] = __uint_as_float(wa[q]);
+                            wv[q][1] = __uint_as_float(wb[q]);
                         }
                     };
                     auto mfma_group = [&](const float4& x, const float (&wv)[KG][2]) {
@@ -875,10 +883,16 @@ PGM_UNROLL_W(PGM_UW_L2)
 #pragma unroll
                         for (int ri = 0; ri < RS; ++ri) {
                             const int b = b0 + bb, j = b >> 1, ib = b & 1, r = rbase + ri;
-                            const int f = b < NB && live(j, r) ? fb + krow(j, r) * H + ib * TS : offW1;
+                            const bool lv = b < NB && live(j, r);
+                            const int f = lv ? fb + krow(j, r) * H + ib * TS : offW1;
                             bm[bb][ri] = Mo[f];
                             bv[bb][ri] = Vo[f];
-                            bp[bb][ri] = P[f];
+                            if ((ri & 3) == 0) {  // the quad's four k-rows of one column: 16 B of the copy (0 past its range)
+                                const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(
+                                    wrs, lv ? qidx(kb + krow(j, r), ib * TS + c) * 4 : XOOB, 0, 0);
+#pragma unroll
+                                for (int e = 0; e < 4; ++e) bp[bb][ri + e] = __uint_as_float(v[e]);
+                            }
                         }
 #pragma unroll
                     for (int bb = 0; bb < CB; ++bb)
@@ -888,11 +902,17 @@ PGM_UNROLL_W(PGM_UW_L2)
                             if (b >= NB) continue;
                             adam(gs[b][ri], bm[bb][ri], bv[bb][ri], bp[bb][ri]);
                             gs[b][ri] = bp[bb][ri];
+                            if ((ri & 3) == 3) {  // the quad's new parameters as one 16-B store (dropped past the range)
+                                const int r0 = r - 3;
+                                const u32x4 v = {__float_as_uint(bp[bb][ri - 3]), __float_as_uint(bp[bb][ri - 2]),
+                                                 __float_as_uint(bp[bb][ri - 1]), __float_as_uint(bp[bb][ri])};
+                                __builtin_amdgcn_raw_buffer_store_b128(
+                                    v, wrs, live(j, r0) ? qidx(kb + krow(j, r0), ib * TS + c) * 4 : XOOB, 0, 0);
+                            }
                             if (!live(j, r)) continue;
                             const int f = fb + krow(j, r) * H + ib * TS;
                             Mo[f] = bm[bb][ri];
                             Vo[f] = bv[bb][ri];
-                            P[f] = bp[bb][ri];
                         }
                 }
             }
@@ -955,7 +975,12 @@ PGM_UNROLL_W(PGM_UW_L2)
 #pragma unroll
                         for (int ri = 0; ri < RS; ++ri) {
                             const int j = b >> 1, ib = b & 1, r = RS * hh + ri;
-                            if (live(j, r)) P[fb + krow(j, r) * H + ib * TS] = nvb[q & 1][b][ri];
+                            if ((ri & 3) == 0) {  // 16 B: the quad's four k-rows of one column
+                                const u32x4 v = {__float_as_uint(nvb[q & 1][b][ri]), __float_as_uint(nvb[q & 1][b][ri + 1]),
+                                                 __float_as_uint(nvb[q & 1][b][ri + 2]), __float_as_uint(nvb[q & 1][b][ri + 3])};
+                                __builtin_amdgcn_raw_buffer_store_b128(
+                                    v, wrs, live(j, r) ? qidx(kb + krow(j, r), ib * TS + c) * 4 : XOOB, 0, 0);
+                            }
                         }
                 }
             }
@@ -971,8 +996,9 @@ PGM_UNROLL_W(PGM_UW_L2)
         }  // minibatches
     }      // epochs
     PGM_STAMP_FLUSH;
-    if (hs != 0) return;  // parts 1..NS-1 worked on copies
-    // ---- write back the small image (layer 1 was updated in place)
+    if (hs != 0) return;  // parts 1..NS-1: copies only
+    // ---- write back layer 1 (part 0's copy holds every part's slice after the last step) and the small image
+    for (int i = t; i < O * H; i += MT) P[offW1 + i] = Wq[qidx(i / H, i - (i / H) * H)];
     for (int i = t; i < IMG; i += MT) {
         const int f = simg_to_flat<A, K>(i, m, L);
         if (f < 0) continue;
@@ -1038,11 +1064,11 @@ int ppo_update_wide(const pgm_dims* d, const pgm_ppo_hparams* hp, float* params,
         e = hipMemsetAsync(workspace, 0, flags + (ns > 1 ? xbytes : 0), stream);
         if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update (workspace reset)");
     }
-    const size_t row = (size_t)L.total * sizeof(float);
-    for (int hh = 1; hh < ns; ++hh) {  // parts 1..ns-1: private copies of every task's parameters
-        e = hipMemcpy2DAsync(copies + (size_t)(hh - 1) * L.total, (size_t)(ns - 1) * row, params, row, row, d->P,
-                             hipMemcpyDeviceToDevice, stream);
-        if (e != hipSuccess) return hip_fail(e, "pgm_ppo_update (part copies)");
+    // every workgroup's layer-1 copy [P][2 towers][ns parts][O H] (filled by the kernel) in the workspace's copy region,
+    // sized for PGM_NS_MAX parts (ppo_workspace_bytes)
+    if (ns > PGM_NS_MAX) {
+        set_error("pgm_ppo_update: wide layer-1 copies exceed the workspace (ns=%d)", ns);
+        return PGM_E_INVALID_ARG;
     }
     return dispatch_dims(d->O, d->A, d->K, "pgm_ppo_update", [&](auto o, auto aa, auto k) -> int {
         constexpr int O = decltype(o)::value, A = decltype(aa)::value, K = decltype(k)::value;

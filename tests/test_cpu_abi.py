@@ -173,8 +173,8 @@ def test_update_workspace_covers_every_split(env, P, N, T):
     exchange slots [P][2 towers][4 parts][2 parities], and the packed sample table + the feature-split payload
     (obs_dim <= 32: [P][2][NS][2] image slots of NB KiB and parameter slots of 4 ceil(ceil(NB / NS) / 4) KiB, NS = 16,
     the largest a launch with P' <= P tasks may pick, NB = 4 x 6 blocks for obs_dim <= 20 (compact fragments), else
-    4 (ceil(O / 16) + 6)) or the parts' private parameter
-    rows (wide)."""
+    4 (ceil(O / 16) + 6)) or every workgroup's layer-1 copy
+    [P][2 towers][4 parts][O H] (wide)."""
     from pgmorl_amd import envspec
     spec = envspec.make_spec(env)
     O, A, K, H = spec['obs_dim'], spec['act_dim'], spec['obj_num'], 64
@@ -192,12 +192,11 @@ def test_update_workspace_covers_every_split(env, P, N, T):
         fs = P * 2 * ns * 2 * (nb + 4 * -(-(-(-nb // ns)) // 4)) * 1024
         want = flags + P * 2 * 4 * 2 * xslot * 8 + P * T * N * rs * 4 + fs
     else:
-        img = H * (H + 1) + Q * H + 2 * H + Q + A
+        img = H * (H + 1) + Q * (H + 4) + 2 * H + Q + A  # head-weight rows padded to H + 4
         nkt = -(-O // 32)
         nkw = -(-nkt // 4)
-        xslot = -(-((img + nkt * 32 * H + nkw * 16 * 256 + 1) // 2 + 2) // 32) * 32
-        L = ParamLayout(O, A, K).total
-        want = flags + P * 2 * 4 * 2 * xslot * 8 + P * 3 * L * 4
+        xslot = -(-((img + 4 + nkt * 32 * H + nkw * 16 * 256 + 1) // 2 + 2) // 32) * 32
+        want = flags + P * 2 * 4 * 2 * xslot * 8 + P * 2 * 4 * O * H * 4  # + layer-1 copies [P][2][4][O H]
     assert got == want, (got, want)
 
 

@@ -537,12 +537,18 @@ PGM_UNROLL_W(PGM_UW_L2)
                         const int j = rd >> 2, u = rd & 3;
                         if ((ONE || u < nu) && (NKT % 4 == 0 || w + 4 * j < NKT)) {
                             const float* dz = &S.big.scr[u][0][0];
+                            // the round's B operands (dZ1 of tile u) read up front: one read per MFMA pair into the
+                            // same two registers had put an LDS round trip in front of every pair
+                            float bz[16][2];
 #pragma unroll
-                            for (int r = 0; r < 16; ++r) {
-                                const int s = rowof(r, h);
+                            for (int r = 0; r < 16; ++r)
 #pragma unroll
-                                for (int ib = 0; ib < 2; ++ib) dW1[j][ib] = mfma(cur[r], dz[s * SCR + ib * TS + c], dW1[j][ib]);
-                            }
+                                for (int ib = 0; ib < 2; ++ib) bz[r][ib] = dz[rowof(r, h) * SCR + ib * TS + c];
+                            __builtin_amdgcn_sched_barrier(0);  // (left alone, the scheduler sinks each read to its MFMA)
+#pragma unroll
+                            for (int r = 0; r < 16; ++r)
+#pragma unroll
+                                for (int ib = 0; ib < 2; ++ib) dW1[j][ib] = mfma(cur[r], bz[r][ib], dW1[j][ib]);
                         }
                     }
                 }

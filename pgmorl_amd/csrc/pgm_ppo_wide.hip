@@ -35,11 +35,10 @@
 
 PGM_STAMP_UNIT(wupd)
 
-// unroll depths of the layer-2 / dH1 and VALU-head loops (deeper unrolls: spills unchanged or higher)
+// unroll depth of the layer-2 / dH1 loops (deeper unrolls: spills unchanged or higher)
 #define PGM_PRAGMA_W(x) _Pragma(#x)
 #define PGM_UNROLL_W(n) PGM_PRAGMA_W(unroll n)
 #define PGM_UW_L2 8
-#define PGM_UW_HEAD 4
 // block map: the two towers of a row part on one XCD (they read the same observation rows in the same phase, so the
 // second read hits that XCD's L2): Humanoid P = 20 update 31.1 -> 30.4 ms, 56.2 -> 47.8 GB per launch against the
 // round-2 map, the NS parts of one tower on one XCD (profiles/r03o_*)
@@ -364,18 +363,34 @@ PGM_UNROLL_W(PGM_UW_L2)
                     }
                     wave_lds_fence();
                     PGM_STAMP(1);
-                    // ---- heads (VALU): lane = sample c, half h sums units [32h, 32h+32)
+                    // ---- heads on the MFMA: out[s][q] = H2[s][:] . Wh[q][:] (A = H2 from tile B as in layer 2, B =
+                    // Wh^T with the output q on the lane column, q >= Q zero), through the dO tile to lane = sample
                     float outv[Q];
+                    {
+                        f32x16 ho = f32x16{0};
+#pragma unroll 1
+                        for (int k0 = 0; k0 < H / 2; k0 += 8) {
+                            float av[8], bq[8];
 #pragma unroll
-                    for (int q = 0; q < Q; ++q) outv[q] = 0.f;
-PGM_UNROLL_W(PGM_UW_HEAD)
-                    for (int u = 0; u < TS; ++u) {
-                        const float hv = scr2[c * SCR + h * TS + u];
+                            for (int i = 0; i < 8; ++i) {
+                                const int k = 2 * (k0 + i) + h;
+                                av[i] = scr2[c * SCR + k];
+                                bq[i] = c < Q ? W.Wh[c < Q ? c : 0][k] : 0.f;
+                            }
+                            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                        for (int q = 0; q < Q; ++q) outv[q] = fmaf(hv, W.Wh[q][h * TS + u], outv[q]);
+                            for (int i = 0; i < 8; ++i) ho = mfma(av[i], bq[i], ho);
+                            __builtin_amdgcn_sched_barrier(0);
+                        }
+                        if (c < Q) {
+                            const float bias = W.bh[c];
+#pragma unroll
+                            for (int r = 0; r < 16; ++r) S.dout[w][rowof(r, h)][c] = ho[r] + bias;
+                        }
+                        wave_lds_fence();
+#pragma unroll
+                        for (int q = 0; q < Q; ++q) outv[q] = S.dout[w][c][q];
                     }
-#pragma unroll
-                    for (int q = 0; q < Q; ++q) outv[q] = half_sum(outv[q]) + W.bh[q];
                     // ---- per-sample loss gradients (ppo.py:80-96)
                     float dO[Q];
 #pragma unroll

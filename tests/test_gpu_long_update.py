@@ -1,9 +1,11 @@
 """The update launch the bench times, whole: E = 10 epochs x M = 32 minibatches = 320 Adam steps per task in ONE
 pgm_ppo_update launch (a2c_ppo_acktr/algo/ppo.py:58-115, storage.py:118-154: the perms of all ten epochs, every parity
 slot of the hand-offs cycled 160 times, the ragged parts' dummy tiles re-zeroed every step), at the per-GPU loads of
-config 1 (Walker P = 40: NS 6, R 3/3/3/3/2/2, two workgroups per CU) and config 2 (HalfCheetah P = 20: NS 8, R 2, two
-per CU), and config 4 (Humanoid P = 20, N = 8: the wide update, NS 4, 512-row minibatches, the private k-quad layer-1
-copies carried over all 320 steps and written back once, the next minibatch's rows prefetched across epoch ends).
+config 0 (Hopper-v2 P = 5, N = 1: 64-row minibatches, NS 4, R 1), config 1 (Walker P = 40: NS 6, R 3/3/3/3/2/2, two
+workgroups per CU), config 2 (HalfCheetah P = 20: NS 8, R 2, two per CU), config 3 (Hopper-v3 P = 27: three
+objectives, a partial last group of 8 tasks) and config 4 (Humanoid P = 20, N = 8: the wide update, NS 4, 512-row
+minibatches, the private k-quad layer-1 copies carried over all 320 steps and written back once, the next minibatch's
+rows prefetched across epoch ends).
 Every task against the oracle.
 
 Tolerance (drift-aware, not a loosened constant): over 320 Adam steps fp32 arithmetic drifts from the fp64 reference;
@@ -80,6 +82,8 @@ def _oracle_arm(pol, args, data, p, perms, E, M, T, N, spec, lr, dtype, pert_see
 @pytest.mark.parametrize('env,P,N,variant,chaotic', [
     ('MO-Walker2d-v2', 40, 4, 'ppo_update_fs_kernel (NS=6, R=3, 2 per CU)', False),
     ('MO-HalfCheetah-v2', 20, 4, 'ppo_update_fs_kernel (NS=8, R=2, 2 per CU)', False),
+    ('MO-Hopper-v3', 27, 4, 'ppo_update_fs_kernel (NS=8, R=2, 2 per CU)', False),
+    ('MO-Hopper-v2', 5, 1, 'ppo_update_fs_kernel (NS=4, R=1)', False),
     ('MO-Humanoid-v2', 20, 8, 'ppo_update_wide_kernel (NS=4)', True)])
 def test_full_production_update_launch(gpu, env, P, N, variant, chaotic):
     T, E, M, lr = 2048, 10, 32, 3e-4
